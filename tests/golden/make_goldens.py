@@ -1,0 +1,332 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by RUNNING THE REFERENCE (build container only).
+
+The reference (AhmedKishki/AMP-SPARC-SpatialModulation, mounted read-only at
+/root/reference) is imported flat, exactly as its own drivers import it, with
+bytecode writing disabled so nothing is written under /root/reference.  Only
+the data it produces is committed (``*.npz`` / ``*.json`` next to this file);
+no reference source travels.
+
+Seeding protocol (the reference never seeds): for every
+(config, seed S, EbN0) point, ``np.random.seed(S); torch.manual_seed(S)`` and
+then the reference's own per-epoch call order (vamp_model.py:55-61):
+``Channel.generate_as_sparc`` -> ``torch.linalg.svd`` (VAMP only) ->
+``Data.generate_message`` -> ``A @ x + Channel.awgn(SNR)`` -> detector.
+
+Groups:
+  g1  per-iteration traces at small shapes, inputs stored (VAMP, BAMP, SCAMP)
+  g2  denoiser unit vectors (scalar tau, per-element tau, SCAMP mean-only, NaN onset)
+  g3  MAP decision + all 14 metrics on crafted inputs (ties, 16QAM duplicate, NaN rows)
+  g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
+      by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
+
+Usage: python tests/golden/make_goldens.py [g1 g2 g3 g4 ...]
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+sys.dont_write_bytecode = True
+REF = os.environ.get('AMP_REFERENCE', '/root/reference')
+sys.path.insert(0, REF)
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+import numpy as np      # noqa: E402
+import torch            # noqa: E402
+
+from config import Config    # noqa: E402  (reference module)
+from channel import Channel  # noqa: E402
+from data import Data        # noqa: E402
+from loss import Loss        # noqa: E402
+import vamp as ref_vamp      # noqa: E402
+import bamp as ref_bamp      # noqa: E402
+import scamp as ref_scamp    # noqa: E402
+
+torch.set_num_threads(int(os.environ.get('GOLDEN_THREADS', '8')))
+
+
+def cfg_of(Nt, Na, Nr, B, alphabet, iterations=20, Lin=1, Lh=1):
+    return Config(Nt, Na, Nr, Lin, Lh, batch=B, generator_mode='sparc', iterations=iterations,
+                  alphabet=alphabet, channel_profile='uniform', channel_truncation='tail', device='cpu')
+
+
+def snr_of(cfg, EbN0):
+    return 10 ** ((EbN0 + 10 * np.log10(cfg.code_rate)) / 10)
+
+
+def gen_inputs(cfg, seed, EbN0, svd=True):
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    ch, da = Channel(cfg), Data(cfg)
+    W, A = ch.generate_as_sparc()
+    U = s = Vh = None
+    if svd:
+        U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+    x, sym, idx = da.generate_message()
+    SNR = snr_of(cfg, EbN0)
+    y = A @ x + ch.awgn(SNR)
+    return dict(W=W, A=A, U=U, s=s, Vh=Vh, x=x, sym=sym, idx=idx, y=y, SNR=SNR)
+
+
+def loss_to_json(loss):
+    out = {}
+    for k, v in loss.items():
+        v = np.asarray(v)
+        out[k] = float(v) if v.ndim == 0 else [float(t) for t in v.ravel()]
+    return out
+
+
+def sha(t):
+    a = t.numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def c(t):
+    """torch [B,N,1] / [n,N] -> numpy without the trailing singleton."""
+    a = t.detach().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+    if a.ndim == 3 and a.shape[-1] == 1:
+        a = a[..., 0]
+    return a.copy()
+
+
+# ---------------------------------------------------------------------------
+def g1():
+    """Per-iteration traces with stored inputs."""
+    out = {}
+    cases = []
+    for alph in ['QPSK', '16QAM']:
+        for EbN0 in [0.0, 6.0, 20.0, 30.0]:
+            for seed in [0, 1]:
+                cases.append(('vamp', alph, EbN0, seed))
+    for alph in ['QPSK']:
+        for EbN0 in [0.0, 6.0, 12.0]:
+            cases.append(('bamp', alph, EbN0, 0))
+    for alph in ['QPSK', '16QAM']:
+        for EbN0 in [2.0, 8.0]:
+            cases.append(('scamp', alph, EbN0, 0))
+    for algo, alph, EbN0, seed in cases:
+        if algo == 'vamp':
+            cfg = cfg_of(16, 2, 32, 8, alph)
+        elif algo == 'bamp':
+            cfg = cfg_of(4, 1, 8, 100, alph, iterations=10)
+        else:
+            cfg = cfg_of(32, 4, 64, 16, alph)
+        inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
+        trace = []
+        if algo == 'vamp':
+            orig = ref_vamp.VAMPLayer.forward
+
+            def hook(self, T, _o=orig):
+                _o(self, T)
+                trace.append(dict(r=c(T.r), xmmse=c(T.xmmse), var=c(T.var), r_tilde=c(T.r_tilde),
+                                  sigma2_tilde=float(T.sigma2_tilde)))
+            ref_vamp.VAMPLayer.forward = hook
+            try:
+                L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'],
+                                       inp['sym'], inp['idx'])
+            finally:
+                ref_vamp.VAMPLayer.forward = orig
+        elif algo == 'bamp':
+            orig = ref_bamp.BAMPLayer.forward
+
+            def hook(self, T, _o=orig):
+                _o(self, T)
+                trace.append(dict(xmap=c(T.xmap), xmmse=c(T.xmmse), var=c(T.var), z=c(T.z), u=c(T.u)))
+            ref_bamp.BAMPLayer.forward = hook
+            try:
+                L = ref_bamp.BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+            finally:
+                ref_bamp.BAMPLayer.forward = orig
+        else:
+            orig = ref_scamp.SCAMPLayer.forward
+
+            def hook(self, T, _o=orig):
+                _o(self, T)
+                trace.append(dict(xmap=c(T.xmap), xmmse=c(T.xmmse), psi=c(T.psi), z=c(T.z)))
+            ref_scamp.SCAMPLayer.forward = hook
+            try:
+                L = ref_scamp.SCAMP(cfg)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'],
+                                         inp['idx'])
+            finally:
+                ref_scamp.SCAMPLayer.forward = orig
+        key = f'{algo}_{alph}_{EbN0:g}_{seed}'
+        rec = dict(Nt=cfg.Nt, Na=cfg.Na, Nr=cfg.Nr, B=cfg.B, iters=cfg.N_Layers, SNR=inp['SNR'],
+                   A=c(inp['A']), W=c(inp['W']), y=c(inp['y']), x=c(inp['x']), sym=inp['sym'],
+                   idx=inp['idx'], T=len(trace), loss=json.dumps(loss_to_json(L.loss)))
+        if algo == 'vamp':
+            rec.update(U=c(inp['U']), s=c(inp['s']), Vh=c(inp['Vh']))
+        for t, tr in enumerate(trace):
+            for k, v in tr.items():
+                rec[f'it{t}_{k}'] = v
+        out[key] = rec
+        print(key, 'T=', len(trace), flush=True)
+    flat = {}
+    for key, rec in out.items():
+        for k, v in rec.items():
+            flat[f'{key}/{k}'] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, 'g1_traces.npz'), **flat)
+
+
+# ---------------------------------------------------------------------------
+def g2():
+    """Denoiser unit vectors straight from the reference denoiser methods."""
+    rng = np.random.default_rng(1234)
+    flat = {}
+    n = 0
+    for alph in ['QPSK', '16QAM', 'BPSK', 'OOK', '8PSK']:
+        for (Nt, Na, B) in [(16, 2, 8), (64, 4, 4)]:
+            cfg = cfg_of(Nt, Na, 2 * Nt, B, alph)
+            lay_v = ref_vamp.VAMPLayer(cfg)
+            lay_b = ref_bamp.BAMPLayer(cfg)
+            lay_s = ref_scamp.SCAMPLayer(cfg)
+            for tau in [1e-9, 1e-4, 1e-2, 0.1, 0.5, 2.0, 1e2]:
+                r = (rng.standard_normal((B, Nt)) + 1j * rng.standard_normal((B, Nt))).astype(np.complex64) * 0.7
+                # plant one strong entry per section so the posterior is peaked
+                sec = r.reshape(B, Na, Nt // Na)
+                pos = rng.integers(0, Nt // Na, size=(B, Na))
+                kk = rng.integers(0, cfg.K, size=(B, Na))
+                for b in range(B):
+                    for l in range(Na):
+                        sec[b, l, pos[b, l]] += cfg.symbols[kk[b, l]]
+                r = sec.reshape(B, Nt)
+                rt = torch.from_numpy(r).view(B, Nt, 1)
+                xm_v, var_v = lay_v.segmented_denoiser(rt, torch.tensor(np.float32(tau)))
+                cov = (np.abs(rng.standard_normal((B, Nt))) * 0.5 + 0.5).astype(np.float32) * np.float32(tau)
+                xm_b, var_b = lay_b.segmented_denoiser(rt, torch.from_numpy(cov).view(B, Nt, 1))
+                tau_use = np.repeat((np.abs(rng.standard_normal((B, 1))) + 0.5).astype(np.float32) * np.float32(tau),
+                                    Nt, axis=1)
+                xm_s = lay_s.denoiser(rt, torch.from_numpy(tau_use).view(B, Nt, 1))
+                key = f'case{n}'
+                flat.update({f'{key}/alphabet': np.array(alph), f'{key}/Nt': np.array(Nt),
+                             f'{key}/Na': np.array(Na), f'{key}/B': np.array(B),
+                             f'{key}/r': r, f'{key}/tau': np.array(np.float32(tau)), f'{key}/cov': cov,
+                             f'{key}/tau_use': tau_use,
+                             f'{key}/v_xmmse': c(xm_v), f'{key}/v_var': c(var_v),
+                             f'{key}/b_xmmse': c(xm_b), f'{key}/b_var': c(var_b),
+                             f'{key}/s_xmmse': c(xm_s)})
+                n += 1
+    # NaN onset: one section far above the rest at a tiny tau (float64 underflow -> 0/0).
+    for alph in ['QPSK', '16QAM']:
+        cfg = cfg_of(16, 2, 32, 4, alph)
+        lay_v = ref_vamp.VAMPLayer(cfg)
+        r = (rng.standard_normal((4, 16)) * 0.01 + 1j * rng.standard_normal((4, 16)) * 0.01).astype(np.complex64)
+        r[0, 3] = 1.0 + 1.0j
+        for tau in [1e-3, 5e-4, 1e-4]:
+            xm_v, var_v = lay_v.segmented_denoiser(torch.from_numpy(r).view(4, 16, 1), torch.tensor(np.float32(tau)))
+            key = f'case{n}'
+            flat.update({f'{key}/alphabet': np.array(alph), f'{key}/Nt': np.array(16), f'{key}/Na': np.array(2),
+                         f'{key}/B': np.array(4), f'{key}/r': r, f'{key}/tau': np.array(np.float32(tau)),
+                         f'{key}/v_xmmse': c(xm_v), f'{key}/v_var': c(var_v), f'{key}/nan_case': np.array(1)})
+            n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g2_denoiser.npz'), **flat)
+    print('g2 cases', n)
+
+
+# ---------------------------------------------------------------------------
+def g3():
+    """MAP decision + metrics on crafted inputs."""
+    rng = np.random.default_rng(99)
+    flat = {}
+    n = 0
+    for alph in ['QPSK', '16QAM', 'BPSK', '8PSK', 'OOK']:
+        for (Nt, Na, Nr, B, Lin, Lh) in [(16, 2, 32, 8, 1, 1), (32, 4, 16, 6, 3, 2)]:
+            cfg = Config(Nt, Na, Nr, Lin, Lh, batch=B, generator_mode='sparc', iterations=5, alphabet=alph,
+                         channel_profile='uniform', channel_truncation='tail', device='cpu')
+            np.random.seed(n)
+            x, sym, idx = Data(cfg).generate_message()
+            for variant in ['noisy', 'ties', 'nanrows', 'exact']:
+                xv = c(x).reshape(B, -1)
+                if variant == 'noisy':
+                    xmap = xv + (rng.standard_normal(xv.shape) + 1j * rng.standard_normal(xv.shape)).astype(np.complex64) * 0.4
+                elif variant == 'ties':
+                    xmap = np.zeros_like(xv)          # every logit equal -> first index
+                    xmap[::2] = xv[::2]
+                elif variant == 'nanrows':
+                    xmap = xv + (rng.standard_normal(xv.shape)).astype(np.complex64) * 0.2
+                    xmap[0, :] = np.nan
+                    if B > 2:
+                        xmap[2, 1] = np.nan + 0j
+                else:
+                    xmap = xv.copy()
+                xmap = xmap.astype(np.complex64)
+                xmmse = (xv + rng.standard_normal(xv.shape).astype(np.float32) * 0.1).astype(np.complex64)
+                L = Loss(cfg)
+                L(torch.from_numpy(xmap).view(B, -1, 1), torch.from_numpy(xmmse).view(B, -1, 1), x, sym, idx, 3)
+                dec = L.decision(xmap.reshape(-1, cfg.Lin, cfg.Nt))
+                key = f'case{n}'
+                flat.update({f'{key}/alphabet': np.array(alph), f'{key}/dims': np.array([Nt, Na, Nr, B, Lin, Lh]),
+                             f'{key}/xmap': xmap, f'{key}/xmmse': xmmse, f'{key}/x': c(x).reshape(B, -1),
+                             f'{key}/sym': sym, f'{key}/idx': idx,
+                             f'{key}/xhat': dec[0], f'{key}/shat': dec[1], f'{key}/ihat': dec[2],
+                             f'{key}/loss': np.array(json.dumps(loss_to_json(L.loss)))})
+                n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g3_decision.npz'), **flat)
+    print('g3 cases', n)
+
+
+# ---------------------------------------------------------------------------
+G4_CONFIGS = {
+    # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
+    'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
+    'cfg2_vamp_16qam': ('vamp', 64, 4, 128, 1024, '16QAM', 20, list(range(0, 21)), [0]),
+    'cfg2_vamp_qpsk': ('vamp', 64, 4, 128, 1024, 'QPSK', 20, list(range(0, 21)), [0, 1]),
+    'cfg3_scamp_16qam': ('scamp', 128, 8, 256, 4096, '16QAM', 20, list(range(0, 21, 2)), [0]),
+    'cfg3_scamp_qpsk': ('scamp', 128, 8, 256, 4096, 'QPSK', 20, list(range(0, 21, 2)), [0]),
+    'cfg4_vamp_16qam': ('vamp', 256, 8, 512, 4096, '16QAM', 20, list(range(0, 21)), [0]),
+    'cfg4_vamp_qpsk': ('vamp', 256, 8, 512, 4096, 'QPSK', 20, list(range(0, 21, 2)), [0]),
+}
+
+
+def g4(names=None):
+    path = os.path.join(HERE, 'g4_curves.json')
+    db = json.load(open(path)) if os.path.exists(path) else {}
+    for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
+        if names and name not in names:
+            continue
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = db.get(name, {'algo': algo, 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': B, 'alphabet': alph,
+                            'iterations': iters, 'points': {}})
+        for seed in seeds:
+            for EbN0 in grid:
+                key = f'{seed}/{EbN0}'
+                if key in ent['points']:
+                    continue
+                t0 = time.time()
+                inp = gen_inputs(cfg, seed, float(EbN0), svd=(algo == 'vamp'))
+                if algo == 'vamp':
+                    L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'],
+                                           inp['sym'], inp['idx'])
+                elif algo == 'bamp':
+                    L = ref_bamp.BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                else:
+                    L = ref_scamp.SCAMP(cfg)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'],
+                                             inp['idx'])
+                rec = loss_to_json(L.loss)
+                rec['sha_A'] = sha(inp['A'])
+                rec['sha_x'] = sha(inp['x'])
+                rec['sha_sym'] = sha(np.asarray(inp['sym'], dtype=np.int64))
+                rec['y_abs2_sum'] = float(np.sum(np.abs(inp['y'].numpy().astype(np.complex128)) ** 2))
+                ent['points'][key] = rec
+                print(name, key, 'T=', rec['T'], 'ver=', rec['ver'], 'ser=', rec['ser'],
+                      f'{time.time() - t0:.1f}s', flush=True)
+                db[name] = ent
+                with open(path, 'w') as f:
+                    json.dump(db, f, indent=1, sort_keys=True)
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4']
+    names = [w for w in which if w.startswith('cfg')]
+    for w in which:
+        if w == 'g1':
+            g1()
+        elif w == 'g2':
+            g2()
+        elif w == 'g3':
+            g3()
+        elif w == 'g4':
+            g4(names or None)
