@@ -1,0 +1,175 @@
+"""ctypes binding of the gfx950 C-ABI library ``lib/libampsparc.so`` (include/amp_sparc.h).
+
+The product path has no fallback: if the library is missing, or a tensor handed to it
+is not a ROCm device tensor, the call raises.  ``build()`` compiles it in-tree with hipcc.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import torch   # noqa: F401  (loads torch's HIP runtime first: one runtime per process)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+LIB_PATH = os.path.join(HERE, 'lib', 'libampsparc.so')
+
+AMP_MAX_K = 16
+
+
+class AmpConstellation(C.Structure):
+    _fields_ = [('K', C.c_int32), ('symbol_bits', C.c_int32),
+                ('re', C.c_float * AMP_MAX_K), ('im', C.c_float * AMP_MAX_K),
+                ('re64', C.c_double * AMP_MAX_K), ('im64', C.c_double * AMP_MAX_K),
+                ('gray', C.c_int32 * AMP_MAX_K)]
+
+
+class AmpDims(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ('B', 'Nt', 'Na', 'Nr', 'Lin', 'Lout', 'N', 'n', 'L', 'M')]
+
+
+class AmpStatus(C.Structure):
+    _fields_ = [('T', C.c_int32), ('nan_state', C.c_int32), ('stopped', C.c_int32), ('pad', C.c_int32),
+                ('last_scalar', C.c_float * 4)]
+
+
+class AmpCounts(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ('ier', 'ser', 'iber', 'sber', 'ver', 'verf', 'verm', 'verL', 'fer')] + \
+               [(n, C.c_double) for n in ('mse', 'msef', 'msem', 'mseL')]
+
+
+class AmpVampArgs(C.Structure):
+    _fields_ = [('U', C.c_void_p), ('s', C.c_void_p), ('Vh', C.c_void_p), ('y', C.c_void_p),
+                ('k', C.c_int32), ('max_iter', C.c_int32), ('noise_var', C.c_double), ('sparsity', C.c_double),
+                ('r', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p), ('status', C.c_void_p),
+                ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
+
+
+class AmpBampArgs(C.Structure):
+    _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('pad', C.c_int32),
+                ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p),
+                ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
+
+
+class AmpScampArgs(C.Structure):
+    _fields_ = [('W', C.c_void_p), ('A', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32),
+                ('pad', C.c_int32), ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p),
+                ('psi', C.c_void_p), ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
+
+
+_P = C.c_void_p
+_I = C.c_int32
+_D = C.POINTER(AmpDims)
+_K = C.POINTER(AmpConstellation)
+
+# name -> (restype, argtypes); mirrors include/amp_sparc.h
+SIGNATURES = {
+    'amp_vamp_workspace_bytes': (C.c_size_t, [_D, _I, _I]),
+    'amp_vamp_run': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
+    'amp_vamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
+    'amp_vamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
+    'amp_vamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
+    'amp_vamp_profile': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(C.c_float), _P]),
+    'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
+    'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
+    'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),
+    'amp_scamp_run': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
+    'amp_block_denoise': (C.c_int, [_D, _K, _P, _I, C.c_float, _P, _P, _P, _P, C.c_size_t, _P]),
+    'amp_block_denoise_workspace_bytes': (C.c_size_t, [_D]),
+    'amp_map_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
+    'amp_map_decide_workspace_bytes': (C.c_size_t, [_D]),
+    'amp_gemm_nt_f32': (C.c_int, [_P, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P]),
+    'amp_build_cweight': (C.c_int, [_P, C.c_int64, C.c_int64, _I, _P, _I, _I, _P, _I, _I, _P]),
+    'amp_last_error': (C.c_char_p, []),
+    'amp_build_info': (C.c_char_p, []),
+}
+
+_lib = None
+
+
+class AmpError(RuntimeError):
+    """A non-zero status from the C ABI (bad argument, workspace, launch failure)."""
+
+
+def build(verbose: bool = False) -> str:
+    """Compile csrc/*.hip for gfx950 into lib/libampsparc.so (hipcc, in-tree)."""
+    jobs = str(min(8, os.cpu_count() or 1))
+    out = subprocess.run(['make', '-C', CSRC, '-j', jobs], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError('HIP build failed:\n' + out.stdout[-4000:] + out.stderr[-4000:])
+    if verbose:
+        print(out.stdout)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'{LIB_PATH} not found: run __graft_entry__.build() (HIP extension missing; '
+                               'there is no CPU fallback)')
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise AmpError(f'{what} failed ({rc}): {lib().amp_last_error().decode()}')
+
+
+def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
+    """Device pointer of a contiguous ROCm tensor (no copies, no CPU fallback)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f'{name}: expected a torch.Tensor, got {type(t).__name__}')
+    if t.device.type != 'cuda':
+        raise ValueError(f'{name}: the HIP path needs a ROCm device tensor (got {t.device}); '
+                         'there is no CPU fallback')
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f'{name}: expected {dtype}, got {t.dtype}')
+    if not t.is_contiguous():
+        raise ValueError(f'{name}: must be contiguous')
+    return t.data_ptr()
+
+
+def stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def make_constellation(symbols: np.ndarray, gray, symbol_bits: int) -> AmpConstellation:
+    sym = np.asarray(symbols).astype(np.complex128)
+    c = AmpConstellation()
+    c.K = len(sym)
+    c.symbol_bits = int(symbol_bits)
+    for i, a in enumerate(sym):
+        c.re[i] = float(np.float32(a.real))
+        c.im[i] = float(np.float32(a.imag))
+        c.re64[i] = float(a.real)
+        c.im64[i] = float(a.imag)
+        c.gray[i] = int(gray[i])
+    return c
+
+
+class Workspace:
+    """Cached device workspace per (device, purpose, size)."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, device, key, nbytes: int) -> torch.Tensor:
+        k = (str(device), key)
+        b = self._bufs.get(k)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self._bufs[k] = b
+        return b
+
+
+WORKSPACE = Workspace()

@@ -1,0 +1,197 @@
+// amp_common.h — shared device-side definitions for the gfx950 AMP kernels.
+//
+// Numerical conventions: kernels are compiled with
+// -ffp-contract=off so every elementwise step rounds exactly where the
+// reference's torch op rounds; FMAs appear only where written explicitly.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "../../include/amp_sparc.h"
+
+#define AMP_WAVE 64
+#define AMP_WG 256
+
+// float64 exp(x) underflows to exactly 0 for x < ln(2^-1075): the reference's
+// section softmax exp(xi - max|xi|) (vamp.py:112) is 0/0 = NaN for a section
+// whose every logit lies further than this below the batch-global max.
+#define AMP_F64_EXP_UNDERFLOW (-745.13321910194122)
+
+// vamp.py:51-54 (float32 0-dim tensors)
+#define AMP_VAR_RATIO_MIN 1.0e-5f
+#define AMP_VAR_MIN 1.0e-9f
+#define AMP_VAR_MAX 1.0e5f
+
+namespace amp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Per-workgroup partial results of one detector iteration.  The next kernel on
+// the stream reduces them (kernel boundary = visibility), so no atomics and a
+// fixed summation order: every workgroup that reduces them gets identical bits.
+struct alignas(16) Partial {
+    double sumvar;     // sum of var (float64), NaN-propagating
+    double maxabs;     // max |xi| over the block, xi in float64 like the reference (vamp.py:112)
+    double minsecmax;  // min over sections of the section max logit (float64)
+    uint32_t notclose; // elements failing torch.allclose(var_new, var_prev)
+    uint32_t pad;
+};
+
+// Device-resident scalar state of one VAMP iteration (vamp.py:66-94).
+struct alignas(16) VampIter {
+    int32_t stopped;   // 1: the loop already broke (vamp.py:185-186); iteration is a no-op
+    int32_t T;         // executed iterations once stopped
+    int32_t fixed;     // sections of the previous iteration recomputed in exact float64
+    int32_t pad0;
+    float vr;          // var_ratio = noise_var / sigma2_tilde       (vamp.py:66)
+    float alpha;       // clamped alpha                              (vamp.py:75-77)
+    float inv1ma;      // 1 / (1 - alpha) (c64 / f32 == mul by recip) (vamp.py:79)
+    float sigma2;      // clamped sigma2                             (vamp.py:80-82)
+    float inv_sigma2;  // 1 / sigma2 (denoiser s / tau)              (vamp.py:111)
+    float dxdr_prev;   // dxdr of iteration t-1 (0 at t = 0)         (vamp.py:85-87)
+    float ns_prev;     // normScalar of iteration t-1 (1 at t = 0)   (vamp.py:89)
+    float s2t;         // sigma2_tilde entering iteration t
+    float pad1[3];
+    double G;          // previous iteration's max|xi|
+};
+
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ---- NaN-propagating min/max with torch.maximum / torch.minimum semantics ----
+__device__ __forceinline__ float nan_max(float a, float b) { return (a != a || b != b) ? (a + b) : (a > b ? a : b); }
+__device__ __forceinline__ float nan_min(float a, float b) { return (a != a || b != b) ? (a + b) : (a < b ? a : b); }
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || b != b) ? (a + b) : (a > b ? a : b); }
+__device__ __forceinline__ double nan_min(double a, double b) { return (a != a || b != b) ? (a + b) : (a < b ? a : b); }
+__device__ __forceinline__ float clampf_t(float v, float lo, float hi) { return nan_min(nan_max(v, lo), hi); }
+
+// torch.isclose(a, b, rtol=1e-5, atol=1e-8) in float32, no FMA contraction.
+__device__ __forceinline__ bool torch_close(float a, float b) {
+    if (a == b) return true;
+    float actual = fabsf(__fsub_rn(a, b));
+    float allowed = __fadd_rn(1.0e-8f, fabsf(__fmul_rn(1.0e-5f, b)));
+    return isfinite(actual) && actual <= allowed;
+}
+
+// ---- reductions within aligned groups of G lanes (G power of two <= 64) ----
+template <typename T>
+__device__ __forceinline__ T group_max(T v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = v > w ? v : w; }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T group_min(T v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = v < w ? v : w; }
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T group_sum(T v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+// NaN-sticky variants (a NaN anywhere in the group wins)
+__device__ __forceinline__ float group_max_nan(float v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float group_min_nan(float v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) v = nan_min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double group_max_nan(double v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double group_min_nan(double v, int G) {
+    for (int o = G >> 1; o > 0; o >>= 1) v = nan_min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---- workgroup-level reduction of a Partial (256 threads) ----
+// Each thread contributes its own values; thread 0 returns the block result.
+struct PartAcc {
+    double sumvar = 0.0;
+    double maxabs = 0.0;         // |xi| >= 0
+    double minsecmax = INFINITY;
+    uint32_t notclose = 0;
+};
+
+__device__ __forceinline__ void part_wave_reduce(PartAcc& p) {
+    p.sumvar = group_sum(p.sumvar, 64);
+    p.maxabs = group_max_nan(p.maxabs, 64);
+    p.minsecmax = group_min_nan(p.minsecmax, 64);
+    p.notclose = group_sum(p.notclose, 64);
+}
+
+// Reduces across the 4 waves through LDS scratch (>= 4*32 bytes) and stores the
+// block partial from thread 0.
+__device__ __forceinline__ void part_block_store(PartAcc p, Partial* dst, void* lds_scratch) {
+    part_wave_reduce(p);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    __syncthreads();
+    if (lane == 0) {
+        s[wave].sumvar = p.sumvar; s[wave].maxabs = p.maxabs;
+        s[wave].minsecmax = p.minsecmax; s[wave].notclose = p.notclose;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial o;
+        o.sumvar = s[0].sumvar; o.maxabs = s[0].maxabs; o.minsecmax = s[0].minsecmax; o.notclose = s[0].notclose;
+        for (int w = 1; w < AMP_WG / 64; ++w) {
+            o.sumvar += s[w].sumvar; o.maxabs = nan_max(o.maxabs, s[w].maxabs);
+            o.minsecmax = nan_min(o.minsecmax, s[w].minsecmax); o.notclose += s[w].notclose;
+        }
+        o.pad = 0;
+        *dst = o;
+    }
+    __syncthreads();
+}
+
+// Deterministic reduction of nblk partials by one workgroup (every caller gets
+// the same bits: fixed per-thread strides, fixed tree).
+__device__ __forceinline__ PartAcc part_reduce_all(const Partial* src, int nblk, void* lds_scratch) {
+    PartAcc p;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+        Partial q = src[i];
+        p.sumvar += q.sumvar; p.maxabs = nan_max(p.maxabs, q.maxabs);
+        p.minsecmax = nan_min(p.minsecmax, q.minsecmax); p.notclose += q.notclose;
+    }
+    part_wave_reduce(p);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    __syncthreads();
+    if (lane == 0) {
+        s[wave].sumvar = p.sumvar; s[wave].maxabs = p.maxabs;
+        s[wave].minsecmax = p.minsecmax; s[wave].notclose = p.notclose;
+    }
+    __syncthreads();
+    PartAcc o;
+    o.sumvar = s[0].sumvar; o.maxabs = s[0].maxabs; o.minsecmax = s[0].minsecmax; o.notclose = s[0].notclose;
+    for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
+        o.sumvar += s[w].sumvar; o.maxabs = nan_max(o.maxabs, s[w].maxabs);
+        o.minsecmax = nan_min(o.minsecmax, s[w].minsecmax); o.notclose += s[w].notclose;
+    }
+    __syncthreads();
+    return o;
+}
+
+// A section whose max logit lies more than |AMP_DANGER| below the batch max|xi| leaves the
+// normal float64 range in the reference's softmax exp(xi - max|xi|) (vamp.py:112): its
+// normaliser Z is denormal or zero, so c128 / Z (= * (1/Z)) overflows to inf/NaN, and for
+// real alphabets the true division is denormal-quantised or 0/0.  Such sections are
+// recomputed with the reference's exact float64 arithmetic (exact_section_f64).
+#define AMP_DANGER (-700.0)
+__device__ __forceinline__ bool part_danger(const PartAcc& p) { return p.minsecmax - p.maxabs < AMP_DANGER; }
+
+struct Const {
+    int K;
+    int real_alpha;    // OOK / BPSK / 4ASK: float64 symbols in the reference (config.py:117)
+    float re[AMP_MAX_K], im[AMP_MAX_K];
+    double re64[AMP_MAX_K], im64[AMP_MAX_K];
+};
+
+}  // namespace amp

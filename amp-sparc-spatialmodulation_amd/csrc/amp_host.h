@@ -1,0 +1,82 @@
+// amp_host.h — host-side helpers shared by the C entry points.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+
+#include "amp_common.h"
+
+namespace amp {
+
+void set_error(const char* fmt, ...);
+
+#define AMP_REQUIRE(cond, ...)                      \
+    do {                                            \
+        if (!(cond)) {                              \
+            ::amp::set_error(__VA_ARGS__);          \
+            return AMP_E_ARG;                       \
+        }                                           \
+    } while (0)
+
+#define AMP_LAUNCH_CHECK(what)                                                          \
+    do {                                                                                \
+        hipError_t e_ = hipGetLastError();                                              \
+        if (e_ != hipSuccess) {                                                         \
+            ::amp::set_error("%s: %s", what, hipGetErrorString(e_));                    \
+            return AMP_E_LAUNCH;                                                        \
+        }                                                                               \
+    } while (0)
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// Bump allocator used twice: once with base == nullptr to size the workspace, once to carve it.
+struct Carve {
+    char* base;
+    size_t off = 0;
+    explicit Carve(void* b) : base((char*)b) {}
+    template <typename T>
+    T* take(size_t count) {
+        off = align_up(off, 256);
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+inline Const to_const(const amp_constellation* c) {
+    Const k;
+    k.K = c->K;
+    k.real_alpha = 1;
+    for (int i = 0; i < AMP_MAX_K; ++i) {
+        const bool v = i < c->K;
+        k.re[i] = v ? c->re[i] : 0.f;
+        k.im[i] = v ? c->im[i] : 0.f;
+        k.re64[i] = v ? c->re64[i] : 0.0;
+        k.im64[i] = v ? c->im64[i] : 0.0;
+        if (v && c->im64[i] != 0.0) k.real_alpha = 0;
+    }
+    return k;
+}
+
+int check_dims(const amp_dims* d, const amp_constellation* c);
+
+// Column tile width of the section-fused GEMMs: a multiple of 2M so no section straddles
+// two workgroups.
+inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
+
+// Expanded-weight builders (amp_weights.hip)
+int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J,
+                  float* wt, int kap, int ncp, hipStream_t st);
+int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
+                      hipStream_t st);
+template <int BN>
+int set_lds_attr(const void* fn);
+int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,
+               int nc, hipStream_t st);
+
+}  // namespace amp

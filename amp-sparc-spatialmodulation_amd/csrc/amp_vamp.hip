@@ -1,0 +1,528 @@
+// amp_vamp.hip — VAMP (SVD form) detector, device-resident iteration loop.
+//
+// Restates VAMP.forward (vamp.py:159-187): Tracker (vamp.py:12-28), T x
+// VAMPLayer.forward (vamp.py:56-94), the allclose early exit (vamp.py:185).
+//
+// Per iteration t, three launches on one stream, no host synchronisation:
+//   vamp_k1<t>  GEMM1  q = Vh r~ with r~ = (xmmse - dxdr r) ns formed in the A-operand
+//               prologue (vamp.py:89-91, 67), LMMSE epilogue w = scale (y~ + vr q) - q
+//               (vamp.py:68-72).
+//   vamp_k2<t>  GEMM2  V w, epilogue x~ = Vw + r~, r = (x~ - alpha r~)/(1 - alpha)
+//               (vamp.py:72-79), then the section denoiser on the LDS tile (vamp.py:84,
+//               96-119) -> xmmse, var, per-section max logit, workgroup partials.
+//   vamp_r<t>   one workgroup: reduce the partials (sum var, max|xi|, allclose count);
+//               recompute in exact float64 the rare sections whose reference softmax
+//               leaves the normal range (amp_denoise.h, exact_section_f64); then the batch
+//               scalars of iteration t+1 (vamp.py:85-94, 66-82) or the stop record
+//               (vamp.py:185-186).  Later iterations of a stopped loop are no-ops.
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "amp_denoise.h"
+#include "amp_gemm.h"
+#include "amp_host.h"
+
+namespace amp {
+
+constexpr int RWG = 1024;   // threads of the reduction / fix-up workgroup
+
+struct VampK {
+    int B, N, n, k, L, M;
+    int kap0, ncp0, kap1, ncp1, kap2, ncp2, bn2;
+    int nblk2, max_iter;
+    double noise_var, sparsity;
+    const float* Wt0;
+    const float* Wt1;
+    const float* Wt2;
+    const float* s;     // singular values (f32 [k])
+    float* s2;          // s**2 (vamp.py:17)
+    float* ytil;        // [B][2k]
+    float* w;           // [B][2k]
+    float* r;           // [B][2N]  (caller's r)
+    float* xm;          // [B][2N]  (caller's xmmse)
+    float* var0;        // [B][N] caller's var: var of even iterations
+    float* var1;        // [B][N] workspace:    var of odd iterations
+    double* secmax;     // [2][B*L]
+    Partial* parts;     // [max_iter][nblk2]
+    VampIter* iters;    // [max_iter + 1]: iters[t] drives iteration t
+    amp_status* status;
+    Const c;
+};
+
+struct VampWs {
+    float *Wt0, *Wt1, *Wt2, *s2, *ytil, *w, *var1;
+    double* secmax;
+    Partial* parts;
+    VampIter* iters;
+    size_t bytes;
+};
+
+static void vamp_geometry(const amp_dims* d, int k, VampK& P) {
+    P.B = d->B; P.N = d->N; P.n = d->n; P.k = k; P.L = d->L; P.M = d->M;
+    P.kap0 = round_up(2 * d->n, GBK); P.ncp0 = round_up(2 * k, 128);
+    P.kap1 = round_up(2 * d->N, GBK); P.ncp1 = round_up(2 * k, 128);
+    P.bn2 = section_bn(d);
+    P.kap2 = round_up(2 * k, GBK); P.ncp2 = round_up(2 * d->N, P.bn2);
+    P.nblk2 = cdiv(d->B, GBM) * (P.ncp2 / P.bn2);
+}
+
+static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
+    VampK P;
+    vamp_geometry(d, k, P);
+    Carve cv(base);
+    VampWs w;
+    w.Wt0 = cv.take<float>((size_t)P.ncp0 * P.kap0);
+    w.Wt1 = cv.take<float>((size_t)P.ncp1 * P.kap1);
+    w.Wt2 = cv.take<float>((size_t)P.ncp2 * P.kap2);
+    w.s2 = cv.take<float>((size_t)k);
+    w.ytil = cv.take<float>((size_t)d->B * 2 * k);
+    w.w = cv.take<float>((size_t)d->B * 2 * k);
+    w.var1 = cv.take<float>((size_t)d->B * d->N);
+    w.secmax = cv.take<double>((size_t)2 * d->B * d->L);
+    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
+    w.iters = cv.take<VampIter>((size_t)max_iter + 1);
+    w.bytes = cv.off;
+    return w;
+}
+
+__device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1) ? P.var1 : P.var0; }
+
+// ---------------------------------------------------------------------------
+// Batch scalars of iteration t (vamp.py:66-82) from sigma2_tilde; t == 0 uses the
+// Tracker's Python-float sigma2_tilde (vamp.py:26).  Called by one workgroup.
+// ---------------------------------------------------------------------------
+__device__ void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
+    const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
+    double ss = 0.0;
+    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s2[i] + vr));  // vamp.py:68
+    ss = group_sum(ss, 64);
+    double* sl = reinterpret_cast<double*>(lds);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sl[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    ss = 0.0;
+    for (int w = 0; w < (int)(blockDim.x / 64); ++w) ss += sl[w];
+    __syncthreads();
+    const float varL = (float)(ss / (double)P.k) * (float)P.noise_var;                         // vamp.py:71
+    const double eta = (double)P.k / (double)P.N;                                              // vamp.py:28
+    float xtv, s2t32;
+    if (first) {
+        xtv = (float)eta * varL + (float)((1.0 - eta) * s2t64);                                // vamp.py:73
+        s2t32 = (float)s2t64;
+    } else {
+        xtv = (float)eta * varL + (float)(1.0 - eta) * s2t;
+        s2t32 = s2t;
+    }
+    const float alpha = clampf_t(xtv / s2t32, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);    // vamp.py:75-77
+    const float sigma2 = clampf_t((alpha / (1.0f - alpha)) * s2t32, AMP_VAR_MIN, AMP_VAR_MAX);  // vamp.py:80-82
+    it.vr = vr;
+    it.alpha = alpha;
+    it.inv1ma = 1.0f / (1.0f - alpha);
+    it.sigma2 = sigma2;
+    it.inv_sigma2 = 1.0f / sigma2;
+    it.s2t = s2t32;
+}
+
+__global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
+    __shared__ __attribute__((aligned(16))) float lds[64];
+    VampIter it;
+    it.stopped = 0; it.T = 0; it.fixed = 0; it.pad0 = 0; it.G = 0.0;
+    it.pad1[0] = it.pad1[1] = it.pad1[2] = 0.f;
+    it.dxdr_prev = 0.f;   // r~ = (xmmse - 0 * r) * 1 = sparsity at t = 0 (vamp.py:25)
+    it.ns_prev = 1.f;
+    const double p = P.sparsity;
+    vamp_lmmse_scalars(P, true, p * p * (1 - p) + (1 - p) * (1 - p) * p, 0.f, lds, it);   // vamp.py:26
+    if (threadIdx.x == 0) P.iters[0] = it;
+}
+
+// r~ = (xmmse - dxdr * r) * normScalar (vamp.py:91), formed while loading GEMM1's A tile.
+struct ALoadRt {
+    const float* __restrict__ xm;
+    const float* __restrict__ r;
+    int lda, rows, ka;
+    float dxdr, ns;
+    __device__ __forceinline__ float4 operator()(int row, int k) const {
+        if (row >= rows || k >= ka) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const size_t o = (size_t)row * lda + k;
+        const float4 x = *reinterpret_cast<const float4*>(xm + o);
+        const float4 q = *reinterpret_cast<const float4*>(r + o);
+        return make_float4((x.x - dxdr * q.x) * ns, (x.y - dxdr * q.y) * ns, (x.z - dxdr * q.z) * ns,
+                           (x.w - dxdr * q.w) * ns);
+    }
+};
+
+__global__ __launch_bounds__(AMP_WG) void vamp_k1(VampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const VampIter it = P.iters[t];
+    if (it.stopped) return;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const int twoN = 2 * P.N, twok = 2 * P.k;
+    gemm_tile<128>(ALoadRt{P.xm, P.r, twoN, P.B, twoN, it.dxdr_prev, it.ns_prev}, P.Wt1, P.kap1, row0, col0, lds);
+    using C = GemmCfg<128>;
+    // w = scale * (y~ + vr * q) - q   (vamp.py:68-72; `x_tilde - q` is what V @ consumes)
+    for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
+        const int rho = e >> 7, cc = e & 127;
+        const int row = row0 + rho, col = col0 + cc;
+        if (row < P.B && col < twok) {
+            const float q = lds[rho * C::LDC + cc];
+            const float sc = 1.0f / (P.s2[col >> 1] + it.vr);
+            const size_t o = (size_t)row * twok + col;
+            P.w[o] = sc * (P.ytil[o] + it.vr * q) - q;
+        }
+    }
+}
+
+struct VampDenoisePolicy {
+    const float* tile;
+    int ldc, spr, M, N, L, row0, colc0;
+    float inv_sigma2;
+    float* xm;
+    float* var_new;
+    const float* var_prev;
+    double* secmax;
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * (sj * M + m));
+        rr = v.x; ri = v.y; it = inv_sigma2;
+    }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const size_t o = (size_t)(row0 + rho) * N + colc0 + sj * M + m;
+        *reinterpret_cast<float2*>(xm + 2 * o) = make_float2(xr, xi);
+        var_new[o] = var;
+        pa.sumvar += (double)var;
+        pa.notclose += torch_close(var, var_prev[o]) ? 0u : 1u;     // vamp.py:185
+    }
+    __device__ __forceinline__ void section(int sec, double smax) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+    }
+};
+
+template <int BN>
+__global__ __launch_bounds__(AMP_WG) void vamp_k2(VampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const VampIter it = P.iters[t];
+    if (it.stopped) return;
+    using C = GemmCfg<BN>;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const int twoN = 2 * P.N, twok = 2 * P.k;
+    gemm_tile<BN>(ALoadPlain{P.w, twok, P.B, twok}, P.Wt2, P.kap2, row0, col0, lds);
+    // x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
+    const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
+    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
+        const int rho = e / BN, cc = e % BN;
+        if (rho < nrows && cc < ncols) {
+            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+            const float rt = (P.xm[o] - it.dxdr_prev * P.r[o]) * it.ns_prev;
+            const float xt = lds[rho * C::LDC + cc] + rt;
+            const float rn = (xt - it.alpha * rt) * it.inv1ma;
+            P.r[o] = rn;
+            lds[rho * C::LDC + cc] = rn;
+        }
+    }
+    __syncthreads();
+    VampDenoisePolicy pol;
+    pol.tile = lds; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.L = P.L;
+    pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2;
+    pol.inv_sigma2 = it.inv_sigma2;
+    pol.xm = P.xm;
+    pol.var_new = var_buf(P, t);
+    pol.var_prev = var_buf(P, t + 1);
+    pol.secmax = P.secmax + (size_t)(t & 1) * P.B * P.L;
+    PartAcc pa;
+    denoise_sections<true>(pol, nrows * pol.spr, P.M, P.c, pa);
+    part_block_store(pa, P.parts + (size_t)t * P.nblk2 + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
+}
+
+// One workgroup after K2(t): partial reduction, exact float64 fix-up of out-of-range
+// sections, allclose decision and the scalars of iteration t+1.
+__global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    __shared__ double s_fix[RWG / 64];
+    __shared__ unsigned s_nc[RWG / 64];
+    __shared__ int s_cnt[RWG / 64];
+    const VampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) P.iters[t + 1] = cur;
+        return;
+    }
+    PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk2, P.nblk2, lds);
+    int fixed = 0;
+    if (part_danger(pa)) {
+        // exact float64 recompute of every section below the danger line (rare)
+        const double G = pa.maxabs;
+        const double* sm = P.secmax + (size_t)(t & 1) * P.B * P.L;
+        float* vn = var_buf(P, t);
+        const float* vp = var_buf(P, t + 1);
+        double dsum = 0.0;
+        int dnc = 0, cnt = 0;
+        for (int s = threadIdx.x; s < P.B * P.L; s += blockDim.x) {
+            if (!(sm[s] - G < AMP_DANGER)) continue;
+            ++cnt;
+            const size_t o0 = (size_t)s * P.M;
+            const float inv = cur.inv_sigma2;
+            auto ld = [&](int m, float& rr, float& ri, float& it) {
+                const float2 v = reinterpret_cast<const float2*>(P.r)[o0 + m];
+                rr = v.x; ri = v.y; it = inv;
+            };
+            auto st = [&](int m, float xr, float xi, float var) {
+                const size_t o = o0 + m;
+                const float old = vn[o];
+                dsum += (double)var - (double)old;
+                dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(old, vp[o]) ? 0 : 1);
+                reinterpret_cast<float2*>(P.xm)[o] = make_float2(xr, xi);
+                vn[o] = var;
+            };
+            exact_section_f64<true>(ld, st, P.M, P.c, G);
+        }
+        dsum = group_sum(dsum, 64);
+        dnc = group_sum(dnc, 64);
+        cnt = group_sum(cnt, 64);
+        if ((threadIdx.x & 63) == 0) {
+            s_fix[threadIdx.x >> 6] = dsum;
+            s_nc[threadIdx.x >> 6] = (unsigned)dnc;
+            s_cnt[threadIdx.x >> 6] = cnt;
+        }
+        __syncthreads();
+        double d = 0.0;
+        unsigned nc = 0;
+        for (int w = 0; w < RWG / 64; ++w) { d += s_fix[w]; nc += s_nc[w]; fixed += s_cnt[w]; }
+        // the recomputed values replace the fast-path ones: (sum - old) + new, in float64
+        pa.sumvar += d;
+        pa.notclose += nc;
+        __syncthreads();
+    }
+    VampIter nx;
+    nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.pad0 = 0; nx.G = pa.maxabs;
+    nx.pad1[0] = nx.pad1[1] = nx.pad1[2] = 0.f;
+    if (pa.notclose == 0) {                                              // vamp.py:185-186
+        nx = cur;
+        nx.stopped = 1;
+        nx.T = t + 1;
+        nx.fixed = fixed;
+    } else {
+        // var.mean() (vamp.py:85): float64 sum of the float32 values, NaN / inf propagate
+        const float mean = (float)(pa.sumvar / ((double)P.B * (double)P.N));
+        const float dxdr = clampf_t(mean / cur.sigma2, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);  // vamp.py:85-87
+        const float ns = 1.0f / (1.0f - dxdr);                                                        // vamp.py:89
+        const float s2t = clampf_t((cur.sigma2 * dxdr) * ns, AMP_VAR_MIN, AMP_VAR_MAX);              // vamp.py:92-94
+        nx.dxdr_prev = dxdr;
+        nx.ns_prev = ns;
+        vamp_lmmse_scalars(P, false, 0.0, s2t, lds, nx);
+    }
+    if (threadIdx.x == 0) {
+        P.iters[t + 1] = nx;
+        if (nx.stopped || t + 1 == P.max_iter) {
+            amp_status s;
+            s.T = nx.stopped ? nx.T : P.max_iter;
+            s.nan_state = fixed > 0 ? 1 : 0;
+            s.stopped = nx.stopped;
+            s.pad = 0;
+            s.last_scalar[0] = cur.s2t; s.last_scalar[1] = cur.alpha; s.last_scalar[2] = cur.sigma2;
+            s.last_scalar[3] = nx.stopped ? cur.dxdr_prev : nx.dxdr_prev;
+            *P.status = s;
+        }
+    }
+}
+
+__global__ void vamp_init_kernel(VampK P) {
+    // Tracker (vamp.py:22-26) in the form the fused kernels consume:
+    //   xmmse = p, r = 0 so that r~ = (xmmse - 0*r)*1 = p   (vamp.py:25)
+    //   var buffer 1 = ones: the `prev` of iteration 0      (vamp.py:24, 182)
+    const float p = (float)P.sparsity;
+    const size_t BN_ = (size_t)P.B * P.N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < BN_; e += (size_t)gridDim.x * blockDim.x) {
+        reinterpret_cast<float2*>(P.xm)[e] = make_float2(p, 0.f);
+        reinterpret_cast<float2*>(P.r)[e] = make_float2(0.f, 0.f);
+        P.var1[e] = 1.0f;
+    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < P.k; i += gridDim.x * blockDim.x) P.s2[i] = P.s[i] * P.s[i];
+}
+
+// The last executed iteration wrote var into buffer (T-1)&1; buffer 0 is the caller's.
+__global__ void vamp_output_kernel(VampK P) {
+    const int T = P.status->T;
+    if (((T - 1) & 1) == 0) return;
+    const size_t BN_ = (size_t)P.B * P.N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < BN_; e += (size_t)gridDim.x * blockDim.x)
+        P.var0[e] = P.var1[e];
+}
+
+static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P) {
+    int rc = check_dims(d, c);
+    if (rc) return rc;
+    AMP_REQUIRE(a && a->U && a->s && a->Vh && a->y && a->r && a->xmmse && a->var && a->status && a->ws,
+                "amp_vamp: null pointer argument");
+    AMP_REQUIRE(a->k > 0 && a->k <= d->N && a->k <= d->n && a->k % 2 == 0, "amp_vamp: k = %d must be min(n, N), even",
+                a->k);
+    AMP_REQUIRE(a->max_iter > 0, "amp_vamp: max_iter must be positive");
+    const VampWs w = vamp_carve(d, a->k, a->max_iter, a->ws);
+    AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_vamp: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
+    vamp_geometry(d, a->k, P);
+    P.max_iter = a->max_iter;
+    P.noise_var = a->noise_var;
+    P.sparsity = a->sparsity;
+    P.Wt0 = w.Wt0; P.Wt1 = w.Wt1; P.Wt2 = w.Wt2;
+    P.s = (const float*)a->s; P.s2 = w.s2; P.ytil = w.ytil; P.w = w.w;
+    P.r = (float*)a->r; P.xm = (float*)a->xmmse;
+    P.var0 = (float*)a->var;
+    P.var1 = w.var1;
+    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.c = to_const(c);
+    return AMP_OK;
+}
+
+static std::once_flag g_vamp_attr_once;
+static int g_vamp_attr_rc = 0;
+
+static int vamp_attrs() {
+    std::call_once(g_vamp_attr_once, [] {
+        g_vamp_attr_rc = set_lds_attr<128>((const void*)vamp_k1);
+        if (!g_vamp_attr_rc) g_vamp_attr_rc = set_lds_attr<128>((const void*)vamp_k2<128>);
+        if (!g_vamp_attr_rc) g_vamp_attr_rc = set_lds_attr<256>((const void*)vamp_k2<256>);
+    });
+    return g_vamp_attr_rc;
+}
+
+
+static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t st) {
+    int rc = vamp_attrs();
+    if (rc) return rc;
+    // Wt0: y~ = (s * U^H) y        (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
+    rc = build_cweight((const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, st);
+    if (rc) return rc;
+    // Wt1: q = Vh r~               (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
+    rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wt1, P.kap1, P.ncp1, st);
+    if (rc) return rc;
+    // Wt2: V (x~ - q), V = Vh^H    (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
+    rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wt2, P.kap2, P.ncp2, st);
+    if (rc) return rc;
+    const int g = (int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048);
+    hipLaunchKernelGGL(vamp_init_kernel, dim3(g), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("vamp_init");
+    hipLaunchKernelGGL(vamp_init_scalars, dim3(1), dim3(RWG), 0, st, P);
+    AMP_LAUNCH_CHECK("vamp_init_scalars");
+    // y~ = (s * U^H) y as a GEMM over the batch
+    return gemm_store((const float*)a->y, 2 * P.n, P.B, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k, 2 * P.k, st);
+}
+
+static int vamp_iterate_impl(const VampK& P, int t, hipStream_t st) {
+    dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
+    hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_k1");
+    dim3 g2(cdiv(P.B, GBM), P.ncp2 / P.bn2);
+    if (P.bn2 == 128)
+        hipLaunchKernelGGL(vamp_k2<128>, g2, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    else
+        hipLaunchKernelGGL(vamp_k2<256>, g2, dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_k2");
+    hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_r");
+    return AMP_OK;
+}
+
+static int vamp_finalize_impl(const VampK& P, hipStream_t st) {
+    const int g = (int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048);
+    hipLaunchKernelGGL(vamp_output_kernel, dim3(g), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("vamp_output");
+    return AMP_OK;
+}
+
+}  // namespace amp
+
+using namespace amp;
+
+extern "C" {
+
+size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter) {
+    if (!d || k <= 0 || max_iter <= 0) return 0;
+    return vamp_carve(d, k, max_iter, nullptr).bytes;
+}
+
+int amp_vamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
+    VampK P;
+    int rc = vamp_setup(d, c, a, P);
+    if (rc) return rc;
+    return vamp_prepare_impl(P, a, (hipStream_t)stream);
+}
+
+int amp_vamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t t, void* stream) {
+    VampK P;
+    int rc = vamp_setup(d, c, a, P);
+    if (rc) return rc;
+    AMP_REQUIRE(t >= 0 && t < a->max_iter, "amp_vamp_iterate: t = %d outside [0, %d)", t, a->max_iter);
+    rc = vamp_attrs();
+    if (rc) return rc;
+    return vamp_iterate_impl(P, t, (hipStream_t)stream);
+}
+
+int amp_vamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
+    VampK P;
+    int rc = vamp_setup(d, c, a, P);
+    if (rc) return rc;
+    return vamp_finalize_impl(P, (hipStream_t)stream);
+}
+
+int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
+    VampK P;
+    int rc = vamp_setup(d, c, a, P);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_prepare_impl(P, a, st);
+    if (rc) return rc;
+    for (int t = 0; t < P.max_iter; ++t) {
+        rc = vamp_iterate_impl(P, t, st);
+        if (rc) return rc;
+    }
+    return vamp_finalize_impl(P, st);
+}
+
+// Measurement helper (bench.py): one full forward with hipEvents between the launches on
+// `stream`; ms_out[0..3] = average vamp_k1, vamp_k2, vamp_r duration per executed iteration,
+// and the whole forward.  Synchronises the stream (not for use inside a timed region).
+int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, float* ms_out,
+                     void* stream) {
+    VampK P;
+    int rc = vamp_setup(d, c, a, P);
+    if (rc) return rc;
+    AMP_REQUIRE(ms_out, "amp_vamp_profile: null output");
+    hipStream_t st = (hipStream_t)stream;
+    const int n = P.max_iter;
+    std::vector<hipEvent_t> ev(3 * n + 2);
+    for (auto& e : ev) hipEventCreate(&e);
+    hipEventRecord(ev[0], st);
+    rc = vamp_prepare_impl(P, a, st);
+    dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128), g2(cdiv(P.B, GBM), P.ncp2 / P.bn2);
+    for (int t = 0; t < n && !rc; ++t) {
+        hipEventRecord(ev[1 + 3 * t], st);
+        hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        hipEventRecord(ev[2 + 3 * t], st);
+        if (P.bn2 == 128)
+            hipLaunchKernelGGL(vamp_k2<128>, g2, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        else
+            hipLaunchKernelGGL(vamp_k2<256>, g2, dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+        hipEventRecord(ev[3 + 3 * t], st);
+        hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, t);
+    }
+    if (!rc) rc = vamp_finalize_impl(P, st);
+    hipEventRecord(ev[3 * n + 1], st);
+    hipStreamSynchronize(st);
+    amp_status s;
+    hipMemcpy(&s, P.status, sizeof(s), hipMemcpyDeviceToHost);
+    const int T = s.T > 0 ? s.T : n;
+    float k1 = 0.f, k2 = 0.f, rr = 0.f, ms = 0.f;
+    for (int t = 0; t < T; ++t) {
+        hipEventElapsedTime(&ms, ev[1 + 3 * t], ev[2 + 3 * t]); k1 += ms;
+        hipEventElapsedTime(&ms, ev[2 + 3 * t], ev[3 + 3 * t]); k2 += ms;
+        hipEventElapsedTime(&ms, ev[3 + 3 * t], t + 1 < n ? ev[1 + 3 * (t + 1)] : ev[3 * n + 1]); rr += ms;
+    }
+    hipEventElapsedTime(&ms, ev[0], ev[3 * n + 1]);
+    ms_out[0] = k1 / T; ms_out[1] = k2 / T; ms_out[2] = rr / T; ms_out[3] = ms;
+    for (auto& e : ev) hipEventDestroy(e);
+    AMP_LAUNCH_CHECK("amp_vamp_profile");
+    return rc;
+}
+
+}  // extern "C"

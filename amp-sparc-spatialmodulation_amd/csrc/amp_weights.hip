@@ -1,0 +1,171 @@
+// amp_weights.hip — expanded-weight builders, the plain-store GEMM, error state.
+#include <stdarg.h>
+
+#include <algorithm>
+
+#include "amp_gemm.h"
+#include "amp_host.h"
+
+namespace amp {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int check_dims(const amp_dims* d, const amp_constellation* c) {
+    AMP_REQUIRE(d && c, "null dims/constellation");
+    AMP_REQUIRE(d->B > 0 && d->Nt > 0 && d->Na > 0 && d->Nr > 0 && d->Lin > 0 && d->Lout > 0, "non-positive dimension");
+    AMP_REQUIRE(d->Nt % d->Na == 0, "Na must divide Nt (config.py:133)");
+    AMP_REQUIRE(d->M == d->Nt / d->Na && d->L == d->Na * d->Lin && d->N == d->Nt * d->Lin && d->n == d->Nr * d->Lout,
+                "inconsistent derived dimensions");
+    AMP_REQUIRE(is_pow2(d->M), "section size M = Nt/Na = %d must be a power of two", d->M);
+    AMP_REQUIRE(2 * d->M <= 256, "section size M = %d > 128 not supported", d->M);
+    AMP_REQUIRE(c->K >= 1 && c->K <= AMP_MAX_K, "constellation size K = %d out of range", c->K);
+    const int bn = section_bn(d);
+    AMP_REQUIRE(2 * d->N <= bn || (2 * d->N) % bn == 0, "2N = %d must be <= %d or a multiple of it", 2 * d->N, bn);
+    return AMP_OK;
+}
+
+// Wt[2o][2j] = Re X, Wt[2o][2j+1] = -Im X, Wt[2o+1][2j] = Im X, Wt[2o+1][2j+1] = Re X,
+// X[o][j] = rowscale[o] * op(src[o*so + j*sj]), op = conj if `conj`; zero padding up to [ncp][kap].
+// rowscale multiplies like the reference's `s.view(-1,1) * Uh` (f32 x c64 -> per-component products).
+__global__ void build_cweight_kernel(const float2* __restrict__ src, long so, long sj, int conj,
+                                     const float* __restrict__ rowscale, int O, int J, float* __restrict__ wt,
+                                     int kap, int ncp) {
+    const long total = (long)(ncp / 2) * (kap / 2);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int o = (int)(e / (kap / 2)), j = (int)(e % (kap / 2));
+        float xr = 0.f, xi = 0.f;
+        if (o < O && j < J) {
+            const float2 v = src[o * so + j * sj];
+            xr = v.x;
+            xi = conj ? -v.y : v.y;
+            if (rowscale) {
+                const float s = rowscale[o];
+                xr = s * xr;
+                xi = s * xi;
+            }
+        }
+        float* w0 = wt + (size_t)(2 * o) * kap + 2 * j;
+        float* w1 = w0 + kap;
+        w0[0] = xr;
+        w0[1] = -xi;
+        w1[0] = xi;
+        w1[1] = xr;
+    }
+}
+
+// Wt[o][j] = |src[o*so + j*sj]|^2 with torch's complex abs (correctly rounded hypot) then an
+// f32 square (bamp.py:18 `H.abs()**2`).
+__global__ void build_abs2_kernel(const float2* __restrict__ src, long so, long sj, int O, int J,
+                                  float* __restrict__ wt, int kap, int ncp) {
+    const long total = (long)ncp * kap;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int o = (int)(e / kap), j = (int)(e % kap);
+        float v = 0.f;
+        if (o < O && j < J) {
+            const float2 z = src[o * so + j * sj];
+            const float a = (float)sqrt((double)z.x * z.x + (double)z.y * z.y);
+            v = a * a;
+        }
+        wt[e] = v;
+    }
+}
+
+int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J, float* wt,
+                  int kap, int ncp, hipStream_t st) {
+    const long total = (long)(ncp / 2) * (kap / 2);
+    const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(build_cweight_kernel, dim3(grid), dim3(256), 0, st, src, so, sj, conj, rowscale, O, J, wt,
+                       kap, ncp);
+    AMP_LAUNCH_CHECK("build_cweight");
+    return AMP_OK;
+}
+
+int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
+                      hipStream_t st) {
+    const long total = (long)ncp * kap;
+    const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(build_abs2_kernel, dim3(grid), dim3(256), 0, st, src, so, sj, O, J, wt, kap, ncp);
+    AMP_LAUNCH_CHECK("build_abs2_weight");
+    return AMP_OK;
+}
+
+template <int BN>
+int set_lds_attr(const void* fn) {
+    static_assert(GemmCfg<BN>::LDS_BYTES <= 160 * 1024, "LDS budget");
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GemmCfg<BN>::LDS_BYTES);
+    if (e != hipSuccess) {
+        set_error("hipFuncSetAttribute: %s", hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    return AMP_OK;
+}
+template int set_lds_attr<128>(const void*);
+template int set_lds_attr<256>(const void*);
+
+// Plain GEMM: C[rows][ldc] = A[rows][lda](ka valid) . Wt^T, columns [0, nc) stored.
+template <int BN>
+__global__ __launch_bounds__(AMP_WG) void gemm_store_kernel(const float* __restrict__ a, int lda, int rows, int ka,
+                                                            const float* __restrict__ wt, int kap,
+                                                            float* __restrict__ c, int ldc, int nc) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    gemm_tile<BN>(ALoadPlain{a, lda, rows, ka}, wt, kap, row0, col0, lds);
+    using C = GemmCfg<BN>;
+    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
+        const int rho = e / BN, cc = e % BN;
+        const int row = row0 + rho, col = col0 + cc;
+        if (row < rows && col < nc) c[(size_t)row * ldc + col] = lds[rho * C::LDC + cc];
+    }
+}
+
+int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,
+               int nc, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        int rc = set_lds_attr<128>((const void*)gemm_store_kernel<128>);
+        if (rc) return rc;
+        attr = true;
+    }
+    dim3 grid(cdiv(rows, GBM), ncp / 128);
+    hipLaunchKernelGGL(gemm_store_kernel<128>, grid, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, a, lda, rows, ka, wt,
+                       kap, c, ldc, nc);
+    AMP_LAUNCH_CHECK("gemm_store");
+    return AMP_OK;
+}
+
+}  // namespace amp
+
+extern "C" {
+
+const char* amp_last_error(void) { return amp::g_err; }
+
+const char* amp_build_info(void) {
+    return "amp_sparc gfx950: fp32 MFMA v_mfma_f32_32x32x2_f32 GEMM engine (BM=32, BK=32, BN=128/256), "
+           "fused LMMSE/Onsager/section-denoiser epilogues";
+}
+
+// Test/diagnostic entry point: C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T (first ka columns of A valid,
+// first nc columns of C stored).  Requirements: lda % 4 == 0, ka % 4 == 0, kap % 32 == 0, ncp % 128 == 0.
+int amp_gemm_nt_f32(const void* a, int32_t lda, int32_t rows, int32_t ka, const void* wt, int32_t kap, int32_t ncp,
+                    void* c, int32_t ldc, int32_t nc, void* stream) {
+    AMP_REQUIRE(lda % 4 == 0 && ka % 4 == 0 && kap % 32 == 0 && ncp % 128 == 0 && ka <= kap && nc <= ncp,
+                "amp_gemm_nt_f32: bad shape (lda %d ka %d kap %d ncp %d nc %d)", lda, ka, kap, ncp, nc);
+    return amp::gemm_store((const float*)a, lda, rows, ka, (const float*)wt, kap, ncp, (float*)c, ldc, nc,
+                           (hipStream_t)stream);
+}
+
+// Test/diagnostic entry point for the complex weight expansion (see build_cweight_kernel).
+int amp_build_cweight(const void* src, int64_t so, int64_t sj, int32_t conj, const void* rowscale, int32_t O,
+                      int32_t J, void* wt, int32_t kap, int32_t ncp, void* stream) {
+    return amp::build_cweight((const float2*)src, so, sj, conj, (const float*)rowscale, O, J, (float*)wt, kap, ncp,
+                              (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+"""VAMP detector (SVD form) — drop-in for the reference's ``VAMP`` / ``VAMPLayer`` /
+``Tracker`` (vamp.py:12-191), running on the gfx950 kernels of libampsparc.so.
+
+``VAMP.forward(U, s, Vh, y, SNR, x, symbols, indices) -> Loss`` keeps the reference's
+signature and returns its own reused ``Loss`` (vamp.py:187-191).  The whole
+iteration loop, the allclose early exit and the decision/counting run on the device;
+the host reads back one 128-byte record per forward.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+from torch import nn
+
+import amp_native as nat
+from config import Config
+from loss import Loss
+
+
+def _c64(t: torch.Tensor, shape) -> torch.Tensor:
+    t = t.reshape(shape)
+    if t.dtype != torch.complex64:
+        t = t.to(torch.complex64)
+    return t.contiguous()
+
+
+class _Buffers:
+    """Per-shape device buffers reused across forwards (no allocation in steady state)."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, device, B, N, k, iters, ws_bytes):
+        key = (str(device), B, N, k, iters, ws_bytes)
+        if key != self.key:
+            self.r = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.xmmse = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.var = torch.empty(B, N, dtype=torch.float32, device=device)
+            self.res = torch.zeros(256, dtype=torch.uint8, device=device)     # amp_status @0, amp_counts @64
+            self.ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=device)
+            self.key = key
+        return self
+
+
+class Tracker:
+    """Device state of one VAMP forward (vamp.py:12-28): r, xmmse, var and the workspace
+    holding the expanded V/Vh/U weights, y~ and the per-iteration scalar record."""
+
+    def __init__(self, U, s, Vh, y, x, sigma2: float, sparsity: float, config: Config, bufs: _Buffers | None = None):
+        self.config = config
+        B = config.B
+        n, k = U.shape[0], U.shape[1]
+        N = Vh.shape[1]
+        self.U = _c64(U, (n, k))
+        self.s = s.reshape(k).to(torch.float32).contiguous()
+        self.Vh = _c64(Vh, (k, N))
+        self.y = _c64(y, (B, n))
+        self.noise_var = sigma2
+        self.sparsity = sparsity
+        self.k = k
+        self.t = 0
+        self.dims = config.dims()
+        self.const = config.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_vamp_workspace_bytes(C.byref(self.dims), k, config.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_vamp_workspace_bytes: invalid dimensions')
+        self.buf = (bufs or _Buffers()).get(self.y.device, B, N, k, config.N_Layers, wsb)
+        a = nat.AmpVampArgs()
+        a.U, a.s, a.Vh, a.y = (nat.dptr(self.U, name='U'), nat.dptr(self.s, torch.float32, 's'),
+                               nat.dptr(self.Vh, name='Vh'), nat.dptr(self.y, name='y'))
+        a.k, a.max_iter = k, config.N_Layers
+        a.noise_var, a.sparsity = float(sigma2), float(sparsity)
+        a.r, a.xmmse, a.var = nat.dptr(self.buf.r), nat.dptr(self.buf.xmmse), nat.dptr(self.buf.var)
+        a.status = nat.dptr(self.buf.res)
+        a.ws, a.ws_bytes = nat.dptr(self.buf.ws), self.buf.ws.numel()
+        self.args = a
+        self.stream = nat.stream_ptr(self.y.device)
+
+    @property
+    def r(self):
+        return self.buf.r.view(self.config.B, -1, 1)
+
+    @property
+    def xmmse(self):
+        return self.buf.xmmse.view(self.config.B, -1, 1)
+
+    @property
+    def var(self):
+        return self.buf.var.view(self.config.B, -1, 1)
+
+    def prepare(self):
+        nat.check(nat.lib().amp_vamp_prepare(C.byref(self.dims), C.byref(self.const), C.byref(self.args),
+                                             self.stream), 'amp_vamp_prepare')
+
+    def finalize(self):
+        nat.check(nat.lib().amp_vamp_finalize(C.byref(self.dims), C.byref(self.const), C.byref(self.args),
+                                              self.stream), 'amp_vamp_finalize')
+
+    def status(self) -> nat.AmpStatus:
+        return nat.AmpStatus.from_buffer_copy(self.buf.res[:C.sizeof(nat.AmpStatus)].cpu().numpy().tobytes())
+
+
+class VAMPLayer(nn.Module):
+    """One VAMP iteration (vamp.py:56-94) as a device launch pair; a no-op once the
+    early exit of vamp.py:185 has fired."""
+
+    def __init__(self, config: Config, index: int = 0) -> None:
+        super().__init__()
+        self.config = config
+        self.index = index
+        self.Nt, self.Na, self.Lin, self.B = config.Nt, config.Na, config.Lin, config.B
+        self.K = config.K
+        self.M = self.Nt // self.Na
+        self.L = self.Na * self.Lin
+        self.LM = self.L * self.M
+
+    def forward(self, T: Tracker) -> None:
+        nat.check(nat.lib().amp_vamp_iterate(C.byref(T.dims), C.byref(T.const), C.byref(T.args), self.index,
+                                             T.stream), 'amp_vamp_iterate')
+
+    def segmented_denoiser(self, s: torch.Tensor, tau) -> tuple[torch.Tensor, torch.Tensor]:
+        """vamp.py:96-119 on the device: (xmmse c64 [B, LM, 1], var f32 [B, LM, 1])."""
+        return block_denoise(self.config, s, tau, mode=0)
+
+
+def block_denoise(config: Config, s: torch.Tensor, tau, mode: int):
+    """amp_block_denoise: mode 0 scalar tau (VAMP), 1 per-element cov (BAMP, tau = cov/2),
+    2 per-element tau_use, mean only (SCAMP)."""
+    B = config.B
+    r = _c64(s, (B, -1))
+    d = config.dims()
+    cst = config.constellation()
+    xm = torch.empty_like(r)
+    var = torch.empty(r.shape, dtype=torch.float32, device=r.device) if mode != 2 else None
+    tau_s = 0.0
+    tau_p = None
+    if mode == 0:
+        tau_s = float(tau.item() if isinstance(tau, torch.Tensor) else tau)
+    else:
+        tv = tau.reshape(B, -1).to(torch.float32).contiguous()
+        tau_p = nat.dptr(tv, torch.float32, 'tau')
+    lib = nat.lib()
+    wsb = lib.amp_block_denoise_workspace_bytes(C.byref(d))
+    ws = nat.WORKSPACE.get(r.device, 'denoise', wsb)
+    nat.check(lib.amp_block_denoise(C.byref(d), C.byref(cst), nat.dptr(r, name='r'), mode, tau_s, tau_p,
+                                    nat.dptr(xm), nat.dptr(var) if var is not None else None, nat.dptr(ws), wsb,
+                                    nat.stream_ptr(r.device)), 'amp_block_denoise')
+    if mode == 2:
+        return xm.view(B, -1, 1)
+    return xm.view(B, -1, 1), var.view(B, -1, 1)
+
+
+class VAMP(nn.Module):
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        self.config = config
+        self.E = config.Na / config.Nr                                   # vamp.py:154
+        self.sparsity = config.Na / config.Nt                            # vamp.py:155
+        self.layers = nn.ModuleList([VAMPLayer(config, i) for i in range(config.N_Layers)])
+        self.L = Loss(config)
+        self._bufs = _Buffers()
+        self.last = None
+
+    def detect(self, U, s, Vh, y, SNR: float) -> Tracker:
+        """All iterations on the device, asynchronous (no host sync)."""
+        T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
+        nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
+                  'amp_vamp_run')
+        return T
+
+    def forward(self, U: torch.Tensor, s: torch.Tensor, Vh: torch.Tensor, y: torch.Tensor, SNR: float,
+                x: torch.Tensor, symbols: np.ndarray, indices: np.ndarray) -> Loss:
+        T = self.detect(U, s, Vh, y, SNR)
+        self.L.dump()                                                    # vamp.py:180
+        # decision on T.r (vamp.py:187); counters land next to the status record
+        self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=T.buf.res[64:])
+        status, counts = read_result(T.buf.res)                          # the forward's one host sync
+        self.L.record(self.L.rates_from_counts(counts), int(status.T))
+        self.last = T
+        return self.L
+
+
+def read_result(res: torch.Tensor):
+    """(amp_status, amp_counts) from the 256-byte result buffer (status @0, counts @64)."""
+    raw = res.cpu().numpy().tobytes()
+    return (nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)]),
+            nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)]))
+

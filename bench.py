@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Benchmark: detected symbol-vectors/s of the VAMP detector at BASELINE.json's config
+(Nt=256, Nr=512, Na=8, 16-QAM, batch 4096, T <= 20), one process per GPU.
+
+A step = one Monte-Carlo epoch of the hot path on inputs already resident in HBM:
+VAMP.forward (all iterations, early exit, MAP decision and every error counter on the
+GPU) + the one 128-byte result read-back — exactly what Model.simulate calls per epoch
+(vamp_model.py:61).  Input generation and the SVD are outside the timed region
+(SURVEY.md §8(d)).  Each rank runs its own independent epoch (its own seed): Monte-Carlo
+epochs are independent, so the path shards with no data-path collective ("weak").
+
+  python bench.py [--gpus N --steps K --warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'amp-sparc-spatialmodulation_amd'))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch        # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (Nt, Na, Nr, B, alphabet, iterations)
+    'cfg4': (256, 8, 512, 4096, '16QAM', 20),
+    'cfg2': (64, 4, 128, 1024, '16QAM', 20),
+}
+
+
+def make_inputs(cfg, seed, EbN0, device):
+    """Reference call order on the host RNG replica (CPU), then moved to the GPU."""
+    from channel import Channel
+    from data import Data
+    dev = cfg.device
+    cfg.device = 'cpu'
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    ch, da = Channel(cfg), Data(cfg)
+    _, A = ch.generate_as_sparc()
+    U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+    x, sym, idx = da.generate_message()
+    SNR = cfg.snr(EbN0)
+    y = A @ x + ch.awgn(SNR)
+    cfg.device = dev
+    to = lambda t: t.to(device).contiguous()  # noqa: E731
+    return dict(A=A, U=to(U), s=to(s), Vh=to(Vh), y=to(y), x=to(x), SNR=SNR,
+                sym=torch.from_numpy(np.asarray(sym, np.int64)).to(device),
+                idx=torch.from_numpy(np.asarray(idx, np.int64)).to(device),
+                cpu=dict(U=U.numpy(), s=s.numpy(), Vh=Vh.numpy(), y=y.numpy()[..., 0], x=x.numpy()[..., 0],
+                         sym=sym, idx=idx))
+
+
+def cpu_baseline(cfgname, EbN0, seed, sample_trials):
+    """The oracle (numpy restatement of the reference path, oracle/) timed on this host's
+    cores on a bounded sample of the same workload: `sample_trials` trials of the config."""
+    from threadpoolctl import threadpool_limits
+    from oracle import OracleConfig, vamp_detect, loss_dict
+    from config import Config
+    Nt, Na, Nr, B, alph, iters = CONFIGS[cfgname]
+    cores = min(16, os.cpu_count() or 1)
+    cfg = Config(Nt, Na, Nr, 1, 1, batch=sample_trials, generator_mode='sparc', iterations=iters, alphabet=alph,
+                 channel_profile='uniform', channel_truncation='tail', device='cpu')
+    inp = make_inputs(cfg, seed, EbN0, 'cpu')['cpu']
+    ocfg = OracleConfig(Nt, Na, Nr, B=sample_trials, alphabet=alph, iterations=iters)
+    with threadpool_limits(limits=cores):
+        t0 = time.perf_counter()
+        out = vamp_detect(inp['U'], inp['s'], inp['Vh'], inp['y'], cfg.snr(EbN0), ocfg)
+        loss_dict(out['r'], out['xmmse'], inp['x'], inp['sym'], inp['idx'], out['T'], ocfg)
+        dt = time.perf_counter() - t0
+    return dict(value=sample_trials / dt, unit='symbol-vectors/s', cores=cores, kind='port',
+                sample=f'{sample_trials} trials of {cfgname} (Nt={Nt} Nr={Nr} Na={Na} {alph}), EbN0={EbN0} dB, '
+                       f'T={out["T"]}, numpy oracle incl. decision+metrics, {dt:.1f} s')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='cfg4', choices=sorted(CONFIGS))
+    ap.add_argument('--ebn0', type=float, default=8.0)
+    ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--cpu-sample', type=int, default=4096)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+
+    from config import Config
+    from vamp import VAMP
+    import ctypes as C
+    import amp_native as nat
+
+    Nt, Na, Nr, B, alph, iters = CONFIGS[args.config]
+    cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
+                 channel_profile='uniform', channel_truncation='tail', device='cuda')
+    inp = make_inputs(cfg, args.seed + rank, args.ebn0, device)
+    det = VAMP(cfg)
+
+    def step():
+        return det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        L = step()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    if dist:
+        tdist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        el = t.item()
+    T = int(L.loss['T'])
+    ver, ser = float(L.loss['ver']), float(L.loss['ser'])
+
+    # dominant kernel (GEMM2 + fused denoiser) timed with HIP events on the stream it runs on
+    Tr = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    ms = (C.c_float * 4)()
+    nat.check(nat.lib().amp_vamp_profile(C.byref(Tr.dims), C.byref(Tr.const), C.byref(Tr.args), ms, Tr.stream),
+              'amp_vamp_profile')
+    N, k = Nt, min(Nt, Nr)
+    flops_k2 = 8.0 * B * N * k                     # complex [N x k] . [k] per trial = 8 real flop / CMAC
+    achieved = flops_k2 / (ms[1] * 1e-3) / 1e12
+    if rank != 0:
+        if dist:
+            tdist.destroy_process_group()
+        return
+    ms_step = el / args.steps * 1e3
+    value = world * B / (el / args.steps)
+    out = {
+        'metric': 'detected symbol-vectors/sec, VAMP Nt=256 Nr=512 16-QAM; SER match vs ref',
+        'value': value, 'unit': 'symbol-vectors/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': ms_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic (reference generators replayed: sparc channel, segmented 16-QAM messages, AWGN)',
+        'config': {'workload': f'{args.config}: VAMP Nt={Nt} Nr={Nr} Na={Na} {alph} batch={B} iterations<={iters} '
+                               f'EbN0={args.ebn0} dB, one channel per batch',
+                   'global_batch': world * B, 'parallelism': f'trial-shard x{world} (independent epochs)'},
+        'detail': {'T': T, 'ver': ver, 'ser': ser, 'trial_iterations_per_s': world * B * T / (el / args.steps),
+                   'kernel_ms': {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}},
+        'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
+                     'kernel': 'vamp_k2 (GEMM2 + Onsager update + section denoiser)',
+                     'flop_per_launch': flops_k2},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out['cpu_baseline'] = cpu_baseline(args.config, args.ebn0, args.seed, args.cpu_sample)
+    print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

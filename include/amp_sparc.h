@@ -1,0 +1,191 @@
+/*
+ * amp_sparc.h — C ABI of the MI355X (gfx950) AMP/VAMP spatial-modulation detector.
+ *
+ * Drop-in boundary for the hot path of AhmedKishki/AMP-SPARC-SpatialModulation.
+ * The reference exposes no FFI: its boundary is the Python class surface
+ * (VAMP / BAMP / SCAMP / Loss).  The host package
+ * `amp-sparc-spatialmodulation_amd/` keeps that surface and binds these entry
+ * points through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every array argument is a DEVICE pointer
+ *    owned by the caller; nothing is retained after a call returns.
+ *  - complex64 arrays are interleaved {re, im} float pairs (torch.complex64 layout).
+ *    Batched vectors are row-major [B][len] (the reference's [B, len, 1]).
+ *  - Every call is asynchronous on `stream` (a hipStream_t passed as void*), makes
+ *    no allocation and no host synchronisation, so it may be captured in a hipGraph.
+ *    Results that the host needs (iteration count, error counters) are written to
+ *    small device structs the caller copies back once.
+ *  - Return value: 0 on success, a negative AMP_E* code otherwise;
+ *    amp_last_error() returns a message for the last failure on this thread.
+ *    The reference raises Python exceptions instead (AssertionError in
+ *    config.py:40-44, ValueError on bad reshapes); the host layer maps a
+ *    non-zero code to a Python exception.  NaN outputs are a legal state
+ *     and never an error.
+ */
+#ifndef AMP_SPARC_H
+#define AMP_SPARC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMP_OK 0
+#define AMP_E_ARG (-1)       /* bad argument / unsupported shape */
+#define AMP_E_WORKSPACE (-2) /* workspace too small */
+#define AMP_E_LAUNCH (-3)    /* HIP launch failure */
+
+#define AMP_MAX_K 16         /* largest constellation of config.py:44 (16PSK / 16QAM) */
+
+/* Constellation of Config (config.py:78-118): unit-power points in float32 (for the
+ * denoiser) and float64 (for the MAP decision, loss.py:295), plus gray labels. */
+typedef struct amp_constellation {
+    int32_t K;
+    int32_t symbol_bits;          /* int(log2 K), config.py:119 */
+    float re[AMP_MAX_K];
+    float im[AMP_MAX_K];
+    double re64[AMP_MAX_K];
+    double im64[AMP_MAX_K];
+    int32_t gray[AMP_MAX_K];
+} amp_constellation;
+
+/* System dimensions (Config, config.py:49-71, 132-144; sparc mode).
+ * N = Nt*Lin (unknowns per trial), n = Nr*Lout (observations per trial),
+ * L = Na*Lin sections of M = Nt/Na positions each. */
+typedef struct amp_dims {
+    int32_t B, Nt, Na, Nr, Lin, Lout;
+    int32_t N, n, L, M;
+} amp_dims;
+
+/* Per-forward result written by the detector drivers (device memory). */
+typedef struct amp_status {
+    int32_t T;          /* executed iterations (t+1 at the early-exit break, vamp.py:185) */
+    int32_t nan_state;  /* 1 when the last iteration produced NaN sections (float64 underflow rule) */
+    int32_t stopped;    /* 1 when the allclose early exit fired */
+    int32_t pad;
+    float last_scalar[4]; /* VAMP: sigma2_tilde, alpha, sigma2, dxdr of the last iteration */
+} amp_status;
+
+/* Error counters of Loss.error_rate (loss.py:67-179), written by amp_map_decide_count. */
+typedef struct amp_counts {
+    int64_t ier, ser;           /* index / gray-label mismatches over Ns sections (loss.py:165-166) */
+    int64_t iber, sber;         /* bit mismatches (loss.py:168, 172) */
+    int64_t ver, verf, verm, verL;  /* channel uses with any wrong entry (loss.py:133-136) */
+    int64_t fer;                /* trials with any wrong entry (loss.py:150) */
+    double mse, msef, msem, mseL;   /* sum |xmmse - x|^2, all / lin 0 / Lin//2 / last (loss.py:116-119) */
+} amp_counts;
+
+/* ---- VAMP (SVD form) — replaces VAMP.forward (vamp.py:159-187) with its
+ *      Tracker (vamp.py:12-28) and T x VAMPLayer.forward (vamp.py:56-94). ---- */
+typedef struct amp_vamp_args {
+    const void* U;      /* c64 [n][k]  (torch.linalg.svd output, vamp_model.py:58) */
+    const void* s;      /* f32 [k] */
+    const void* Vh;     /* c64 [k][N] */
+    const void* y;      /* c64 [B][n] */
+    int32_t k;          /* min(n, N) */
+    int32_t max_iter;   /* config.N_Layers */
+    double noise_var;   /* Na/Nr/SNR (vamp.py:179) */
+    double sparsity;    /* Na/Nt (vamp.py:155) */
+    void* r;            /* out c64 [B][N]: decision input T.r (vamp.py:187) */
+    void* xmmse;        /* out c64 [B][N] */
+    void* var;          /* out f32 [B][N] */
+    void* status;       /* out amp_status (device) */
+    void* ws;           /* workspace, amp_vamp_workspace_bytes() bytes */
+    size_t ws_bytes;
+} amp_vamp_args;
+
+size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter);
+int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
+/* Layer-level pieces of amp_vamp_run: prepare = Tracker (vamp.py:13-28);
+ * iterate(t) = one VAMPLayer.forward + the allclose test of vamp.py:185 (no-op once stopped);
+ * finalize = iteration count and NaN bookkeeping for the returned Loss. */
+int amp_vamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
+int amp_vamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t t, void* stream);
+int amp_vamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
+/* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
+ * launches; ms_out[4] = mean GEMM1 / GEMM2+denoiser / reduction kernel time per executed
+ * iteration and the whole forward, in milliseconds. */
+int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, float* ms_out,
+                     void* stream);
+
+/* ---- BAMP — replaces BAMP.forward (bamp.py:116-143) with BAMPLayer.forward
+ *      (bamp.py:48-64) and its per-element-tau denoiser (bamp.py:66-77). ---- */
+typedef struct amp_bamp_args {
+    const void* H;      /* c64 [n][N] */
+    const void* y;      /* c64 [B][n] */
+    int32_t max_iter;
+    int32_t pad;
+    double noise_var;   /* Na/Nr/SNR (bamp.py:124) */
+    void* xmap;         /* out c64 [B][N]: decision input T.xmap (bamp.py:142) */
+    void* xmmse;        /* out c64 [B][N] */
+    void* var;          /* out f32 [B][N] */
+    void* status;
+    void* ws;
+    size_t ws_bytes;
+} amp_bamp_args;
+
+size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
+int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
+
+/* ---- SCAMP — replaces SCAMP.forward (scamp.py:77-107) with SCAMPLayer.forward
+ *      (scamp.py:43-59) and its mean-only denoiser (scamp.py:61-68). ---- */
+typedef struct amp_scamp_args {
+    const void* W;      /* f32 [Lout][Lin] base matrix (channel.py:80-83) */
+    const void* A;      /* c64 [n][N] */
+    const void* y;      /* c64 [B][n] */
+    int32_t max_iter;
+    int32_t pad;
+    double noise_var;   /* Na/Nr/SNR (scamp.py:98) */
+    void* xmap;         /* out c64 [B][N] (scamp.py:107) */
+    void* xmmse;        /* out c64 [B][N] */
+    void* psi;          /* out f32 [B][Lin] */
+    void* status;
+    void* ws;
+    size_t ws_bytes;
+} amp_scamp_args;
+
+size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
+int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+
+/* ---- Block-sparse denoiser — replaces VAMPLayer.segmented_denoiser
+ *      (vamp.py:96-119), BAMPLayer.segmented_denoiser (bamp.py:66-77) and
+ *      SCAMPLayer.denoiser (scamp.py:61-68) as a standalone op.
+ * tau_mode 0: tau = tau_scalar (VAMP sigma2); 1: tau[b][j] = tau_vec[b*N+j]*0.5 (BAMP cov);
+ *          2: as 1 but mean only (SCAMP, var may be NULL).
+ * The batch-global float64 max|xi| shift of the reference is reproduced by its
+ * NaN rule: a section is NaN iff its max logit lies > 745.1332 below max|xi|. */
+int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void* r, int32_t tau_mode,
+                      float tau_scalar, const void* tau_vec, void* xmmse, void* var, void* ws,
+                      size_t ws_bytes, void* stream);
+size_t amp_block_denoise_workspace_bytes(const amp_dims* d);
+
+/* ---- MAP decision + error counting — replaces Loss.error_rate (loss.py:67-103),
+ *      Loss.MAP_decision (loss.py:282-302) and the metric helpers (loss.py:105-179).
+ * sym: int64 [B*L] true gray labels; idx: int64 [B*L] true flat nonzero indices
+ * (data.py:89-90).  ibits_trunc = ceil(log2(Lin*B*Na)) (loss.py:20).
+ * decisions (optional, may be NULL): int32 [B*L] flat argmax m*K + k per section. */
+int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap,
+                         const void* xmmse, const void* x, const void* sym, const void* idx,
+                         int32_t ibits_trunc, void* counts, void* decisions, void* ws, size_t ws_bytes,
+                         void* stream);
+size_t amp_map_decide_workspace_bytes(const amp_dims* d);
+
+/* ---- Building blocks exposed for tests and tools ---- */
+/* C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T on fp32 MFMA (first ka columns of A, first nc of C). */
+int amp_gemm_nt_f32(const void* a, int32_t lda, int32_t rows, int32_t ka, const void* wt, int32_t kap,
+                    int32_t ncp, void* c, int32_t ldc, int32_t nc, void* stream);
+/* Real expansion of a complex operator X[o][j] = rowscale[o] * op(src[o*so + j*sj]) into Wt. */
+int amp_build_cweight(const void* src, int64_t so, int64_t sj, int32_t conj, const void* rowscale,
+                      int32_t O, int32_t J, void* wt, int32_t kap, int32_t ncp, void* stream);
+
+/* Diagnostics. */
+const char* amp_last_error(void);
+const char* amp_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMP_SPARC_H */

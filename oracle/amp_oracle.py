@@ -141,6 +141,11 @@ def allclose_f32(nxt: np.ndarray, prev: np.ndarray) -> bool:
     return bool(np.all(close))
 
 
+def _torch_abs(z: np.ndarray) -> np.ndarray:
+    """torch.abs of complex64 on CPU = correctly rounded hypot (measured)."""
+    return np.sqrt(z.real.astype(np.float64) ** 2 + z.imag.astype(np.float64) ** 2).astype(F32)
+
+
 def _div_real(z: np.ndarray, d) -> np.ndarray:
     """complex64 / float32 as the reference computes it: z * (1/d)."""
     return (z * _recip(d)).astype(C64, copy=False)
@@ -169,7 +174,9 @@ def block_denoise(r: np.ndarray, tau, cfg: OracleConfig):
     Returns (xmmse complex64 [B,N], var float32 [B,N]).
     """
     B = r.shape[0]
-    sym = cfg.symbols.astype(np.complex128)
+    # keep the symbols' dtype: float64 for OOK/BPSK/4ASK (real division by Z), complex128
+    # otherwise (c128 / f64 = multiply by 1/Z, which overflows once Z is denormal)
+    sym = cfg.symbols
     xi = _logits(r, tau, cfg, B)
     with np.errstate(under='ignore', invalid='ignore', divide='ignore', over='ignore'):
         eta = np.exp(xi - np.abs(xi).max())
@@ -185,7 +192,7 @@ def block_denoise(r: np.ndarray, tau, cfg: OracleConfig):
 def scamp_denoise(r: np.ndarray, tau_half: np.ndarray, cfg: OracleConfig) -> np.ndarray:
     """SCAMPLayer.denoiser (scamp.py:61-68): posterior mean only, tau = tau_use/2."""
     B = r.shape[0]
-    sym = cfg.symbols.astype(np.complex128)
+    sym = cfg.symbols
     xi = _logits(r, tau_half, cfg, B)
     with np.errstate(under='ignore', invalid='ignore', divide='ignore', over='ignore'):
         eta = np.exp(xi - np.abs(xi).max())
@@ -265,7 +272,7 @@ def bamp_detect(H, y, SNR: float, cfg: OracleConfig, trace: list | None = None):
     N = H.shape[1]
     sigma2 = (cfg.Na / cfg.Nr) / SNR                              # bamp.py:124 (Python float)
     Hc = np.conj(H)
-    abs2 = (np.abs(H) ** 2).astype(F32)                           # bamp.py:18
+    abs2 = (_torch_abs(H) ** 2).astype(F32)                        # bamp.py:18
     xm = np.zeros((B, N), C64)
     var = np.ones((B, N), F32)
     z = y.copy()
@@ -320,7 +327,7 @@ def scamp_detect(W, A, y, SNR: float, cfg: OracleConfig, trace: list | None = No
         g = (_div_real(z, phi_use) @ Ac).astype(C64)
         xmap = (xm + tau_use * g).astype(C64)                     # scamp.py:57
         xm = scamp_denoise(xmap, (tau_use / F32(2)).astype(F32), cfg)   # scamp.py:58
-        psi = (F32(1) - (np.abs(xm) ** 2).reshape(B, Lc, Mc).sum(axis=-1) / F32(cfg.Na)).astype(F32)  # scamp.py:59
+        psi = (F32(1) - (_torch_abs(xm) ** 2).reshape(B, Lc, Mc).sum(axis=-1) / F32(cfg.Na)).astype(F32)  # scamp.py:59
         if trace is not None:
             trace.append(dict(xmap=xmap.copy(), xmmse=xm.copy(), psi=psi.copy(), z=z.copy()))
         if allclose_f32(psi, psi_prev):                           # scamp.py:105

@@ -1,0 +1,213 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
+and the numpy oracle.  Run with  pytest -m gpu.
+
+Tolerances (north star, BASELINE.json): VER / SER within 1e-3 absolute of the reference
+at every SNR point on the same seeds; iteration count T exact.  Traces at small shapes
+(g1) must reproduce the reference's Loss dict exactly on the counting metrics.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_io as gio
+from oracle import OracleConfig, vamp_detect
+
+pytestmark = pytest.mark.gpu
+
+G1 = gio.g1_cases()
+G2 = gio.g2_cases()
+G3 = gio.g3_cases()
+
+
+def _config(Nt, Na, Nr, B, alphabet, iterations=20, Lin=1, Lh=1, device='cuda'):
+    from config import Config
+    return Config(Nt, Na, Nr, Lin, Lh, batch=B, generator_mode='sparc', iterations=iterations, alphabet=alphabet,
+                  channel_profile='uniform', channel_truncation='tail', device=device)
+
+
+def _t(a, device, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(device)
+
+
+# ----------------------------------------------------------------------------- engine
+@pytest.mark.parametrize('rows,ka,nc', [(32, 32, 128), (100, 8, 16), (64, 512, 512), (77, 36, 200), (4096, 512, 512)])
+def test_gemm_engine_matches_fp64(device, rows, ka, nc):
+    import ctypes as C
+    import amp_native as nat
+    g = torch.Generator().manual_seed(rows + ka)
+    A = torch.randn(rows, ka, generator=g, dtype=torch.float32)
+    Wl = torch.randn(nc, ka, generator=g, dtype=torch.float32)
+    kap = (ka + 31) // 32 * 32
+    ncp = (nc + 127) // 128 * 128
+    Wt = torch.zeros(ncp, kap)
+    Wt[:nc, :ka] = Wl
+    Ad, Wd = A.to(device), Wt.to(device)
+    Cd = torch.full((rows, nc), float('nan'), device=device)
+    nat.check(nat.lib().amp_gemm_nt_f32(nat.dptr(Ad), ka, rows, ka, nat.dptr(Wd), kap, ncp, nat.dptr(Cd), nc, nc,
+                                        nat.stream_ptr(device)), 'gemm')
+    ref = (A.double() @ Wl.double().T)
+    err = (Cd.cpu().double() - ref).abs().max().item()
+    scale = (A.double().abs() @ Wl.double().abs().T).max().item()
+    assert err <= 2e-6 * scale, (err, scale)
+
+
+def test_complex_weight_expansion(device):
+    """Wt built from X must turn the real GEMM into the complex product X x (asymmetric X)."""
+    import amp_native as nat
+    g = torch.Generator().manual_seed(5)
+    O, J, B = 40, 24, 50
+    X = torch.complex(torch.randn(O, J, generator=g), torch.randn(O, J, generator=g))
+    x = torch.complex(torch.randn(B, J, generator=g), torch.randn(B, J, generator=g))
+    kap = (2 * J + 31) // 32 * 32
+    ncp = (2 * O + 127) // 128 * 128
+    Xd = X.to(device).contiguous()
+    Wt = torch.empty(ncp, kap, device=device)
+    for conj, Xuse in ((0, X), (1, X.conj())):
+        nat.check(nat.lib().amp_build_cweight(nat.dptr(Xd), J, 1, conj, None, O, J, nat.dptr(Wt), kap, ncp,
+                                              nat.stream_ptr(device)), 'cweight')
+        xd = x.to(device).contiguous()
+        y = torch.empty(B, O, dtype=torch.complex64, device=device)
+        nat.check(nat.lib().amp_gemm_nt_f32(nat.dptr(xd), 2 * J, B, 2 * J, nat.dptr(Wt), kap, ncp, nat.dptr(y),
+                                            2 * O, 2 * O, nat.stream_ptr(device)), 'gemm')
+        ref = (x.to(torch.complex128) @ Xuse.to(torch.complex128).T)
+        assert (y.cpu().to(torch.complex128) - ref).abs().max().item() < 1e-4
+
+
+# ----------------------------------------------------------------------------- denoiser
+@pytest.mark.parametrize('name', sorted(G2))
+def test_g2_denoiser(device, name):
+    from vamp import block_denoise
+    c = G2[name]
+    cfg = _config(int(c.Nt), int(c.Na), 2 * int(c.Nt), int(c.B), str(c.alphabet))
+    r = _t(c.r, device)
+    xm, var = block_denoise(cfg, r, float(c.tau), mode=0)
+    xm, var = xm.cpu().numpy()[..., 0], var.cpu().numpy()[..., 0]
+    assert np.array_equal(np.isnan(xm), np.isnan(c.v_xmmse))
+    np.testing.assert_allclose(xm, c.v_xmmse, rtol=0, atol=3e-6, equal_nan=True)
+    np.testing.assert_allclose(var, c.v_var, rtol=1e-4, atol=2e-7, equal_nan=True)
+    if 'b_xmmse' in c:
+        xm, var = block_denoise(cfg, r, _t(c.cov, device), mode=1)
+        np.testing.assert_allclose(xm.cpu().numpy()[..., 0], c.b_xmmse, rtol=0, atol=3e-6, equal_nan=True)
+        np.testing.assert_allclose(var.cpu().numpy()[..., 0], c.b_var, rtol=1e-4, atol=2e-7, equal_nan=True)
+        xs = block_denoise(cfg, r, _t(c.tau_use, device), mode=2)
+        np.testing.assert_allclose(xs.cpu().numpy()[..., 0], c.s_xmmse, rtol=0, atol=3e-6, equal_nan=True)
+
+
+# ----------------------------------------------------------------------------- decision
+@pytest.mark.parametrize('name', sorted(G3))
+def test_g3_decision_metrics(device, name):
+    from loss import Loss
+    c = G3[name]
+    Nt, Na, Nr, B, Lin, Lh = (int(v) for v in c.dims)
+    cfg = _config(Nt, Na, Nr, B, str(c.alphabet), Lin=Lin, Lh=Lh)
+    L = Loss(cfg)
+    xmap = _t(c.xmap, device)
+    xhat, shat, ihat = L.MAP_decision(xmap)
+    np.testing.assert_array_equal(xhat, c.xhat)
+    np.testing.assert_array_equal(shat, c.shat)
+    np.testing.assert_array_equal(ihat, c.ihat)
+    L.dump()
+    L(xmap, _t(c.xmmse, device), _t(c.x, device), c.sym, c.idx, 3)
+    bad = gio.loss_close(L.loss, c.loss_ref, count_tol=0.0, mse_rtol=1e-5)
+    assert not bad, bad
+    assert L.loss['T'] == 3
+
+
+# ----------------------------------------------------------------------------- VAMP traces
+VAMP_G1 = sorted(k for k in G1 if k.startswith('vamp'))
+
+
+@pytest.mark.parametrize('name', VAMP_G1)
+def test_vamp_g1_reference_inputs(device, name):
+    """Stored reference inputs -> same T and same counting metrics as the reference."""
+    from vamp import VAMP
+    c = G1[name]
+    cfg = _config(int(c.Nt), int(c.Na), int(c.Nr), int(c.B), c.alphabet, iterations=int(c.iters))
+    det = VAMP(cfg)
+    L = det(_t(c.U, device), _t(c.s, device), _t(c.Vh, device), _t(c.y, device), float(c.SNR), _t(c.x, device),
+            c.sym, c.idx)
+    assert L.loss['T'] == int(c.T)
+    bad = gio.loss_close(L.loss, c.loss_ref, count_tol=0.0, mse_rtol=5e-2)
+    assert not bad, bad
+    # first-iteration state against the reference trace / the oracle on the same inputs
+    ocfg = OracleConfig(int(c.Nt), int(c.Na), int(c.Nr), B=int(c.B), alphabet=c.alphabet, iterations=int(c.iters))
+    out = vamp_detect(c.U, c.s, c.Vh, c.y, float(c.SNR), ocfg)
+    assert out['T'] == L.loss['T']
+    r = det.last.r.cpu().numpy()[..., 0]
+    if out['T'] <= 4 and np.all(np.isfinite(out['r'])):
+        np.testing.assert_allclose(r, out['r'], rtol=0, atol=1e-3 * max(1.0, np.abs(out['r']).max()))
+
+
+def test_vamp_layerwise_equals_fused(device):
+    """Tracker + VAMPLayer.forward per iteration == the fused amp_vamp_run."""
+    from vamp import VAMP, Tracker
+    c = G1['vamp_QPSK_0_0']
+    cfg = _config(int(c.Nt), int(c.Na), int(c.Nr), int(c.B), c.alphabet, iterations=int(c.iters))
+    det = VAMP(cfg)
+    args = (_t(c.U, device), _t(c.s, device), _t(c.Vh, device), _t(c.y, device), float(c.SNR))
+    T1 = det.detect(*args)
+    r1, st1 = T1.r.clone(), T1.status().T
+    T = Tracker(args[0], args[1], args[2], args[3], None, det.E / args[4], det.sparsity, cfg)
+    T.prepare()
+    for layer in det.layers:
+        layer(T)
+    T.finalize()
+    assert T.status().T == st1
+    assert torch.equal(T.r, r1)
+
+
+# ----------------------------------------------------------------------------- VAMP curves
+def _regen_inputs(cfg, seed, EbN0, svd=True):
+    """The reference's per-epoch call order with the build's host RNG replica (CPU), then
+    moved to the GPU — same bits as the reference's CPU path."""
+    from channel import Channel
+    from data import Data
+    dev = cfg.device
+    cfg.device = 'cpu'
+    try:
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        ch, da = Channel(cfg), Data(cfg)
+        W, A = ch.generate_as_sparc()
+        U = s = Vh = None
+        if svd:
+            U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+        x, sym, idx = da.generate_message()
+        SNR = cfg.snr(EbN0)
+        y = A @ x + ch.awgn(SNR)
+    finally:
+        cfg.device = dev
+    mv = (lambda t: t.to(dev) if t is not None else None)
+    return dict(W=mv(W), A=mv(A), U=mv(U), s=mv(s), Vh=mv(Vh), x=mv(x), y=mv(y), sym=sym, idx=idx, SNR=SNR)
+
+
+CURVES = gio.g4_curves()
+
+
+def _curve_points(name, every=1):
+    ent = CURVES[name]
+    keys = sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1])))
+    return [(name, k) for k in keys[::every]]
+
+
+VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk') +
+               _curve_points('cfg4_vamp_16qam', 2) + _curve_points('cfg4_vamp_qpsk'))
+
+
+@pytest.mark.parametrize('name,key', VAMP_POINTS)
+def test_vamp_curve_point(device, name, key):
+    """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar)."""
+    from vamp import VAMP
+    ent = CURVES[name]
+    ref = ent['points'][key]
+    seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    inp = _regen_inputs(cfg, seed, EbN0)
+    L = VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    got = L.loss
+    assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
+    assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
+    assert abs(int(got['T']) - int(ref['T'])) <= 1, (got['T'], ref['T'])
