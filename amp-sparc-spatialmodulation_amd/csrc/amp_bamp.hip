@@ -1,10 +1,369 @@
-// amp_bamp.hip — BAMP detector (placeholder until the fused kernels land).
+// amp_bamp.hip — BAMP detector, device-resident iteration loop.
+//
+// Restates BAMP.forward (bamp.py:116-143) with its Tracker (bamp.py:12-25) and
+// BAMPLayer.forward (bamp.py:48-64):
+//   v = |H|^2 var ; z = H xmmse - v (y - z) / u ; u = v + sigma2 ;
+//   cov = 1 / (|H|^2^T (1/u)) ; xmap = xmmse + cov (H^H ((y - z)/u)) ;
+//   xmmse, var = denoiser(xmap, tau = cov/2)  (bamp.py:66-77)
+// and the allclose(var) early exit (bamp.py:140).
+// Per iteration: four fp32-MFMA GEMM launches with fused epilogues + one reduction /
+// exact-float64 fix-up workgroup (same scheme as amp_vamp.hip).
+#include <algorithm>
+#include <mutex>
+
+#include "amp_denoise.h"
+#include "amp_gemm.h"
 #include "amp_host.h"
+
+namespace amp {
+
+constexpr int BRWG = 1024;
+
+struct alignas(16) BampIter {
+    int32_t stopped, T, fixed, pad;
+};
+
+struct BampK {
+    int B, N, n, L, M, bn;
+    int kapA1, ncpA1, kapA2, ncpA2, kapB1, ncpB1, kapB2, ncpB2;
+    int nblk, max_iter;
+    float sigma2;       // f32(noise_var): u = v + sigma2 (bamp.py:61)
+    const float* Wabs2;    // [ncpA1][kapA1]   v = |H|^2 var
+    const float* WH;       // [ncpA2][kapA2]   H xmmse
+    const float* Wabs2T;   // [ncpB1][kapB1]   |H|^2^T (1/u)
+    const float* WHH;      // [ncpB2][kapB2]   H^H s
+    const float* y;        // [B][2n]
+    float* v;              // [B][n]
+    float* z;              // [B][2n]
+    float* invu;           // [B][n]
+    float* s;              // [B][2n]  (y - z)/u
+    float* cov;            // [B][N]
+    float* xmap;           // [B][2N]  caller
+    float* xm;             // [B][2N]  caller
+    float* var0;           // caller's var (even iterations)
+    float* var1;           // workspace  (odd iterations)
+    double* secmax;        // [B*L]
+    Partial* parts;        // [max_iter][nblk]
+    BampIter* iters;       // [max_iter + 1]
+    amp_status* status;
+    Const c;
+};
+
+struct BampWs {
+    float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
+    double* secmax;
+    Partial* parts;
+    BampIter* iters;
+    size_t bytes;
+};
+
+static void bamp_geometry(const amp_dims* d, BampK& P) {
+    P.B = d->B; P.N = d->N; P.n = d->n; P.L = d->L; P.M = d->M;
+    P.bn = section_bn(d);
+    P.kapA1 = round_up(d->N, GBK); P.ncpA1 = round_up(d->n, 128);
+    P.kapA2 = round_up(2 * d->N, GBK); P.ncpA2 = round_up(2 * d->n, 128);
+    P.kapB1 = round_up(d->n, GBK); P.ncpB1 = round_up(d->N, 128);
+    P.kapB2 = round_up(2 * d->n, GBK); P.ncpB2 = round_up(2 * d->N, P.bn);
+    P.nblk = cdiv(d->B, GBM) * (P.ncpB2 / P.bn);
+}
+
+static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
+    BampK P;
+    bamp_geometry(d, P);
+    Carve cv(base);
+    BampWs w;
+    w.Wabs2 = cv.take<float>((size_t)P.ncpA1 * P.kapA1);
+    w.WH = cv.take<float>((size_t)P.ncpA2 * P.kapA2);
+    w.Wabs2T = cv.take<float>((size_t)P.ncpB1 * P.kapB1);
+    w.WHH = cv.take<float>((size_t)P.ncpB2 * P.kapB2);
+    w.v = cv.take<float>((size_t)d->B * d->n);
+    w.z = cv.take<float>((size_t)d->B * 2 * d->n);
+    w.invu = cv.take<float>((size_t)d->B * d->n);
+    w.s = cv.take<float>((size_t)d->B * 2 * d->n);
+    w.cov = cv.take<float>((size_t)d->B * d->N);
+    w.var1 = cv.take<float>((size_t)d->B * d->N);
+    w.secmax = cv.take<double>((size_t)d->B * d->L);
+    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
+    w.iters = cv.take<BampIter>((size_t)max_iter + 1);
+    w.bytes = cv.off;
+    return w;
+}
+
+__device__ __forceinline__ float* bvar(const BampK& P, int t) { return (t & 1) ? P.var1 : P.var0; }
+
+// v = |H|^2 var (bamp.py:59)
+__global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds);
+    using C = GemmCfg<128>;
+    for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
+        const int rho = e >> 7, cc = e & 127;
+        const int row = row0 + rho, col = col0 + cc;
+        if (row < P.B && col < P.n) P.v[(size_t)row * P.n + col] = lds[rho * C::LDC + cc];
+    }
+}
+
+// z = H xmmse - v (y - z) / u ; u = v + sigma2 ; s = (y - z) / u   (bamp.py:60-63)
+__global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const int twoN = 2 * P.N, twon = 2 * P.n;
+    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds);
+    using C = GemmCfg<128>;
+    for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
+        const int rho = e >> 6, cp = e & 63;           // complex column pair
+        const int row = row0 + rho, i = (col0 >> 1) + cp;
+        if (row < P.B && i < P.n) {
+            const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
+            const float hr = lds[rho * C::LDC + 2 * cp], hi = lds[rho * C::LDC + 2 * cp + 1];
+            const float yr = P.y[oc], yi = P.y[oc + 1];
+            const float vi = P.v[o], iu_old = P.invu[o];
+            const float zr = hr - (vi * (yr - P.z[oc])) * iu_old;
+            const float zi = hi - (vi * (yi - P.z[oc + 1])) * iu_old;
+            const float u = vi + P.sigma2;
+            const float iu = 1.0f / u;
+            P.z[oc] = zr; P.z[oc + 1] = zi;
+            P.invu[o] = iu;
+            P.s[oc] = (yr - zr) * iu; P.s[oc + 1] = (yi - zi) * iu;
+        }
+    }
+}
+
+// cov = 1 / (|H|^2^T (1/u))   (bamp.py:62)
+__global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds);
+    using C = GemmCfg<128>;
+    for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
+        const int rho = e >> 7, cc = e & 127;
+        const int row = row0 + rho, col = col0 + cc;
+        if (row < P.B && col < P.N) P.cov[(size_t)row * P.N + col] = 1.0f / lds[rho * C::LDC + cc];
+    }
+}
+
+struct BampDenoisePolicy {
+    const float* tile;
+    const float* cov;
+    int ldc, spr, M, N, row0, colc0;
+    float* xm;
+    float* var_new;
+    const float* var_prev;
+    double* secmax;
+    int L;
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * (sj * M + m));
+        rr = v.x; ri = v.y;
+        it = 1.0f / (cov[(size_t)(row0 + rho) * N + colc0 + sj * M + m] * 0.5f);   // tau = cov/2 (bamp.py:68)
+    }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const size_t o = (size_t)(row0 + rho) * N + colc0 + sj * M + m;
+        *reinterpret_cast<float2*>(xm + 2 * o) = make_float2(xr, xi);
+        var_new[o] = var;
+        pa.sumvar += (double)var;
+        pa.notclose += torch_close(var, var_prev[o]) ? 0u : 1u;     // bamp.py:140
+    }
+    __device__ __forceinline__ void section(int sec, double smax) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+    }
+};
+
+// xmap = xmmse + cov (H^H s) ; xmmse, var = denoiser(xmap, cov/2)   (bamp.py:63-64)
+template <int BN>
+__global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    using C = GemmCfg<BN>;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const int twoN = 2 * P.N, twon = 2 * P.n;
+    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds);
+    const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
+    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
+        const int rho = e / BN, cc = e % BN;
+        if (rho < nrows && cc < ncols) {
+            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+            const float cv = P.cov[(size_t)(row0 + rho) * P.N + ((col0 + cc) >> 1)];
+            const float xp = P.xm[o] + cv * lds[rho * C::LDC + cc];
+            P.xmap[o] = xp;
+            lds[rho * C::LDC + cc] = xp;
+        }
+    }
+    __syncthreads();
+    BampDenoisePolicy pol;
+    pol.tile = lds; pol.cov = P.cov; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.L = P.L;
+    pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2;
+    pol.xm = P.xm; pol.var_new = bvar(P, t); pol.var_prev = bvar(P, t + 1); pol.secmax = P.secmax;
+    PartAcc pa;
+    denoise_sections<true>(pol, nrows * pol.spr, P.M, P.c, pa);
+    part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
+}
+
+// reduction, exact float64 fix-up, allclose decision (bamp.py:140)
+__global__ __launch_bounds__(BRWG) void bamp_r(BampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    __shared__ unsigned s_nc[BRWG / 64];
+    __shared__ int s_cnt[BRWG / 64];
+    const BampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) P.iters[t + 1] = cur;
+        return;
+    }
+    PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
+    int fixed = 0;
+    if (part_danger(pa)) {
+        const double G = pa.maxabs;
+        float* vn = bvar(P, t);
+        const float* vp = bvar(P, t + 1);
+        int dnc = 0, cnt = 0;
+        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
+            if (!(P.secmax[sct] - G < AMP_DANGER)) continue;
+            ++cnt;
+            const size_t o0 = (size_t)sct * P.M;
+            auto ld = [&](int m, float& rr, float& ri, float& it) {
+                const float2 v = reinterpret_cast<const float2*>(P.xmap)[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (P.cov[o0 + m] * 0.5f);
+            };
+            auto st = [&](int m, float xr, float xi, float var) {
+                const size_t o = o0 + m;
+                dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(vn[o], vp[o]) ? 0 : 1);
+                reinterpret_cast<float2*>(P.xm)[o] = make_float2(xr, xi);
+                vn[o] = var;
+            };
+            exact_section_f64<true>(ld, st, P.M, P.c, G);
+        }
+        dnc = group_sum(dnc, 64);
+        cnt = group_sum(cnt, 64);
+        if ((threadIdx.x & 63) == 0) { s_nc[threadIdx.x >> 6] = (unsigned)dnc; s_cnt[threadIdx.x >> 6] = cnt; }
+        __syncthreads();
+        unsigned nc = 0;
+        for (int w = 0; w < BRWG / 64; ++w) { nc += s_nc[w]; fixed += s_cnt[w]; }
+        pa.notclose += nc;
+    }
+    if (threadIdx.x == 0) {
+        BampIter nx;
+        nx.stopped = pa.notclose == 0 ? 1 : 0;
+        nx.T = t + 1;
+        nx.fixed = fixed;
+        nx.pad = 0;
+        P.iters[t + 1] = nx;
+        if (nx.stopped || t + 1 == P.max_iter) {
+            amp_status s;
+            s.T = t + 1; s.nan_state = fixed > 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+            s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+            *P.status = s;
+        }
+    }
+}
+
+// Tracker (bamp.py:13-25): xmmse = 0, var(prev) = 1, z = y, u = 0 + sigma2 -> 1/u.
+__global__ void bamp_init_kernel(BampK P) {
+    const size_t BN_ = (size_t)P.B * P.N, Bn = (size_t)P.B * P.n;
+    const size_t tot = BN_ > Bn ? BN_ : Bn;
+    const float iu = 1.0f / P.sigma2;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+        if (e < BN_) {
+            reinterpret_cast<float2*>(P.xm)[e] = make_float2(0.f, 0.f);
+            P.var1[e] = 1.0f;
+        }
+        if (e < Bn) {
+            reinterpret_cast<float2*>(P.z)[e] = reinterpret_cast<const float2*>(P.y)[e];
+            P.invu[e] = iu;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        BampIter it;
+        it.stopped = 0; it.T = 0; it.fixed = 0; it.pad = 0;
+        P.iters[0] = it;
+    }
+}
+
+__global__ void bamp_output_kernel(BampK P) {
+    const int T = P.status->T;
+    if (((T - 1) & 1) == 0) return;
+    const size_t BN_ = (size_t)P.B * P.N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < BN_; e += (size_t)gridDim.x * blockDim.x)
+        P.var0[e] = P.var1[e];
+}
+
+static std::once_flag g_bamp_once;
+static int g_bamp_rc = 0;
+
+static int bamp_attrs() {
+    std::call_once(g_bamp_once, [] {
+        g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka1);
+        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka2);
+        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_kb1);
+        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_kb2<128>);
+        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<256>((const void*)bamp_kb2<256>);
+    });
+    return g_bamp_rc;
+}
+
+}  // namespace amp
+
 using namespace amp;
+
 extern "C" {
-size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter) { return (d && max_iter > 0) ? 256 : 0; }
-int amp_bamp_run(const amp_dims*, const amp_constellation*, const amp_bamp_args*, void*) {
-    set_error("amp_bamp_run: not implemented yet");
-    return AMP_E_ARG;
+
+size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter) {
+    if (!d || max_iter <= 0) return 0;
+    return bamp_carve(d, max_iter, nullptr).bytes;
 }
+
+int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
+    int rc = check_dims(d, c);
+    if (rc) return rc;
+    AMP_REQUIRE(a && a->H && a->y && a->xmap && a->xmmse && a->var && a->status && a->ws,
+                "amp_bamp_run: null pointer argument");
+    AMP_REQUIRE(a->max_iter > 0, "amp_bamp_run: max_iter must be positive");
+    AMP_REQUIRE(d->N % 4 == 0 && d->n % 4 == 0, "amp_bamp_run: N (%d) and n (%d) must be multiples of 4", d->N, d->n);
+    const BampWs w = bamp_carve(d, a->max_iter, a->ws);
+    AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_bamp_run: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
+    rc = bamp_attrs();
+    if (rc) return rc;
+    BampK P;
+    bamp_geometry(d, P);
+    P.max_iter = a->max_iter;
+    P.sigma2 = (float)a->noise_var;
+    P.Wabs2 = w.Wabs2; P.WH = w.WH; P.Wabs2T = w.Wabs2T; P.WHH = w.WHH;
+    P.y = (const float*)a->y; P.v = w.v; P.z = w.z; P.invu = w.invu; P.s = w.s; P.cov = w.cov;
+    P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.var0 = (float*)a->var; P.var1 = w.var1;
+    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.c = to_const(c);
+    hipStream_t st = (hipStream_t)stream;
+    const float2* H = (const float2*)a->H;
+    // weights, once per forward (Tracker: adj, abs2, abs2T, bamp.py:17-19)
+    if ((rc = build_abs2_weight(H, P.N, 1, P.n, P.N, (float*)P.Wabs2, P.kapA1, P.ncpA1, st))) return rc;
+    if ((rc = build_cweight(H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WH, P.kapA2, P.ncpA2, st))) return rc;
+    if ((rc = build_abs2_weight(H, 1, P.N, P.N, P.n, (float*)P.Wabs2T, P.kapB1, P.ncpB1, st))) return rc;
+    if ((rc = build_cweight(H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.kapB2, P.ncpB2, st))) return rc;
+    const size_t tot = std::max((size_t)P.B * P.N, (size_t)P.B * P.n);
+    const int g = (int)std::min<size_t>((tot + 255) / 256, 2048);
+    hipLaunchKernelGGL(bamp_init_kernel, dim3(g), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("bamp_init");
+    const int gr = cdiv(P.B, GBM);
+    for (int t = 0; t < P.max_iter; ++t) {
+        hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        if (P.bn == 128)
+            hipLaunchKernelGGL(bamp_kb2<128>, dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        else
+            hipLaunchKernelGGL(bamp_kb2<256>, dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+        hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, t);
+        AMP_LAUNCH_CHECK("bamp iteration");
+    }
+    hipLaunchKernelGGL(bamp_output_kernel, dim3((int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048)),
+                       dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("bamp_output");
+    return AMP_OK;
 }
+
+}  // extern "C"

@@ -202,7 +202,7 @@ size_t amp_map_decide_workspace_bytes(const amp_dims* d) {
 int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
                          const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
                          void* decisions, void* ws, size_t ws_bytes, void* stream) {
-    int rc = check_dims(d, c);
+    int rc = check_dims(d, c, false);
     if (rc) return rc;
     AMP_REQUIRE(xmap && xmmse && x && sym && idx && counts && ws, "amp_map_decide_count: null pointer argument");
     AMP_REQUIRE(ws_bytes >= amp_map_decide_workspace_bytes(d), "amp_map_decide_count: workspace too small");

@@ -110,7 +110,7 @@ size_t amp_block_denoise_workspace_bytes(const amp_dims* d) {
 int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void* r, int32_t tau_mode,
                       float tau_scalar, const void* tau_vec, void* xmmse, void* var, void* ws, size_t ws_bytes,
                       void* stream) {
-    int rc = check_dims(d, c);
+    int rc = check_dims(d, c, false);
     if (rc) return rc;
     AMP_REQUIRE(r && xmmse && ws, "amp_block_denoise: null pointer argument");
     AMP_REQUIRE(tau_mode >= 0 && tau_mode <= 2, "amp_block_denoise: tau_mode %d", tau_mode);

@@ -63,7 +63,7 @@ inline Const to_const(const amp_constellation* c) {
     return k;
 }
 
-int check_dims(const amp_dims* d, const amp_constellation* c);
+int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
 
 // Column tile width of the section-fused GEMMs: a multiple of 2M so no section straddles
 // two workgroups.

@@ -1,10 +1,389 @@
-// amp_scamp.hip — SCAMP detector (placeholder until the fused kernels land).
+// amp_scamp.hip — SCAMP (spatially coupled SPARC AMP), device-resident iteration loop.
+//
+// Restates SCAMP.forward (scamp.py:77-107), Tracker (scamp.py:8-25) and
+// SCAMPLayer.forward (scamp.py:43-59):
+//   gamma = W psi / Lc ; b = gamma / phi ; z = y - A xmmse + b z ; phi = sigma2 + gamma ;
+//   tau = L / (W^T (1/phi)) / Mr ; xmap = xmmse + tau (A^H (z / phi)) ;
+//   xmmse = denoiser(xmap, tau/2) (mean only, scamp.py:61-68) ;
+//   psi = 1 - sum_{block} |xmmse|^2 / Na ; early exit on allclose(psi) (scamp.py:105).
+// Per iteration: two fp32-MFMA GEMM launches with fused epilogues + one reduction /
+// exact-float64 fix-up workgroup.  The second GEMM's column tile holds whole coupling
+// blocks (2*Nt columns) so psi is formed in its epilogue.
+#include <algorithm>
+#include <mutex>
+
+#include "amp_denoise.h"
+#include "amp_gemm.h"
 #include "amp_host.h"
+
+namespace amp {
+
+constexpr int SRWG = 1024;
+constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in registers / LDS
+
+struct alignas(16) ScampIter {
+    int32_t stopped, T, fixed, pad;
+};
+
+struct ScampK {
+    int B, N, n, L, M, Nt, Nr, Na, Lin, Lout, bn;
+    int kapA, ncpA, kapB, ncpB;
+    int nblk, max_iter;
+    float sigma2;          // f32(noise_var) (scamp.py:51)
+    const float* W;        // [Lout][Lin]
+    const float* WA;       // [ncpA][kapA]  A xmmse
+    const float* WAH;      // [ncpB][kapB]  A^H (z/phi)
+    const float* y;        // [B][2n]
+    float* z;              // [B][2n]
+    float* s;              // [B][2n] z / phi_use
+    float* phi;            // [2][B][Lout] ping-pong
+    float* tau;            // [B][Lin] (per iteration)
+    float* xmap;           // caller [B][2N]
+    float* xm;             // caller [B][2N]
+    float* psi0;           // caller's psi [B][Lin] (even iterations)
+    float* psi1;           // workspace     (odd iterations)
+    double* secmax;        // [B*L]
+    Partial* parts;
+    ScampIter* iters;
+    amp_status* status;
+    Const c;
+};
+
+struct ScampWs {
+    float *WA, *WAH, *z, *s, *phi, *tau, *psi1;
+    double* secmax;
+    Partial* parts;
+    ScampIter* iters;
+    size_t bytes;
+};
+
+static int scamp_bn(const amp_dims* d) { return (2 * d->Nt <= 128) ? 128 : 256; }
+
+static void scamp_geometry(const amp_dims* d, ScampK& P) {
+    P.B = d->B; P.N = d->N; P.n = d->n; P.L = d->L; P.M = d->M;
+    P.Nt = d->Nt; P.Nr = d->Nr; P.Na = d->Na; P.Lin = d->Lin; P.Lout = d->Lout;
+    P.bn = scamp_bn(d);
+    P.kapA = round_up(2 * d->N, GBK); P.ncpA = round_up(2 * d->n, 128);
+    P.kapB = round_up(2 * d->n, GBK); P.ncpB = round_up(2 * d->N, P.bn);
+    P.nblk = cdiv(d->B, GBM) * (P.ncpB / P.bn);
+}
+
+static ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
+    ScampK P;
+    scamp_geometry(d, P);
+    Carve cv(base);
+    ScampWs w;
+    w.WA = cv.take<float>((size_t)P.ncpA * P.kapA);
+    w.WAH = cv.take<float>((size_t)P.ncpB * P.kapB);
+    w.z = cv.take<float>((size_t)d->B * 2 * d->n);
+    w.s = cv.take<float>((size_t)d->B * 2 * d->n);
+    w.phi = cv.take<float>((size_t)2 * d->B * d->Lout);
+    w.tau = cv.take<float>((size_t)d->B * d->Lin);
+    w.psi1 = cv.take<float>((size_t)d->B * d->Lin);
+    w.secmax = cv.take<double>((size_t)d->B * d->L);
+    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
+    w.iters = cv.take<ScampIter>((size_t)max_iter + 1);
+    w.bytes = cv.off;
+    return w;
+}
+
+__device__ __forceinline__ float* spsi(const ScampK& P, int t) { return (t & 1) ? P.psi1 : P.psi0; }
+__device__ __forceinline__ float* sphi(const ScampK& P, int t) { return P.phi + (size_t)(t & 1) * P.B * P.Lout; }
+
+// gamma[lo] = (W psi)[lo] / Lc (scamp.py:45), float32 as torch's [Lout x Lin] @ [Lin] product
+__device__ __forceinline__ float scamp_gamma(const ScampK& P, const float* psi_row, int lo) {
+    float g = 0.f;
+    for (int lc = 0; lc < P.Lin; ++lc) g += P.W[lo * P.Lin + lc] * psi_row[lc];
+    return g / (float)P.Lin;
+}
+
+// z = y - A xmmse + b z ; phi = sigma2 + gamma ; s = z / phi   (scamp.py:45-51, 57)
+__global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const int twoN = 2 * P.N, twon = 2 * P.n;
+    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds);
+    using C = GemmCfg<128>;
+    const float* psi = spsi(P, t + 1);               // psi of iteration t-1 (ones at t = 0)
+    const float* phi_old = sphi(P, t + 1);           // +inf at t = 0 (scamp.py:19)
+    float* phi_new = sphi(P, t);
+    for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
+        const int rho = e >> 6, cp = e & 63;
+        const int row = row0 + rho, i = (col0 >> 1) + cp;
+        if (row < P.B && i < P.n) {
+            const int lo = i / P.Nr;
+            const float gma = scamp_gamma(P, psi + (size_t)row * P.Lin, lo);
+            const float b = gma / phi_old[(size_t)row * P.Lout + lo];
+            const size_t oc = (size_t)row * twon + 2 * i;
+            const float ar = lds[rho * C::LDC + 2 * cp], ai = lds[rho * C::LDC + 2 * cp + 1];
+            const float zr = (P.y[oc] - ar) + b * P.z[oc];
+            const float zi = (P.y[oc + 1] - ai) + b * P.z[oc + 1];
+            const float ph = P.sigma2 + gma;
+            const float iph = 1.0f / ph;
+            P.z[oc] = zr; P.z[oc + 1] = zi;
+            P.s[oc] = zr * iph; P.s[oc + 1] = zi * iph;
+            if (i % P.Nr == 0) phi_new[(size_t)row * P.Lout + lo] = ph;
+        }
+    }
+}
+
+struct ScampDenoisePolicy {
+    const float* tile;
+    const float* tau_tile;   // LDS [32][Lin] tau of the tile's rows
+    int ldc, spr, M, N, Nt, L, row0, colc0, Lin;
+    float* xm;
+    double* secmax;
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const int cc = sj * M + m;
+        const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * cc);
+        rr = v.x; ri = v.y;
+        it = 1.0f / (tau_tile[rho * Lin + (colc0 + cc) / Nt] * 0.5f);   // tau_use / 2 (scamp.py:63)
+    }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float, PartAcc&) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        const size_t o = (size_t)(row0 + rho) * N + colc0 + sj * M + m;
+        *reinterpret_cast<float2*>(xm + 2 * o) = make_float2(xr, xi);
+    }
+    __device__ __forceinline__ void section(int sec, double smax) const {
+        const int rho = sec / spr, sj = sec - rho * spr;
+        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+    }
+};
+
+// tau = L / (W^T (1/phi)) / Mr ; xmap = xmmse + tau (A^H s) ; xmmse = denoiser ; psi   (scamp.py:53-59)
+template <int BN>
+__global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (P.iters[t].stopped) return;
+    using C = GemmCfg<BN>;
+    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const int twoN = 2 * P.N, twon = 2 * P.n;
+    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds);
+    const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
+    const int lc0 = (col0 / 2) / P.Nt, nlc = max(1, (ncols / 2) / P.Nt);   // coupling blocks in this tile
+    float* tau_t = lds + C::CTILE_FLOATS;                                    // [32][Lin]
+    const float* phi = sphi(P, t);
+    for (int e = threadIdx.x; e < GBM * P.Lin; e += AMP_WG) {
+        const int rho = e / P.Lin, lc = e % P.Lin;
+        float tv = 0.f;
+        if (rho < nrows) {
+            float acc = 0.f;   // (W^T (1/phi))[lc] in float32
+            for (int lo = 0; lo < P.Lout; ++lo)
+                acc += P.W[lo * P.Lin + lc] * (1.0f / phi[(size_t)(row0 + rho) * P.Lout + lo]);
+            tv = ((1.0f / acc) * (float)P.L) / (float)P.Nr;          // L / x = recip(x) * L ; / Mr
+            if (blockIdx.y == 0) P.tau[(size_t)(row0 + rho) * P.Lin + lc] = tv;
+        }
+        tau_t[rho * P.Lin + lc] = tv;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
+        const int rho = e / BN, cc = e % BN;
+        if (rho < nrows && cc < ncols) {
+            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+            const float tv = tau_t[rho * P.Lin + ((col0 + cc) >> 1) / P.Nt];
+            const float xp = P.xm[o] + tv * lds[rho * C::LDC + cc];
+            P.xmap[o] = xp;
+            lds[rho * C::LDC + cc] = xp;
+        }
+    }
+    __syncthreads();
+    ScampDenoisePolicy pol;
+    pol.tile = lds; pol.tau_tile = tau_t; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.Nt = P.Nt; pol.L = P.L;
+    pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2; pol.Lin = P.Lin;
+    pol.xm = P.xm; pol.secmax = P.secmax;
+    PartAcc pa;
+    denoise_sections<false>(pol, nrows * pol.spr, P.M, P.c, pa);
+    __syncthreads();
+    // psi = 1 - sum_block |xmmse|^2 / Na (scamp.py:59) from the freshly written tile
+    const float* psi_prev = spsi(P, t + 1);
+    float* psi_new = spsi(P, t);
+    unsigned nc = 0;
+    for (int e = threadIdx.x; e < GBM * nlc; e += AMP_WG) {
+        const int rho = e / nlc, b = e % nlc;
+        if (rho >= nrows) continue;
+        const int lc = lc0 + b;
+        const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)(row0 + rho) * P.N + (size_t)lc * P.Nt;
+        double ssum = 0.0;
+        for (int m = 0; m < P.Nt; ++m) {
+            const float2 v = xr[m];
+            const float a = (float)sqrt((double)v.x * v.x + (double)v.y * v.y);   // torch abs (hypot)
+            ssum += (double)(a * a);
+        }
+        const float ps = 1.0f - (float)ssum / (float)P.Na;
+        const size_t o = (size_t)(row0 + rho) * P.Lin + lc;
+        nc += torch_close(ps, psi_prev[o]) ? 0u : 1u;                // scamp.py:105
+        psi_new[o] = ps;
+    }
+    pa.notclose += nc;
+    part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds);
+}
+
+// reduction, exact float64 fix-up of out-of-range sections (+ their psi), allclose(psi)
+__global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    __shared__ unsigned s_nc[SRWG / 64];
+    __shared__ int s_cnt[SRWG / 64];
+    const ScampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) P.iters[t + 1] = cur;
+        return;
+    }
+    PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
+    int fixed = 0;
+    if (part_danger(pa)) {
+        const double G = pa.maxabs;
+        int cnt = 0, dnc = 0;
+        // sections, then every coupling block that holds a recomputed section
+        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
+            if (!(P.secmax[sct] - G < AMP_DANGER)) continue;
+            ++cnt;
+            const size_t o0 = (size_t)sct * P.M;
+            const int b = sct / P.L, lc = (int)((o0 % (size_t)P.N) / P.Nt);
+            const float tv = P.tau[(size_t)b * P.Lin + lc];
+            auto ld = [&](int m, float& rr, float& ri, float& it) {
+                const float2 v = reinterpret_cast<const float2*>(P.xmap)[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
+            };
+            auto st = [&](int m, float xr, float xi, float) {
+                reinterpret_cast<float2*>(P.xm)[o0 + m] = make_float2(xr, xi);
+            };
+            exact_section_f64<false>(ld, st, P.M, P.c, G);
+        }
+        __syncthreads();
+        const float* psi_prev = spsi(P, t + 1);
+        float* psi_new = spsi(P, t);
+        const int spb = P.Nt / P.M;   // sections per coupling block
+        for (int blk = threadIdx.x; blk < P.B * P.Lin; blk += blockDim.x) {
+            bool hit = false;
+            for (int j = 0; j < spb && !hit; ++j) hit = P.secmax[(size_t)blk * spb + j] - G < AMP_DANGER;
+            if (!hit) continue;
+            const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
+            double ssum = 0.0;
+            for (int m = 0; m < P.Nt; ++m) {
+                const float a = (float)sqrt((double)xr[m].x * xr[m].x + (double)xr[m].y * xr[m].y);
+                ssum += (double)(a * a);
+            }
+            const float ps = 1.0f - (float)ssum / (float)P.Na;
+            dnc += (torch_close(ps, psi_prev[blk]) ? 0 : 1) - (torch_close(psi_new[blk], psi_prev[blk]) ? 0 : 1);
+            psi_new[blk] = ps;
+        }
+        dnc = group_sum(dnc, 64);
+        cnt = group_sum(cnt, 64);
+        if ((threadIdx.x & 63) == 0) { s_nc[threadIdx.x >> 6] = (unsigned)dnc; s_cnt[threadIdx.x >> 6] = cnt; }
+        __syncthreads();
+        unsigned nc = 0;
+        for (int w = 0; w < SRWG / 64; ++w) { nc += s_nc[w]; fixed += s_cnt[w]; }
+        pa.notclose += nc;
+    }
+    if (threadIdx.x == 0) {
+        ScampIter nx;
+        nx.stopped = pa.notclose == 0 ? 1 : 0;
+        nx.T = t + 1;
+        nx.fixed = fixed;
+        nx.pad = 0;
+        P.iters[t + 1] = nx;
+        if (nx.stopped || t + 1 == P.max_iter) {
+            amp_status s;
+            s.T = t + 1; s.nan_state = fixed > 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+            s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+            *P.status = s;
+        }
+    }
+}
+
+// Tracker (scamp.py:9-25): z = y, psi = 1, phi = inf, xmmse = 0
+__global__ void scamp_init_kernel(ScampK P) {
+    const size_t BN_ = (size_t)P.B * P.N, Bn = (size_t)P.B * P.n, BL = (size_t)P.B * P.Lout;
+    const size_t tot = std::max(std::max(BN_, Bn), BL);
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+        if (e < BN_) reinterpret_cast<float2*>(P.xm)[e] = make_float2(0.f, 0.f);
+        if (e < Bn) reinterpret_cast<float2*>(P.z)[e] = reinterpret_cast<const float2*>(P.y)[e];
+        if (e < (size_t)P.B * P.Lin) P.psi1[e] = 1.0f;
+        if (e < BL) P.phi[BL + e] = INFINITY;        // phi buffer of "iteration -1"
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ScampIter it;
+        it.stopped = 0; it.T = 0; it.fixed = 0; it.pad = 0;
+        P.iters[0] = it;
+    }
+}
+
+__global__ void scamp_output_kernel(ScampK P) {
+    const int T = P.status->T;
+    if (((T - 1) & 1) == 0) return;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < (size_t)P.B * P.Lin;
+         e += (size_t)gridDim.x * blockDim.x)
+        P.psi0[e] = P.psi1[e];
+}
+
+static std::once_flag g_scamp_once;
+static int g_scamp_rc = 0;
+
+static int scamp_attrs() {
+    std::call_once(g_scamp_once, [] {
+        g_scamp_rc = set_lds_attr<128>((const void*)scamp_ka);
+        if (!g_scamp_rc) g_scamp_rc = set_lds_attr<128>((const void*)scamp_kb<128>);
+        if (!g_scamp_rc) g_scamp_rc = set_lds_attr<256>((const void*)scamp_kb<256>);
+    });
+    return g_scamp_rc;
+}
+
+}  // namespace amp
+
 using namespace amp;
+
 extern "C" {
-size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter) { return (d && max_iter > 0) ? 256 : 0; }
-int amp_scamp_run(const amp_dims*, const amp_constellation*, const amp_scamp_args*, void*) {
-    set_error("amp_scamp_run: not implemented yet");
-    return AMP_E_ARG;
+
+size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter) {
+    if (!d || max_iter <= 0) return 0;
+    return scamp_carve(d, max_iter, nullptr).bytes;
 }
+
+int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
+    int rc = check_dims(d, c);
+    if (rc) return rc;
+    AMP_REQUIRE(a && a->W && a->A && a->y && a->xmap && a->xmmse && a->psi && a->status && a->ws,
+                "amp_scamp_run: null pointer argument");
+    AMP_REQUIRE(a->max_iter > 0, "amp_scamp_run: max_iter must be positive");
+    AMP_REQUIRE(is_pow2(d->Nt) && 2 * d->Nt <= 256, "amp_scamp_run: Nt = %d must be a power of two <= 128", d->Nt);
+    AMP_REQUIRE(d->Lin <= SMAXLIN, "amp_scamp_run: Lin = %d > %d", d->Lin, SMAXLIN);
+    const ScampWs w = scamp_carve(d, a->max_iter, a->ws);
+    AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_scamp_run: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
+    rc = scamp_attrs();
+    if (rc) return rc;
+    ScampK P;
+    scamp_geometry(d, P);
+    P.max_iter = a->max_iter;
+    P.sigma2 = (float)a->noise_var;
+    P.W = (const float*)a->W;
+    P.WA = w.WA; P.WAH = w.WAH;
+    P.y = (const float*)a->y; P.z = w.z; P.s = w.s; P.phi = w.phi; P.tau = w.tau;
+    P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
+    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.c = to_const(c);
+    hipStream_t st = (hipStream_t)stream;
+    const float2* A = (const float2*)a->A;
+    if ((rc = build_cweight(A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.kapA, P.ncpA, st))) return rc;
+    if ((rc = build_cweight(A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WAH, P.kapB, P.ncpB, st))) return rc;
+    const size_t tot = std::max(std::max((size_t)P.B * P.N, (size_t)P.B * P.n), (size_t)P.B * P.Lout);
+    hipLaunchKernelGGL(scamp_init_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("scamp_init");
+    const int gr = cdiv(P.B, GBM);
+    const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
+    for (int t = 0; t < P.max_iter; ++t) {
+        hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        if (P.bn == 128)
+            hipLaunchKernelGGL(scamp_kb<128>, dim3(gr, P.ncpB / 128), dim3(AMP_WG), ldsB, st, P, t);
+        else
+            hipLaunchKernelGGL(scamp_kb<256>, dim3(gr, P.ncpB / 256), dim3(AMP_WG), ldsB, st, P, t);
+        hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, t);
+        AMP_LAUNCH_CHECK("scamp iteration");
+    }
+    hipLaunchKernelGGL(scamp_output_kernel, dim3(64), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("scamp_output");
+    return AMP_OK;
 }
+
+}  // extern "C"

@@ -17,15 +17,17 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
-int check_dims(const amp_dims* d, const amp_constellation* c) {
+int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled) {
     AMP_REQUIRE(d && c, "null dims/constellation");
     AMP_REQUIRE(d->B > 0 && d->Nt > 0 && d->Na > 0 && d->Nr > 0 && d->Lin > 0 && d->Lout > 0, "non-positive dimension");
     AMP_REQUIRE(d->Nt % d->Na == 0, "Na must divide Nt (config.py:133)");
     AMP_REQUIRE(d->M == d->Nt / d->Na && d->L == d->Na * d->Lin && d->N == d->Nt * d->Lin && d->n == d->Nr * d->Lout,
                 "inconsistent derived dimensions");
     AMP_REQUIRE(is_pow2(d->M), "section size M = Nt/Na = %d must be a power of two", d->M);
-    AMP_REQUIRE(2 * d->M <= 256, "section size M = %d > 128 not supported", d->M);
     AMP_REQUIRE(c->K >= 1 && c->K <= AMP_MAX_K, "constellation size K = %d out of range", c->K);
+    if (!tiled) return AMP_OK;   // the decision / standalone denoiser have no GEMM tiling
+    AMP_REQUIRE(2 * d->M <= 256, "section size M = %d > 128 not supported by the fused detectors", d->M);
+    AMP_REQUIRE(d->N % 2 == 0 && d->n % 2 == 0, "N (%d) and n (%d) must be even", d->N, d->n);
     const int bn = section_bn(d);
     AMP_REQUIRE(2 * d->N <= bn || (2 * d->N) % bn == 0, "2N = %d must be <= %d or a multiple of it", 2 * d->N, bn);
     return AMP_OK;
