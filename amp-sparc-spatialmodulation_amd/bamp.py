@@ -41,7 +41,7 @@ class BAMP(nn.Module):
         self._key = None
         self.last = None
 
-    def _buffers(self, dev, B, N, wsb):
+    def _ensure_buffers(self, dev, B, N, wsb):
         key = (str(dev), B, N, wsb)
         if key != self._key:
             self.xmap = torch.empty(B, N, dtype=torch.complex64, device=dev)
@@ -60,7 +60,7 @@ class BAMP(nn.Module):
         d, c = cfg.dims(), cfg.constellation()
         lib = nat.lib()
         wsb = lib.amp_bamp_workspace_bytes(C.byref(d), cfg.N_Layers)
-        self._buffers(y.device, B, N, wsb)
+        self._ensure_buffers(y.device, B, N, wsb)
         a = nat.AmpBampArgs()
         a.H, a.y = nat.dptr(H, name='H'), nat.dptr(y, name='y')
         a.max_iter = cfg.N_Layers

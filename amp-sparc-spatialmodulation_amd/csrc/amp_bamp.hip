@@ -20,7 +20,7 @@ namespace amp {
 constexpr int BRWG = 1024;
 
 struct alignas(16) BampIter {
-    int32_t stopped, T, fixed, pad;
+    int32_t stopped, T, fixed, fixed_all;
 };
 
 struct BampK {
@@ -217,7 +217,11 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, int t) {
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
     int fixed = 0;
-    if (part_danger(pa)) {
+    if (part_allnan(pa)) {
+        if (!cur.fixed_all) nan_fill(P.xm, bvar(P, t), (size_t)P.B * P.N);
+        pa.notclose = 1;
+        fixed = -1;
+    } else if (part_danger(pa)) {
         const double G = pa.maxabs;
         float* vn = bvar(P, t);
         const float* vp = bvar(P, t + 1);
@@ -251,11 +255,11 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, int t) {
         nx.stopped = pa.notclose == 0 ? 1 : 0;
         nx.T = t + 1;
         nx.fixed = fixed;
-        nx.pad = 0;
+        nx.fixed_all = (fixed < 0) ? 1 : 0;
         P.iters[t + 1] = nx;
         if (nx.stopped || t + 1 == P.max_iter) {
             amp_status s;
-            s.T = t + 1; s.nan_state = fixed > 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+            s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
             s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
             *P.status = s;
         }
@@ -279,7 +283,7 @@ __global__ void bamp_init_kernel(BampK P) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         BampIter it;
-        it.stopped = 0; it.T = 0; it.fixed = 0; it.pad = 0;
+        it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0;
         P.iters[0] = it;
     }
 }

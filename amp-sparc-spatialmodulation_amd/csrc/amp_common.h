@@ -43,8 +43,8 @@ struct alignas(16) Partial {
 struct alignas(16) VampIter {
     int32_t stopped;   // 1: the loop already broke (vamp.py:185-186); iteration is a no-op
     int32_t T;         // executed iterations once stopped
-    int32_t fixed;     // sections of the previous iteration recomputed in exact float64
-    int32_t pad0;
+    int32_t fixed;     // sections of the previous iteration recomputed in exact float64 (-1: all NaN)
+    int32_t fixed_all; // the previous iteration was set all-NaN (later ones stay NaN by propagation)
     float vr;          // var_ratio = noise_var / sigma2_tilde       (vamp.py:66)
     float alpha;       // clamped alpha                              (vamp.py:75-77)
     float inv1ma;      // 1 / (1 - alpha) (c64 / f32 == mul by recip) (vamp.py:79)
@@ -186,6 +186,19 @@ __device__ __forceinline__ PartAcc part_reduce_all(const Partial* src, int nblk,
 // recomputed with the reference's exact float64 arithmetic (exact_section_f64).
 #define AMP_DANGER (-700.0)
 __device__ __forceinline__ bool part_danger(const PartAcc& p) { return p.minsecmax - p.maxabs < AMP_DANGER; }
+
+// torch's x.abs().max() propagates NaN: once any logit of the batch is NaN or +-inf the
+// reference's shift G is NaN / inf and exp(xi - G) makes EVERY section NaN (0/0 or NaN).
+__device__ __forceinline__ bool part_allnan(const PartAcc& p) { return !(p.maxabs <= 1.7976931348623157e308); }
+
+// One workgroup writes NaN over n complex entries (and n var entries when var != nullptr).
+__device__ __forceinline__ void nan_fill(float* xm, float* var, size_t n) {
+    const float q = __int_as_float(0x7fc00000);
+    for (size_t e = threadIdx.x; e < n; e += blockDim.x) {
+        reinterpret_cast<float2*>(xm)[e] = make_float2(q, q);
+        if (var) var[e] = q;
+    }
+}
 
 struct Const {
     int K;

@@ -22,7 +22,7 @@ constexpr int SRWG = 1024;
 constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in registers / LDS
 
 struct alignas(16) ScampIter {
-    int32_t stopped, T, fixed, pad;
+    int32_t stopped, T, fixed, fixed_all;
 };
 
 struct ScampK {
@@ -232,7 +232,15 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
     int fixed = 0;
-    if (part_danger(pa)) {
+    if (part_allnan(pa)) {
+        if (!cur.fixed_all) {
+            nan_fill(P.xm, nullptr, (size_t)P.B * P.N);
+            float* psi_new = spsi(P, t);
+            for (int e = threadIdx.x; e < P.B * P.Lin; e += blockDim.x) psi_new[e] = __int_as_float(0x7fc00000);
+        }
+        pa.notclose = 1;
+        fixed = -1;
+    } else if (part_danger(pa)) {
         const double G = pa.maxabs;
         int cnt = 0, dnc = 0;
         // sections, then every coupling block that holds a recomputed section
@@ -282,11 +290,11 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
         nx.stopped = pa.notclose == 0 ? 1 : 0;
         nx.T = t + 1;
         nx.fixed = fixed;
-        nx.pad = 0;
+        nx.fixed_all = (fixed < 0) ? 1 : 0;
         P.iters[t + 1] = nx;
         if (nx.stopped || t + 1 == P.max_iter) {
             amp_status s;
-            s.T = t + 1; s.nan_state = fixed > 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+            s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
             s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
             *P.status = s;
         }
@@ -305,7 +313,7 @@ __global__ void scamp_init_kernel(ScampK P) {
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ScampIter it;
-        it.stopped = 0; it.T = 0; it.fixed = 0; it.pad = 0;
+        it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0;
         P.iters[0] = it;
     }
 }

@@ -127,7 +127,7 @@ __device__ void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, flo
 __global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
     __shared__ __attribute__((aligned(16))) float lds[64];
     VampIter it;
-    it.stopped = 0; it.T = 0; it.fixed = 0; it.pad0 = 0; it.G = 0.0;
+    it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0; it.G = 0.0;
     it.pad1[0] = it.pad1[1] = it.pad1[2] = 0.f;
     it.dxdr_prev = 0.f;   // r~ = (xmmse - 0 * r) * 1 = sparsity at t = 0 (vamp.py:25)
     it.ns_prev = 1.f;
@@ -250,7 +250,13 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk2, P.nblk2, lds);
     int fixed = 0;
-    if (part_danger(pa)) {
+    if (part_allnan(pa)) {
+        // the reference's G is NaN / inf: every section of this iteration is NaN
+        if (!cur.fixed_all) nan_fill(P.xm, var_buf(P, t), (size_t)P.B * P.N);
+        pa.sumvar = __longlong_as_double(0x7ff8000000000000LL);
+        pa.notclose = 1;
+        fixed = -1;
+    } else if (part_danger(pa)) {
         // exact float64 recompute of every section below the danger line (rare)
         const double G = pa.maxabs;
         const double* sm = P.secmax + (size_t)(t & 1) * P.B * P.L;
@@ -295,7 +301,7 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
         __syncthreads();
     }
     VampIter nx;
-    nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.pad0 = 0; nx.G = pa.maxabs;
+    nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.fixed_all = (fixed < 0) ? 1 : 0; nx.G = pa.maxabs;
     nx.pad1[0] = nx.pad1[1] = nx.pad1[2] = 0.f;
     if (pa.notclose == 0) {                                              // vamp.py:185-186
         nx = cur;
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
         if (nx.stopped || t + 1 == P.max_iter) {
             amp_status s;
             s.T = nx.stopped ? nx.T : P.max_iter;
-            s.nan_state = fixed > 0 ? 1 : 0;
+            s.nan_state = fixed != 0 ? 1 : 0;
             s.stopped = nx.stopped;
             s.pad = 0;
             s.last_scalar[0] = cur.s2t; s.last_scalar[1] = cur.alpha; s.last_scalar[2] = cur.sigma2;

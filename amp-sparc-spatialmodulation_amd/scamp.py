@@ -44,7 +44,7 @@ class SCAMP(nn.Module):
         self._key = None
         self.last = None
 
-    def _buffers(self, dev, B, N, Lin, wsb):
+    def _ensure_buffers(self, dev, B, N, Lin, wsb):
         key = (str(dev), B, N, Lin, wsb)
         if key != self._key:
             self.xmap = torch.empty(B, N, dtype=torch.complex64, device=dev)
@@ -64,7 +64,7 @@ class SCAMP(nn.Module):
         d, c = cfg.dims(), cfg.constellation()
         lib = nat.lib()
         wsb = lib.amp_scamp_workspace_bytes(C.byref(d), cfg.N_Layers)
-        self._buffers(y.device, B, N, cfg.Lin, wsb)
+        self._ensure_buffers(y.device, B, N, cfg.Lin, wsb)
         a = nat.AmpScampArgs()
         a.W, a.A, a.y = nat.dptr(W, torch.float32, 'W'), nat.dptr(A, name='A'), nat.dptr(y, name='y')
         a.max_iter = cfg.N_Layers
