@@ -42,7 +42,8 @@ struct BampK {
     float* xm;             // [B][2N]  caller
     float* var0;           // caller's var (even iterations)
     float* var1;           // workspace  (odd iterations)
-    double* secmax;        // [B*L]
+    float* secmax;         // [B*L] per-section max logit (fast path)
+    float* secabs;         // [B*L] per-section max |logit|
     Partial* parts;        // [max_iter][nblk]
     BampIter* iters;       // [max_iter + 1]
     amp_status* status;
@@ -51,7 +52,7 @@ struct BampK {
 
 struct BampWs {
     float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
-    double* secmax;
+    float *secmax, *secabs;
     Partial* parts;
     BampIter* iters;
     size_t bytes;
@@ -82,7 +83,8 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.s = cv.take<float>((size_t)d->B * 2 * d->n);
     w.cov = cv.take<float>((size_t)d->B * d->N);
     w.var1 = cv.take<float>((size_t)d->B * d->N);
-    w.secmax = cv.take<double>((size_t)d->B * d->L);
+    w.secmax = cv.take<float>((size_t)d->B * d->L);
+    w.secabs = cv.take<float>((size_t)d->B * d->L);
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
     w.iters = cv.take<BampIter>((size_t)max_iter + 1);
     w.bytes = cv.off;
@@ -153,7 +155,8 @@ struct BampDenoisePolicy {
     float* xm;
     float* var_new;
     const float* var_prev;
-    double* secmax;
+    float* secmax;
+    float* secabs;
     int L;
     __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
         const int rho = sec / spr, sj = sec - rho * spr;
@@ -169,14 +172,16 @@ struct BampDenoisePolicy {
         pa.sumvar += (double)var;
         pa.notclose += torch_close(var, var_prev[o]) ? 0u : 1u;     // bamp.py:140
     }
-    __device__ __forceinline__ void section(int sec, double smax) const {
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
         const int rho = sec / spr, sj = sec - rho * spr;
-        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+        const size_t o = (size_t)(row0 + rho) * L + (colc0 / M) + sj;
+        secmax[o] = smax;
+        secabs[o] = sabs;
     }
 };
 
 // xmap = xmmse + cov (H^H s) ; xmmse, var = denoiser(xmap, cov/2)   (bamp.py:63-64)
-template <int BN>
+template <int BN, int KK>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -199,17 +204,17 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
     BampDenoisePolicy pol;
     pol.tile = lds; pol.cov = P.cov; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.L = P.L;
     pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2;
-    pol.xm = P.xm; pol.var_new = bvar(P, t); pol.var_prev = bvar(P, t + 1); pol.secmax = P.secmax;
+    pol.xm = P.xm; pol.var_new = bvar(P, t); pol.var_prev = bvar(P, t + 1); pol.secmax = P.secmax; pol.secabs = P.secabs;
     PartAcc pa;
-    denoise_sections<true>(pol, nrows * pol.spr, P.M, P.c, pa);
+    denoise_sections<true, KK>(pol, nrows * pol.spr, P.M, P.c, pa);
     part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
 }
 
 // reduction, exact float64 fix-up, allclose decision (bamp.py:140)
-__global__ __launch_bounds__(BRWG) void bamp_r(BampK P, int t) {
+__global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
     __shared__ unsigned s_nc[BRWG / 64];
-    __shared__ int s_cnt[BRWG / 64];
+    __shared__ double s_d[BRWG / 64];
     const BampIter cur = P.iters[t];
     if (cur.stopped) {
         if (threadIdx.x == 0) P.iters[t + 1] = cur;
@@ -222,32 +227,36 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, int t) {
         pa.notclose = 1;
         fixed = -1;
     } else if (part_danger(pa)) {
-        const double G = pa.maxabs;
         float* vn = bvar(P, t);
         const float* vp = bvar(P, t + 1);
-        int dnc = 0, cnt = 0;
-        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
-            if (!(P.secmax[sct] - G < AMP_DANGER)) continue;
-            ++cnt;
-            const size_t o0 = (size_t)sct * P.M;
-            auto ld = [&](int m, float& rr, float& ri, float& it) {
-                const float2 v = reinterpret_cast<const float2*>(P.xmap)[o0 + m];
-                rr = v.x; ri = v.y; it = 1.0f / (P.cov[o0 + m] * 0.5f);
+        const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+        const float* cov = P.cov;
+        float2* x2 = reinterpret_cast<float2*>(P.xm);
+        const int M = P.M;
+        int dnc = 0;
+        auto ldf = [=](int sct) {
+            const size_t o0 = (size_t)sct * M;
+            return [=](int m, float& rr, float& ri, float& it) {
+                const float2 v = xp2[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (cov[o0 + m] * 0.5f);
             };
-            auto st = [&](int m, float xr, float xi, float var) {
+        };
+        auto stf = [&](int sct) {
+            const size_t o0 = (size_t)sct * M;
+            return [&, o0](int m, float xr, float xi, float var) {
                 const size_t o = o0 + m;
                 dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(vn[o], vp[o]) ? 0 : 1);
-                reinterpret_cast<float2*>(P.xm)[o] = make_float2(xr, xi);
+                x2[o] = make_float2(xr, xi);
                 vn[o] = var;
             };
-            exact_section_f64<true>(ld, st, P.M, P.c, G);
-        }
+        };
+        double G;
+        fixed = fixup_sections<true>(P.B * P.L, M, P.secmax, P.secabs, pa.maxabs, c64, ldf, stf, &G, s_d);
         dnc = group_sum(dnc, 64);
-        cnt = group_sum(cnt, 64);
-        if ((threadIdx.x & 63) == 0) { s_nc[threadIdx.x >> 6] = (unsigned)dnc; s_cnt[threadIdx.x >> 6] = cnt; }
+        if ((threadIdx.x & 63) == 0) s_nc[threadIdx.x >> 6] = (unsigned)dnc;
         __syncthreads();
         unsigned nc = 0;
-        for (int w = 0; w < BRWG / 64; ++w) { nc += s_nc[w]; fixed += s_cnt[w]; }
+        for (int w = 0; w < BRWG / 64; ++w) nc += s_nc[w];
         pa.notclose += nc;
     }
     if (threadIdx.x == 0) {
@@ -296,6 +305,30 @@ __global__ void bamp_output_kernel(BampK P) {
         P.var0[e] = P.var1[e];
 }
 
+template <int KK>
+static int bamp_kb2_attrs() {
+    int rc = set_lds_attr<128>((const void*)bamp_kb2<128, KK>);
+    return rc ? rc : set_lds_attr<256>((const void*)bamp_kb2<256, KK>);
+}
+
+template <int KK>
+static void launch_kb2_kk(const BampK& P, int gr, int t, hipStream_t st) {
+    if (P.bn == 128)
+        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    else
+        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+}
+
+static void launch_kb2(const BampK& P, int gr, int t, hipStream_t st) {
+    switch (P.c.K) {
+    case 1: launch_kb2_kk<1>(P, gr, t, st); break;
+    case 2: launch_kb2_kk<2>(P, gr, t, st); break;
+    case 4: launch_kb2_kk<4>(P, gr, t, st); break;
+    case 8: launch_kb2_kk<8>(P, gr, t, st); break;
+    default: launch_kb2_kk<16>(P, gr, t, st); break;
+    }
+}
+
 static std::once_flag g_bamp_once;
 static int g_bamp_rc = 0;
 
@@ -304,8 +337,11 @@ static int bamp_attrs() {
         g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka1);
         if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka2);
         if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_kb1);
-        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_kb2<128>);
-        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<256>((const void*)bamp_kb2<256>);
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<1>();
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<2>();
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<4>();
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<8>();
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<16>();
     });
     return g_bamp_rc;
 }
@@ -339,8 +375,9 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     P.Wabs2 = w.Wabs2; P.WH = w.WH; P.Wabs2T = w.Wabs2T; P.WHH = w.WHH;
     P.y = (const float*)a->y; P.v = w.v; P.z = w.z; P.invu = w.invu; P.s = w.s; P.cov = w.cov;
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.var0 = (float*)a->var; P.var1 = w.var1;
-    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    const Const64 c64 = to_const64(c);
     hipStream_t st = (hipStream_t)stream;
     const float2* H = (const float2*)a->H;
     // weights, once per forward (Tracker: adj, abs2, abs2T, bamp.py:17-19)
@@ -357,11 +394,8 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
         hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
         hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
         hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        if (P.bn == 128)
-            hipLaunchKernelGGL(bamp_kb2<128>, dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        else
-            hipLaunchKernelGGL(bamp_kb2<256>, dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
-        hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, t);
+        launch_kb2(P, gr, t, st);
+        hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
         AMP_LAUNCH_CHECK("bamp iteration");
     }
     hipLaunchKernelGGL(bamp_output_kernel, dim3((int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048)),

@@ -33,8 +33,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // fixed summation order: every workgroup that reduces them gets identical bits.
 struct alignas(16) Partial {
     double sumvar;     // sum of var (float64), NaN-propagating
-    double maxabs;     // max |xi| over the block, xi in float64 like the reference (vamp.py:112)
-    double minsecmax;  // min over sections of the section max logit (float64)
+    double maxabs;     // max |xi| over the block (float32 logits; NaN if any input is non-finite)
+    double minsecmax;  // min over sections of the section max logit
     uint32_t notclose; // elements failing torch.allclose(var_new, var_prev)
     uint32_t pad;
 };
@@ -77,37 +77,56 @@ __device__ __forceinline__ bool torch_close(float a, float b) {
 }
 
 // ---- reductions within aligned groups of G lanes (G power of two <= 64) ----
-template <typename T>
-__device__ __forceinline__ T group_max(T v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = v > w ? v : w; }
+// Butterfly steps run with the partner distance O ascending, so before step O every aligned
+// group of O lanes already holds one value and any pairing of the two halves of a 2O group
+// works: DPP quad_perm for O = 1, 2, row_half_mirror / row_mirror for O = 4, 8 (no LDS
+// traffic, foldable into the consuming VALU op), ds_swizzle xor for 16, bpermute for 32.
+// Every lane ends with the same bits (the combining ops are commutative).
+template <int O>
+__device__ __forceinline__ int xl_i32(int v) {
+    if constexpr (O == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    else if constexpr (O == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    else if constexpr (O == 4) return __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true); // row_half_mirror
+    else if constexpr (O == 8) return __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true); // row_mirror
+    else if constexpr (O == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);            // xor 16 in 32
+    else return __shfl_xor(v, 32, 64);
+}
+template <int O> __device__ __forceinline__ float xl(float v) { return __int_as_float(xl_i32<O>(__float_as_int(v))); }
+template <int O> __device__ __forceinline__ int xl(int v) { return xl_i32<O>(v); }
+template <int O> __device__ __forceinline__ unsigned xl(unsigned v) { return (unsigned)xl_i32<O>((int)v); }
+template <int O> __device__ __forceinline__ long long xl(long long v) {
+    const int lo = xl_i32<O>((int)(unsigned)v), hi = xl_i32<O>((int)(v >> 32));
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int O> __device__ __forceinline__ double xl(double v) { return __longlong_as_double(xl<O>(__double_as_longlong(v))); }
+
+template <class T, class Op>
+__device__ __forceinline__ T group_reduce(T v, int G, Op op) {
+    if (G > 1) v = op(v, xl<1>(v));
+    if (G > 2) v = op(v, xl<2>(v));
+    if (G > 4) v = op(v, xl<4>(v));
+    if (G > 8) v = op(v, xl<8>(v));
+    if (G > 16) v = op(v, xl<16>(v));
+    if (G > 32) v = op(v, xl<32>(v));
     return v;
 }
 template <typename T>
-__device__ __forceinline__ T group_min(T v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) { T w = __shfl_xor(v, o, 64); v = v < w ? v : w; }
-    return v;
-}
+__device__ __forceinline__ T group_max(T v, int G) { return group_reduce(v, G, [](T a, T b) { return a > b ? a : b; }); }
 template <typename T>
-__device__ __forceinline__ T group_sum(T v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+__device__ __forceinline__ T group_min(T v, int G) { return group_reduce(v, G, [](T a, T b) { return a < b ? a : b; }); }
+template <typename T>
+__device__ __forceinline__ T group_sum(T v, int G) { return group_reduce(v, G, [](T a, T b) { return a + b; }); }
+__device__ __forceinline__ float group_fmax(float v, int G) {
+    return group_reduce(v, G, [](float a, float b) { return fmaxf(a, b); });
 }
 // NaN-sticky variants (a NaN anywhere in the group wins)
-__device__ __forceinline__ float group_max_nan(float v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, 64));
-    return v;
+template <typename T>
+__device__ __forceinline__ T group_max_nan(T v, int G) {
+    return group_reduce(v, G, [](T a, T b) { return nan_max(a, b); });
 }
-__device__ __forceinline__ float group_min_nan(float v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) v = nan_min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double group_max_nan(double v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double group_min_nan(double v, int G) {
-    for (int o = G >> 1; o > 0; o >>= 1) v = nan_min(v, __shfl_xor(v, o, 64));
-    return v;
+template <typename T>
+__device__ __forceinline__ T group_min_nan(T v, int G) {
+    return group_reduce(v, G, [](T a, T b) { return nan_min(a, b); });
 }
 
 // ---- workgroup-level reduction of a Partial (256 threads) ----
@@ -184,8 +203,13 @@ __device__ __forceinline__ PartAcc part_reduce_all(const Partial* src, int nblk,
 // normaliser Z is denormal or zero, so c128 / Z (= * (1/Z)) overflows to inf/NaN, and for
 // real alphabets the true division is denormal-quantised or 0/0.  Such sections are
 // recomputed with the reference's exact float64 arithmetic (exact_section_f64).
+// The fast path's float32 logits carry a few ulp of |xi| of error: every decision on them
+// (danger, batch max) is taken with this slack, and the exact path settles it in float64.
 #define AMP_DANGER (-700.0)
-__device__ __forceinline__ bool part_danger(const PartAcc& p) { return p.minsecmax - p.maxabs < AMP_DANGER; }
+__device__ __forceinline__ double logit_slack(double G) { return 1e-5 * fabs(G) + 2.0; }
+__device__ __forceinline__ bool part_danger(const PartAcc& p) {
+    return p.minsecmax - p.maxabs < AMP_DANGER + logit_slack(p.maxabs);
+}
 
 // torch's x.abs().max() propagates NaN: once any logit of the batch is NaN or +-inf the
 // reference's shift G is NaN / inf and exp(xi - G) makes EVERY section NaN (0/0 or NaN).
@@ -200,11 +224,17 @@ __device__ __forceinline__ void nan_fill(float* xm, float* var, size_t n) {
     }
 }
 
+// Constellation for the fast path (kept small: it lives in SGPRs of every fused kernel).
 struct Const {
     int K;
-    int real_alpha;    // OOK / BPSK / 4ASK: float64 symbols in the reference (config.py:117)
     float re[AMP_MAX_K], im[AMP_MAX_K];
-    double re64[AMP_MAX_K], im64[AMP_MAX_K];
+};
+
+// Constellation in float64 for the reference-exact rare path (never in a hot kernel's args).
+struct Const64 {
+    int K;
+    int real_alpha;    // OOK / BPSK / 4ASK: float64 symbols in the reference (config.py:117)
+    double re[AMP_MAX_K], im[AMP_MAX_K];
 };
 
 }  // namespace amp

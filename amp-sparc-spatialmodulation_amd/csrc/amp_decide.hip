@@ -139,9 +139,10 @@ __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
     }
 }
 
-__global__ __launch_bounds__(AMP_WG) void map_count_kernel(DecK P) {
+__global__ __launch_bounds__(1024) void map_count_kernel(DecK P) {
+    // channel-use / trial "any mismatch" counts (loss.py:133-136, 150) ...
     long long ver = 0, verf = 0, verm = 0, verL = 0, fer = 0;
-    for (int b = threadIdx.x; b < P.B; b += AMP_WG) {
+    for (int b = threadIdx.x; b < P.B; b += blockDim.x) {
         int trial = 0;
         for (int lin = 0; lin < P.Lin; ++lin) {
             int cu = 0;
@@ -155,26 +156,37 @@ __global__ __launch_bounds__(AMP_WG) void map_count_kernel(DecK P) {
         }
         fer += trial;
     }
+    // ... and the per-workgroup partials of map_decide_kernel, folded in a fixed order
+    DecPart t = DecPart{0, 0, 0, 0, 0.0, 0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < P.nblk; i += blockDim.x) {
+        const DecPart q = P.parts[i];
+        t.ier += q.ier; t.ser += q.ser; t.iber += q.iber; t.sber += q.sber;
+        t.mse += q.mse; t.msef += q.msef; t.msem += q.msem; t.mseL += q.mseL;
+    }
     ver = group_sum(ver, 64); verf = group_sum(verf, 64); verm = group_sum(verm, 64); verL = group_sum(verL, 64);
     fer = group_sum(fer, 64);
-    __shared__ long long sc[AMP_WG / 64][5];
+    t.ier = group_sum(t.ier, 64); t.ser = group_sum(t.ser, 64); t.iber = group_sum(t.iber, 64);
+    t.sber = group_sum(t.sber, 64);
+    t.mse = group_sum(t.mse, 64); t.msef = group_sum(t.msef, 64); t.msem = group_sum(t.msem, 64);
+    t.mseL = group_sum(t.mseL, 64);
+    __shared__ long long sc[16][5];
+    __shared__ DecPart sp[16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) { sc[wave][0] = ver; sc[wave][1] = verf; sc[wave][2] = verm; sc[wave][3] = verL; sc[wave][4] = fer; }
+    if (lane == 0) {
+        sc[wave][0] = ver; sc[wave][1] = verf; sc[wave][2] = verm; sc[wave][3] = verL; sc[wave][4] = fer;
+        sp[wave] = t;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         amp_counts c;
         c.ver = c.verf = c.verm = c.verL = c.fer = 0;
-        for (int w = 0; w < AMP_WG / 64; ++w) {
+        c.ier = c.ser = c.iber = c.sber = 0;
+        c.mse = c.msef = c.msem = c.mseL = 0.0;
+        for (int w = 0; w < (int)(blockDim.x / 64); ++w) {
             c.ver += sc[w][0]; c.verf += sc[w][1]; c.verm += sc[w][2]; c.verL += sc[w][3]; c.fer += sc[w][4];
+            c.ier += sp[w].ier; c.ser += sp[w].ser; c.iber += sp[w].iber; c.sber += sp[w].sber;
+            c.mse += sp[w].mse; c.msef += sp[w].msef; c.msem += sp[w].msem; c.mseL += sp[w].mseL;
         }
-        DecPart t = P.parts[0];
-        for (int i = 1; i < P.nblk; ++i) {
-            const DecPart q = P.parts[i];
-            t.ier += q.ier; t.ser += q.ser; t.iber += q.iber; t.sber += q.sber;
-            t.mse += q.mse; t.msef += q.msef; t.msem += q.msem; t.mseL += q.mseL;
-        }
-        c.ier = t.ier; c.ser = t.ser; c.iber = t.iber; c.sber = t.sber;
-        c.mse = t.mse; c.msef = t.msef; c.msem = t.msem; c.mseL = t.mseL;
         *P.out = c;
     }
 }
@@ -231,7 +243,7 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(map_decide_kernel, dim3(P.nblk), dim3(AMP_WG), 0, st, P);
     AMP_LAUNCH_CHECK("map_decide");
-    hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(AMP_WG), 0, st, P);
+    hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(1024), 0, st, P);
     AMP_LAUNCH_CHECK("map_count");
     return AMP_OK;
 }

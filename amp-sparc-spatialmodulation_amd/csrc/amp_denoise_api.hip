@@ -1,9 +1,11 @@
 // amp_denoise_api.hip — the block-sparse denoiser as a standalone op
 // (VAMPLayer.segmented_denoiser vamp.py:96-119, BAMPLayer.segmented_denoiser bamp.py:66-77,
 //  SCAMPLayer.denoiser scamp.py:61-68).
-// Three launches: sections -> (xmmse, var, section max, block partials); one workgroup
-// reduces the partials to the batch max|xi|; sections whose reference float64 softmax
-// leaves the normal range are recomputed with the reference's exact arithmetic.
+// Three launches: sections -> (xmmse, var, section max / max|xi|, block partials); one
+// workgroup reduces the partials and, when some section is near the edge of the float64
+// range, settles the exact float64 batch max|xi|; sections whose reference float64 softmax
+// leaves the normal range are then recomputed with the reference's exact arithmetic (and a
+// NaN / inf anywhere makes every section NaN, as torch's max|xi| propagates it).
 #include <algorithm>
 
 #include "amp_denoise.h"
@@ -18,12 +20,15 @@ struct DnK {
     const float* tau;
     float2* xm;
     float* var;
-    double* secmax;
+    float* secmax;
+    float* secabs;
     Partial* parts;
     int nblk;
-    double* G;
+    double* G;          // [0] exact batch max|xi|, [1] action: 0 none, 1 fix-up, 2 all NaN, [2] slack
     Const c;
 };
+
+constexpr int DRWG = 1024;
 
 struct DnPolicy {
     const DnK* P;
@@ -40,9 +45,13 @@ struct DnPolicy {
         if (P->var) P->var[o] = var;
         pa.sumvar += (double)var;
     }
-    __device__ __forceinline__ void section(int sec, double smax) const { P->secmax[sec0 + sec] = smax; }
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
+        P->secmax[sec0 + sec] = smax;
+        P->secabs[sec0 + sec] = sabs;
+    }
 };
 
+template <int KK>
 __global__ __launch_bounds__(AMP_WG) void denoise_kernel(DnK P) {
     __shared__ __attribute__((aligned(16))) float lds[64];
     const int G = P.M < 64 ? P.M : 64;
@@ -52,37 +61,74 @@ __global__ __launch_bounds__(AMP_WG) void denoise_kernel(DnK P) {
         DnPolicy pol{&P, sec0};
         const int n = min(per, P.S - sec0);
         if (P.mode == 2)
-            denoise_sections<false>(pol, n, P.M, P.c, pa);
+            denoise_sections<false, KK>(pol, n, P.M, P.c, pa);
         else
-            denoise_sections<true>(pol, n, P.M, P.c, pa);
+            denoise_sections<true, KK>(pol, n, P.M, P.c, pa);
     }
     part_block_store(pa, P.parts + blockIdx.x, lds);
 }
 
-__global__ __launch_bounds__(AMP_WG) void denoise_reduce_kernel(DnK P) {
-    __shared__ __attribute__((aligned(16))) float lds[64];
+struct DnLoad {
+    const DnK* P;
+    size_t o0;
+    __device__ __forceinline__ void operator()(int m, float& rr, float& ri, float& it) const {
+        const float2 v = P->r[o0 + m];
+        rr = v.x; ri = v.y;
+        it = (P->mode == 0) ? P->tau_scalar_inv : 1.0f / (P->tau[o0 + m] * 0.5f);
+    }
+};
+
+__global__ __launch_bounds__(DRWG) void denoise_reduce_kernel(DnK P, Const64 c64) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    __shared__ double s_d[DRWG / 64];
     const PartAcc pa = part_reduce_all(P.parts, P.nblk, lds);
-    if (threadIdx.x == 0) *P.G = pa.maxabs;
+    double act = 0.0, G = pa.maxabs;
+    if (part_allnan(pa)) {
+        act = 2.0;
+    } else if (part_danger(pa)) {
+        // exact float64 max|xi| over the candidate sections
+        const double slack = logit_slack(pa.maxabs);
+        double gm = 0.0;
+        for (int s = threadIdx.x; s < P.S; s += blockDim.x)
+            if ((double)P.secabs[s] >= pa.maxabs - slack)
+                gm = fmax(gm, section_absmax_f64(DnLoad{&P, (size_t)s * P.M}, P.M, c64));
+        gm = group_max(gm, 64);
+        if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        G = 0.0;
+        for (int w = 0; w < DRWG / 64; ++w) G = fmax(G, s_d[w]);
+        act = 1.0;
+    }
+    if (threadIdx.x == 0) {
+        P.G[0] = G;
+        P.G[1] = act;
+        P.G[2] = logit_slack(pa.maxabs);
+    }
 }
 
-__global__ void denoise_fix_kernel(DnK P) {
-    const double G = *P.G;
+__global__ void denoise_fix_kernel(DnK P, Const64 c64) {
+    const double G = P.G[0], act = P.G[1], slack = P.G[2];
+    if (act == 0.0) return;
+    if (act == 2.0) {
+        const float q = __int_as_float(0x7fc00000);
+        for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < (size_t)P.S * P.M;
+             e += (size_t)gridDim.x * blockDim.x) {
+            P.xm[e] = make_float2(q, q);
+            if (P.var) P.var[e] = q;
+        }
+        return;
+    }
     for (int sec = blockIdx.x * blockDim.x + threadIdx.x; sec < P.S; sec += gridDim.x * blockDim.x) {
-        if (!(P.secmax[sec] - G < AMP_DANGER)) continue;
+        if (!((double)P.secmax[sec] - G < AMP_DANGER + slack)) continue;
         const size_t o0 = (size_t)sec * P.M;
-        auto ld = [&](int m, float& rr, float& ri, float& it) {
-            const float2 v = P.r[o0 + m];
-            rr = v.x; ri = v.y;
-            it = (P.mode == 0) ? P.tau_scalar_inv : 1.0f / (P.tau[o0 + m] * 0.5f);
-        };
         auto st = [&](int m, float xr, float xi, float var) {
             P.xm[o0 + m] = make_float2(xr, xi);
             if (P.var) P.var[o0 + m] = var;
         };
         if (P.mode == 2)
-            exact_section_f64<false>(ld, st, P.M, P.c, G);
+            exact_section_f64<false>(DnLoad{&P, o0}, st, P.M, c64, G);
         else
-            exact_section_f64<true>(ld, st, P.M, P.c, G);
+            exact_section_f64<true>(DnLoad{&P, o0}, st, P.M, c64, G);
     }
 }
 
@@ -101,9 +147,10 @@ extern "C" {
 size_t amp_block_denoise_workspace_bytes(const amp_dims* d) {
     if (!d) return 0;
     Carve cv(nullptr);
-    cv.take<double>((size_t)d->B * d->L);
+    cv.take<float>((size_t)d->B * d->L);
+    cv.take<float>((size_t)d->B * d->L);
     cv.take<Partial>((size_t)dn_nblk(d));
-    cv.take<double>(2);
+    cv.take<double>(4);
     return cv.off;
 }
 
@@ -123,18 +170,26 @@ int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void*
     P.r = (const float2*)r; P.tau = (const float*)tau_vec; P.xm = (float2*)xmmse;
     P.var = (tau_mode == 2) ? nullptr : (float*)var;
     Carve cv(ws);
-    P.secmax = cv.take<double>((size_t)P.S);
+    P.secmax = cv.take<float>((size_t)P.S);
+    P.secabs = cv.take<float>((size_t)P.S);
     P.nblk = dn_nblk(d);
     P.parts = cv.take<Partial>((size_t)P.nblk);
-    P.G = cv.take<double>(2);
+    P.G = cv.take<double>(4);
     P.c = to_const(c);
+    const Const64 c64 = to_const64(c);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(denoise_kernel, dim3(P.nblk), dim3(AMP_WG), 0, st, P);
+    switch (P.c.K) {
+    case 1: hipLaunchKernelGGL(denoise_kernel<1>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    case 2: hipLaunchKernelGGL(denoise_kernel<2>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    case 4: hipLaunchKernelGGL(denoise_kernel<4>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    case 8: hipLaunchKernelGGL(denoise_kernel<8>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    default: hipLaunchKernelGGL(denoise_kernel<16>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    }
     AMP_LAUNCH_CHECK("denoise");
-    hipLaunchKernelGGL(denoise_reduce_kernel, dim3(1), dim3(AMP_WG), 0, st, P);
+    hipLaunchKernelGGL(denoise_reduce_kernel, dim3(1), dim3(DRWG), 0, st, P, c64);
     AMP_LAUNCH_CHECK("denoise_reduce");
     const int g = std::max(1, std::min(cdiv(P.S, 256), 1024));
-    hipLaunchKernelGGL(denoise_fix_kernel, dim3(g), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(denoise_fix_kernel, dim3(g), dim3(256), 0, st, P, c64);
     AMP_LAUNCH_CHECK("denoise_fix");
     return AMP_OK;
 }

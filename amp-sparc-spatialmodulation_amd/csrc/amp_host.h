@@ -51,13 +51,22 @@ struct Carve {
 inline Const to_const(const amp_constellation* c) {
     Const k;
     k.K = c->K;
-    k.real_alpha = 1;
     for (int i = 0; i < AMP_MAX_K; ++i) {
         const bool v = i < c->K;
         k.re[i] = v ? c->re[i] : 0.f;
         k.im[i] = v ? c->im[i] : 0.f;
-        k.re64[i] = v ? c->re64[i] : 0.0;
-        k.im64[i] = v ? c->im64[i] : 0.0;
+    }
+    return k;
+}
+
+inline Const64 to_const64(const amp_constellation* c) {
+    Const64 k;
+    k.K = c->K;
+    k.real_alpha = 1;
+    for (int i = 0; i < AMP_MAX_K; ++i) {
+        const bool v = i < c->K;
+        k.re[i] = v ? c->re64[i] : 0.0;
+        k.im[i] = v ? c->im64[i] : 0.0;
         if (v && c->im64[i] != 0.0) k.real_alpha = 0;
     }
     return k;

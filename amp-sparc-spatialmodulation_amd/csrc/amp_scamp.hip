@@ -42,7 +42,8 @@ struct ScampK {
     float* xm;             // caller [B][2N]
     float* psi0;           // caller's psi [B][Lin] (even iterations)
     float* psi1;           // workspace     (odd iterations)
-    double* secmax;        // [B*L]
+    float* secmax;         // [B*L] per-section max logit (fast path)
+    float* secabs;         // [B*L] per-section max |logit|
     Partial* parts;
     ScampIter* iters;
     amp_status* status;
@@ -51,7 +52,7 @@ struct ScampK {
 
 struct ScampWs {
     float *WA, *WAH, *z, *s, *phi, *tau, *psi1;
-    double* secmax;
+    float *secmax, *secabs;
     Partial* parts;
     ScampIter* iters;
     size_t bytes;
@@ -80,7 +81,8 @@ static ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.phi = cv.take<float>((size_t)2 * d->B * d->Lout);
     w.tau = cv.take<float>((size_t)d->B * d->Lin);
     w.psi1 = cv.take<float>((size_t)d->B * d->Lin);
-    w.secmax = cv.take<double>((size_t)d->B * d->L);
+    w.secmax = cv.take<float>((size_t)d->B * d->L);
+    w.secabs = cv.take<float>((size_t)d->B * d->L);
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
     w.iters = cv.take<ScampIter>((size_t)max_iter + 1);
     w.bytes = cv.off;
@@ -133,7 +135,8 @@ struct ScampDenoisePolicy {
     const float* tau_tile;   // LDS [32][Lin] tau of the tile's rows
     int ldc, spr, M, N, Nt, L, row0, colc0, Lin;
     float* xm;
-    double* secmax;
+    float* secmax;
+    float* secabs;
     __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
         const int rho = sec / spr, sj = sec - rho * spr;
         const int cc = sj * M + m;
@@ -146,14 +149,16 @@ struct ScampDenoisePolicy {
         const size_t o = (size_t)(row0 + rho) * N + colc0 + sj * M + m;
         *reinterpret_cast<float2*>(xm + 2 * o) = make_float2(xr, xi);
     }
-    __device__ __forceinline__ void section(int sec, double smax) const {
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
         const int rho = sec / spr, sj = sec - rho * spr;
-        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+        const size_t o = (size_t)(row0 + rho) * L + (colc0 / M) + sj;
+        secmax[o] = smax;
+        secabs[o] = sabs;
     }
 };
 
 // tau = L / (W^T (1/phi)) / Mr ; xmap = xmmse + tau (A^H s) ; xmmse = denoiser ; psi   (scamp.py:53-59)
-template <int BN>
+template <int BN, int KK>
 __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -192,9 +197,9 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     ScampDenoisePolicy pol;
     pol.tile = lds; pol.tau_tile = tau_t; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.Nt = P.Nt; pol.L = P.L;
     pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2; pol.Lin = P.Lin;
-    pol.xm = P.xm; pol.secmax = P.secmax;
+    pol.xm = P.xm; pol.secmax = P.secmax; pol.secabs = P.secabs;
     PartAcc pa;
-    denoise_sections<false>(pol, nrows * pol.spr, P.M, P.c, pa);
+    denoise_sections<false, KK>(pol, nrows * pol.spr, P.M, P.c, pa);
     __syncthreads();
     // psi = 1 - sum_block |xmmse|^2 / Na (scamp.py:59) from the freshly written tile
     const float* psi_prev = spsi(P, t + 1);
@@ -221,10 +226,10 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
 }
 
 // reduction, exact float64 fix-up of out-of-range sections (+ their psi), allclose(psi)
-__global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
+__global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
     __shared__ unsigned s_nc[SRWG / 64];
-    __shared__ int s_cnt[SRWG / 64];
+    __shared__ double s_d[SRWG / 64];
     const ScampIter cur = P.iters[t];
     if (cur.stopped) {
         if (threadIdx.x == 0) P.iters[t + 1] = cur;
@@ -241,31 +246,35 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
         pa.notclose = 1;
         fixed = -1;
     } else if (part_danger(pa)) {
-        const double G = pa.maxabs;
-        int cnt = 0, dnc = 0;
         // sections, then every coupling block that holds a recomputed section
-        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
-            if (!(P.secmax[sct] - G < AMP_DANGER)) continue;
-            ++cnt;
-            const size_t o0 = (size_t)sct * P.M;
-            const int b = sct / P.L, lc = (int)((o0 % (size_t)P.N) / P.Nt);
-            const float tv = P.tau[(size_t)b * P.Lin + lc];
-            auto ld = [&](int m, float& rr, float& ri, float& it) {
-                const float2 v = reinterpret_cast<const float2*>(P.xmap)[o0 + m];
+        const double slack = logit_slack(pa.maxabs);
+        const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+        float2* x2 = reinterpret_cast<float2*>(P.xm);
+        const float* tau = P.tau;
+        const int M = P.M, L = P.L, N = P.N, Nt = P.Nt, Lin = P.Lin;
+        int dnc = 0;
+        auto ldf = [=](int sct) {
+            const size_t o0 = (size_t)sct * M;
+            const int b = sct / L, lc = (int)((o0 % (size_t)N) / Nt);
+            const float tv = tau[(size_t)b * Lin + lc];
+            return [=](int m, float& rr, float& ri, float& it) {
+                const float2 v = xp2[o0 + m];
                 rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
             };
-            auto st = [&](int m, float xr, float xi, float) {
-                reinterpret_cast<float2*>(P.xm)[o0 + m] = make_float2(xr, xi);
-            };
-            exact_section_f64<false>(ld, st, P.M, P.c, G);
-        }
+        };
+        auto stf = [=](int sct) {
+            const size_t o0 = (size_t)sct * M;
+            return [=](int m, float xr, float xi, float) { x2[o0 + m] = make_float2(xr, xi); };
+        };
+        double G;
+        fixed = fixup_sections<false>(P.B * L, M, P.secmax, P.secabs, pa.maxabs, c64, ldf, stf, &G, s_d);
         __syncthreads();
         const float* psi_prev = spsi(P, t + 1);
         float* psi_new = spsi(P, t);
         const int spb = P.Nt / P.M;   // sections per coupling block
         for (int blk = threadIdx.x; blk < P.B * P.Lin; blk += blockDim.x) {
             bool hit = false;
-            for (int j = 0; j < spb && !hit; ++j) hit = P.secmax[(size_t)blk * spb + j] - G < AMP_DANGER;
+            for (int j = 0; j < spb && !hit; ++j) hit = (double)P.secmax[(size_t)blk * spb + j] - G < AMP_DANGER + slack;
             if (!hit) continue;
             const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
             double ssum = 0.0;
@@ -278,11 +287,10 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, int t) {
             psi_new[blk] = ps;
         }
         dnc = group_sum(dnc, 64);
-        cnt = group_sum(cnt, 64);
-        if ((threadIdx.x & 63) == 0) { s_nc[threadIdx.x >> 6] = (unsigned)dnc; s_cnt[threadIdx.x >> 6] = cnt; }
+        if ((threadIdx.x & 63) == 0) s_nc[threadIdx.x >> 6] = (unsigned)dnc;
         __syncthreads();
         unsigned nc = 0;
-        for (int w = 0; w < SRWG / 64; ++w) { nc += s_nc[w]; fixed += s_cnt[w]; }
+        for (int w = 0; w < SRWG / 64; ++w) nc += s_nc[w];
         pa.notclose += nc;
     }
     if (threadIdx.x == 0) {
@@ -329,11 +337,38 @@ __global__ void scamp_output_kernel(ScampK P) {
 static std::once_flag g_scamp_once;
 static int g_scamp_rc = 0;
 
+template <int KK>
+static int scamp_kb_attrs() {
+    int rc = set_lds_attr<128>((const void*)scamp_kb<128, KK>);
+    return rc ? rc : set_lds_attr<256>((const void*)scamp_kb<256, KK>);
+}
+
+template <int KK>
+static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
+    if (P.bn == 128)
+        hipLaunchKernelGGL((scamp_kb<128, KK>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), ldsB, st, P, t);
+    else
+        hipLaunchKernelGGL((scamp_kb<256, KK>), dim3(gr, P.ncpB / 256), dim3(AMP_WG), ldsB, st, P, t);
+}
+
+static void launch_kb(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
+    switch (P.c.K) {
+    case 1: launch_kb_kk<1>(P, gr, ldsB, t, st); break;
+    case 2: launch_kb_kk<2>(P, gr, ldsB, t, st); break;
+    case 4: launch_kb_kk<4>(P, gr, ldsB, t, st); break;
+    case 8: launch_kb_kk<8>(P, gr, ldsB, t, st); break;
+    default: launch_kb_kk<16>(P, gr, ldsB, t, st); break;
+    }
+}
+
 static int scamp_attrs() {
     std::call_once(g_scamp_once, [] {
         g_scamp_rc = set_lds_attr<128>((const void*)scamp_ka);
-        if (!g_scamp_rc) g_scamp_rc = set_lds_attr<128>((const void*)scamp_kb<128>);
-        if (!g_scamp_rc) g_scamp_rc = set_lds_attr<256>((const void*)scamp_kb<256>);
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<1>();
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<2>();
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<4>();
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<8>();
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<16>();
     });
     return g_scamp_rc;
 }
@@ -369,8 +404,9 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     P.WA = w.WA; P.WAH = w.WAH;
     P.y = (const float*)a->y; P.z = w.z; P.s = w.s; P.phi = w.phi; P.tau = w.tau;
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
-    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    const Const64 c64 = to_const64(c);
     hipStream_t st = (hipStream_t)stream;
     const float2* A = (const float2*)a->A;
     if ((rc = build_cweight(A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.kapA, P.ncpA, st))) return rc;
@@ -382,11 +418,8 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     for (int t = 0; t < P.max_iter; ++t) {
         hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        if (P.bn == 128)
-            hipLaunchKernelGGL(scamp_kb<128>, dim3(gr, P.ncpB / 128), dim3(AMP_WG), ldsB, st, P, t);
-        else
-            hipLaunchKernelGGL(scamp_kb<256>, dim3(gr, P.ncpB / 256), dim3(AMP_WG), ldsB, st, P, t);
-        hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, t);
+        launch_kb(P, gr, ldsB, t, st);
+        hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
         AMP_LAUNCH_CHECK("scamp iteration");
     }
     hipLaunchKernelGGL(scamp_output_kernel, dim3(64), dim3(256), 0, st, P);

@@ -43,7 +43,8 @@ struct VampK {
     float* xm;          // [B][2N]  (caller's xmmse)
     float* var0;        // [B][N] caller's var: var of even iterations
     float* var1;        // [B][N] workspace:    var of odd iterations
-    double* secmax;     // [2][B*L]
+    float* secmax;      // [B*L] per-section max logit (fast path, natural units)
+    float* secabs;      // [B*L] per-section max |logit|
     Partial* parts;     // [max_iter][nblk2]
     VampIter* iters;    // [max_iter + 1]: iters[t] drives iteration t
     amp_status* status;
@@ -52,7 +53,7 @@ struct VampK {
 
 struct VampWs {
     float *Wt0, *Wt1, *Wt2, *s2, *ytil, *w, *var1;
-    double* secmax;
+    float *secmax, *secabs;
     Partial* parts;
     VampIter* iters;
     size_t bytes;
@@ -79,7 +80,8 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.ytil = cv.take<float>((size_t)d->B * 2 * k);
     w.w = cv.take<float>((size_t)d->B * 2 * k);
     w.var1 = cv.take<float>((size_t)d->B * d->N);
-    w.secmax = cv.take<double>((size_t)2 * d->B * d->L);
+    w.secmax = cv.take<float>((size_t)d->B * d->L);
+    w.secabs = cv.take<float>((size_t)d->B * d->L);
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
     w.iters = cv.take<VampIter>((size_t)max_iter + 1);
     w.bytes = cv.off;
@@ -180,7 +182,8 @@ struct VampDenoisePolicy {
     float* xm;
     float* var_new;
     const float* var_prev;
-    double* secmax;
+    float* secmax;
+    float* secabs;
     __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
         const int rho = sec / spr, sj = sec - rho * spr;
         const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * (sj * M + m));
@@ -194,13 +197,15 @@ struct VampDenoisePolicy {
         pa.sumvar += (double)var;
         pa.notclose += torch_close(var, var_prev[o]) ? 0u : 1u;     // vamp.py:185
     }
-    __device__ __forceinline__ void section(int sec, double smax) const {
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
         const int rho = sec / spr, sj = sec - rho * spr;
-        secmax[(size_t)(row0 + rho) * L + (colc0 / M) + sj] = smax;
+        const size_t o = (size_t)(row0 + rho) * L + (colc0 / M) + sj;
+        secmax[o] = smax;
+        secabs[o] = sabs;
     }
 };
 
-template <int BN>
+template <int BN, int KK>
 __global__ __launch_bounds__(AMP_WG) void vamp_k2(VampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const VampIter it = P.iters[t];
@@ -230,19 +235,19 @@ __global__ __launch_bounds__(AMP_WG) void vamp_k2(VampK P, int t) {
     pol.xm = P.xm;
     pol.var_new = var_buf(P, t);
     pol.var_prev = var_buf(P, t + 1);
-    pol.secmax = P.secmax + (size_t)(t & 1) * P.B * P.L;
+    pol.secmax = P.secmax;
+    pol.secabs = P.secabs;
     PartAcc pa;
-    denoise_sections<true>(pol, nrows * pol.spr, P.M, P.c, pa);
+    denoise_sections<true, KK>(pol, nrows * pol.spr, P.M, P.c, pa);
     part_block_store(pa, P.parts + (size_t)t * P.nblk2 + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
 }
 
 // One workgroup after K2(t): partial reduction, exact float64 fix-up of out-of-range
 // sections, allclose decision and the scalars of iteration t+1.
-__global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
+__global__ __launch_bounds__(RWG) void vamp_r(VampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
     __shared__ double s_fix[RWG / 64];
     __shared__ unsigned s_nc[RWG / 64];
-    __shared__ int s_cnt[RWG / 64];
     const VampIter cur = P.iters[t];
     if (cur.stopped) {
         if (threadIdx.x == 0) P.iters[t + 1] = cur;
@@ -257,45 +262,48 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, int t) {
         pa.notclose = 1;
         fixed = -1;
     } else if (part_danger(pa)) {
-        // exact float64 recompute of every section below the danger line (rare)
-        const double G = pa.maxabs;
-        const double* sm = P.secmax + (size_t)(t & 1) * P.B * P.L;
+        // exact float64 G, then exact float64 recompute of every section below the danger
+        // line (rare); the recomputed values replace the fast-path ones in the reductions
         float* vn = var_buf(P, t);
         const float* vp = var_buf(P, t + 1);
+        const float inv = cur.inv_sigma2;
+        const float2* r2 = reinterpret_cast<const float2*>(P.r);
+        float2* x2 = reinterpret_cast<float2*>(P.xm);
+        const int M = P.M;
         double dsum = 0.0;
-        int dnc = 0, cnt = 0;
-        for (int s = threadIdx.x; s < P.B * P.L; s += blockDim.x) {
-            if (!(sm[s] - G < AMP_DANGER)) continue;
-            ++cnt;
-            const size_t o0 = (size_t)s * P.M;
-            const float inv = cur.inv_sigma2;
-            auto ld = [&](int m, float& rr, float& ri, float& it) {
-                const float2 v = reinterpret_cast<const float2*>(P.r)[o0 + m];
+        int dnc = 0;
+        auto ldf = [=](int s) {
+            const size_t o0 = (size_t)s * M;
+            return [=](int m, float& rr, float& ri, float& it) {
+                const float2 v = r2[o0 + m];
                 rr = v.x; ri = v.y; it = inv;
             };
-            auto st = [&](int m, float xr, float xi, float var) {
+        };
+        auto stf = [&](int s) {
+            const size_t o0 = (size_t)s * M;
+            return [&, o0](int m, float xr, float xi, float var) {
                 const size_t o = o0 + m;
                 const float old = vn[o];
                 dsum += (double)var - (double)old;
                 dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(old, vp[o]) ? 0 : 1);
-                reinterpret_cast<float2*>(P.xm)[o] = make_float2(xr, xi);
+                x2[o] = make_float2(xr, xi);
                 vn[o] = var;
             };
-            exact_section_f64<true>(ld, st, P.M, P.c, G);
-        }
+        };
+        double G;
+        fixed = fixup_sections<true>(P.B * P.L, P.M, P.secmax, P.secabs, pa.maxabs, c64, ldf, stf, &G, s_fix);
+        pa.maxabs = G;
         dsum = group_sum(dsum, 64);
         dnc = group_sum(dnc, 64);
-        cnt = group_sum(cnt, 64);
         if ((threadIdx.x & 63) == 0) {
             s_fix[threadIdx.x >> 6] = dsum;
             s_nc[threadIdx.x >> 6] = (unsigned)dnc;
-            s_cnt[threadIdx.x >> 6] = cnt;
         }
         __syncthreads();
         double d = 0.0;
         unsigned nc = 0;
-        for (int w = 0; w < RWG / 64; ++w) { d += s_fix[w]; nc += s_nc[w]; fixed += s_cnt[w]; }
-        // the recomputed values replace the fast-path ones: (sum - old) + new, in float64
+        for (int w = 0; w < RWG / 64; ++w) { d += s_fix[w]; nc += s_nc[w]; }
+        // (sum - old) + new, in float64
         pa.sumvar += d;
         pa.notclose += nc;
         __syncthreads();
@@ -356,7 +364,7 @@ __global__ void vamp_output_kernel(VampK P) {
         P.var0[e] = P.var1[e];
 }
 
-static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P) {
+static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64) {
     int rc = check_dims(d, c);
     if (rc) return rc;
     AMP_REQUIRE(a && a->U && a->s && a->Vh && a->y && a->r && a->xmmse && a->var && a->status && a->ws,
@@ -375,21 +383,52 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.r = (float*)a->r; P.xm = (float*)a->xmmse;
     P.var0 = (float*)a->var;
     P.var1 = w.var1;
-    P.secmax = w.secmax; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    c64 = to_const64(c);
     return AMP_OK;
 }
 
 static std::once_flag g_vamp_attr_once;
 static int g_vamp_attr_rc = 0;
 
+template <int KK>
+static int vamp_k2_attrs() {
+    int rc = set_lds_attr<128>((const void*)vamp_k2<128, KK>);
+    return rc ? rc : set_lds_attr<256>((const void*)vamp_k2<256, KK>);
+}
+
 static int vamp_attrs() {
     std::call_once(g_vamp_attr_once, [] {
-        g_vamp_attr_rc = set_lds_attr<128>((const void*)vamp_k1);
-        if (!g_vamp_attr_rc) g_vamp_attr_rc = set_lds_attr<128>((const void*)vamp_k2<128>);
-        if (!g_vamp_attr_rc) g_vamp_attr_rc = set_lds_attr<256>((const void*)vamp_k2<256>);
+        int rc = set_lds_attr<128>((const void*)vamp_k1);
+        if (!rc) rc = vamp_k2_attrs<1>();
+        if (!rc) rc = vamp_k2_attrs<2>();
+        if (!rc) rc = vamp_k2_attrs<4>();
+        if (!rc) rc = vamp_k2_attrs<8>();
+        if (!rc) rc = vamp_k2_attrs<16>();
+        g_vamp_attr_rc = rc;
     });
     return g_vamp_attr_rc;
+}
+
+template <int KK>
+static void launch_k2_kk(const VampK& P, int t, hipStream_t st) {
+    dim3 g2(cdiv(P.B, GBM), P.ncp2 / P.bn2);
+    if (P.bn2 == 128)
+        hipLaunchKernelGGL((vamp_k2<128, KK>), g2, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    else
+        hipLaunchKernelGGL((vamp_k2<256, KK>), g2, dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+}
+
+// GEMM2 + denoiser, instantiated per constellation size (K is validated by check_dims)
+static void launch_k2(const VampK& P, int t, hipStream_t st) {
+    switch (P.c.K) {
+    case 1: launch_k2_kk<1>(P, t, st); break;
+    case 2: launch_k2_kk<2>(P, t, st); break;
+    case 4: launch_k2_kk<4>(P, t, st); break;
+    case 8: launch_k2_kk<8>(P, t, st); break;
+    default: launch_k2_kk<16>(P, t, st); break;
+    }
 }
 
 
@@ -414,17 +453,13 @@ static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t
     return gemm_store((const float*)a->y, 2 * P.n, P.B, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k, 2 * P.k, st);
 }
 
-static int vamp_iterate_impl(const VampK& P, int t, hipStream_t st) {
+static int vamp_iterate_impl(const VampK& P, const Const64& c64, int t, hipStream_t st) {
     dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
     hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
     AMP_LAUNCH_CHECK("vamp_k1");
-    dim3 g2(cdiv(P.B, GBM), P.ncp2 / P.bn2);
-    if (P.bn2 == 128)
-        hipLaunchKernelGGL(vamp_k2<128>, g2, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    else
-        hipLaunchKernelGGL(vamp_k2<256>, g2, dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+    launch_k2(P, t, st);
     AMP_LAUNCH_CHECK("vamp_k2");
-    hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, t);
+    hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("vamp_r");
     return AMP_OK;
 }
@@ -449,37 +484,41 @@ size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter) 
 
 int amp_vamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
     VampK P;
-    int rc = vamp_setup(d, c, a, P);
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     return vamp_prepare_impl(P, a, (hipStream_t)stream);
 }
 
 int amp_vamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t t, void* stream) {
     VampK P;
-    int rc = vamp_setup(d, c, a, P);
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     AMP_REQUIRE(t >= 0 && t < a->max_iter, "amp_vamp_iterate: t = %d outside [0, %d)", t, a->max_iter);
     rc = vamp_attrs();
     if (rc) return rc;
-    return vamp_iterate_impl(P, t, (hipStream_t)stream);
+    return vamp_iterate_impl(P, c64, t, (hipStream_t)stream);
 }
 
 int amp_vamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
     VampK P;
-    int rc = vamp_setup(d, c, a, P);
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     return vamp_finalize_impl(P, (hipStream_t)stream);
 }
 
 int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream) {
     VampK P;
-    int rc = vamp_setup(d, c, a, P);
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     rc = vamp_prepare_impl(P, a, st);
     if (rc) return rc;
     for (int t = 0; t < P.max_iter; ++t) {
-        rc = vamp_iterate_impl(P, t, st);
+        rc = vamp_iterate_impl(P, c64, t, st);
         if (rc) return rc;
     }
     return vamp_finalize_impl(P, st);
@@ -491,42 +530,40 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
 int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, float* ms_out,
                      void* stream) {
     VampK P;
-    int rc = vamp_setup(d, c, a, P);
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     AMP_REQUIRE(ms_out, "amp_vamp_profile: null output");
     hipStream_t st = (hipStream_t)stream;
     const int n = P.max_iter;
     std::vector<hipEvent_t> ev(3 * n + 2);
-    for (auto& e : ev) hipEventCreate(&e);
-    hipEventRecord(ev[0], st);
+    for (auto& e : ev) (void)hipEventCreate(&e);
+    (void)hipEventRecord(ev[0], st);
     rc = vamp_prepare_impl(P, a, st);
-    dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128), g2(cdiv(P.B, GBM), P.ncp2 / P.bn2);
+    dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
     for (int t = 0; t < n && !rc; ++t) {
-        hipEventRecord(ev[1 + 3 * t], st);
+        (void)hipEventRecord(ev[1 + 3 * t], st);
         hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        hipEventRecord(ev[2 + 3 * t], st);
-        if (P.bn2 == 128)
-            hipLaunchKernelGGL(vamp_k2<128>, g2, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        else
-            hipLaunchKernelGGL(vamp_k2<256>, g2, dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
-        hipEventRecord(ev[3 + 3 * t], st);
-        hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, t);
+        (void)hipEventRecord(ev[2 + 3 * t], st);
+        launch_k2(P, t, st);
+        (void)hipEventRecord(ev[3 + 3 * t], st);
+        hipLaunchKernelGGL(vamp_r, dim3(1), dim3(RWG), 0, st, P, c64, t);
     }
     if (!rc) rc = vamp_finalize_impl(P, st);
-    hipEventRecord(ev[3 * n + 1], st);
-    hipStreamSynchronize(st);
+    (void)hipEventRecord(ev[3 * n + 1], st);
+    (void)hipStreamSynchronize(st);
     amp_status s;
-    hipMemcpy(&s, P.status, sizeof(s), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&s, P.status, sizeof(s), hipMemcpyDeviceToHost);
     const int T = s.T > 0 ? s.T : n;
     float k1 = 0.f, k2 = 0.f, rr = 0.f, ms = 0.f;
     for (int t = 0; t < T; ++t) {
-        hipEventElapsedTime(&ms, ev[1 + 3 * t], ev[2 + 3 * t]); k1 += ms;
-        hipEventElapsedTime(&ms, ev[2 + 3 * t], ev[3 + 3 * t]); k2 += ms;
-        hipEventElapsedTime(&ms, ev[3 + 3 * t], t + 1 < n ? ev[1 + 3 * (t + 1)] : ev[3 * n + 1]); rr += ms;
+        (void)(void)hipEventElapsedTime(&ms, ev[1 + 3 * t], ev[2 + 3 * t]); k1 += ms;
+        (void)hipEventElapsedTime(&ms, ev[2 + 3 * t], ev[3 + 3 * t]); k2 += ms;
+        (void)hipEventElapsedTime(&ms, ev[3 + 3 * t], t + 1 < n ? ev[1 + 3 * (t + 1)] : ev[3 * n + 1]); rr += ms;
     }
-    hipEventElapsedTime(&ms, ev[0], ev[3 * n + 1]);
+    (void)hipEventElapsedTime(&ms, ev[0], ev[3 * n + 1]);
     ms_out[0] = k1 / T; ms_out[1] = k2 / T; ms_out[2] = rr / T; ms_out[3] = ms;
-    for (auto& e : ev) hipEventDestroy(e);
+    for (auto& e : ev) (void)hipEventDestroy(e);
     AMP_LAUNCH_CHECK("amp_vamp_profile");
     return rc;
 }

@@ -1,0 +1,144 @@
+"""Monte-Carlo driver — drop-in for the reference's ``Model`` (vamp_model.py:17-69,
+bamp_model.py:16-68, scamp_model.py:16-67): the EbN0 sweep that calls the detector once
+per epoch, accumulates its ``Loss``, averages, writes ``{EbN0dB}.json`` and stops early
+once FER < 1e-3.
+
+One process per GPU: with ``torch.distributed`` initialised, the epochs of an SNR point
+are split over the ranks in blocks of ``res`` (one channel realisation per block, as
+``i % res == 0`` regenerates it in the reference), every rank runs its blocks on its own
+GPU with its own random stream, and one all-reduce of the accumulated metrics per SNR
+point merges them before the average (the only exchange: Monte-Carlo epochs are
+independent).  With one process the epoch loop and the random-call order are exactly the
+reference's.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+from torch import nn
+
+from channel import Channel
+from config import Config
+from data import Data
+from loss import Loss
+
+_DIRS = {'vamp': 'VAMP', 'bamp': 'BAMPfinal', 'scamp': 'SCAMP'}   # vamp_model.py:29 etc.
+
+
+def _detector(name: str, config: Config):
+    if name == 'vamp':
+        from vamp import VAMP
+        return VAMP(config)
+    if name == 'bamp':
+        from bamp import BAMP
+        return BAMP(config)
+    if name == 'scamp':
+        from scamp import SCAMP
+        return SCAMP(config)
+    raise ValueError(f'unknown detector {name!r}')
+
+
+def _dist():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank(), torch.distributed.get_world_size()
+    return 0, 1
+
+
+class Model(nn.Module):
+    def __init__(self, config: Config, detector: str = 'vamp', path: str | None = None, amp=None,
+                 seed: int | None = None) -> None:
+        super().__init__()
+        self.config = config
+        self.detector = detector
+        self.rate = config.code_rate
+        self.shannon_limit = config.shannon_limit_dB
+        self.min_snr = self.shannon_limit
+        self.amp = amp if amp is not None else _detector(detector, config)
+        self.loss = Loss(config)
+        self.channel = Channel(config)
+        self.data = Data(config)
+        self.path = path if path is not None else f'Simulations/{_DIRS[detector]}/{config.name}'
+        self.rank, self.world = _dist()
+        if seed is not None:
+            # one independent stream per rank (rank 0 of a 1-process run = the plain seed)
+            np.random.seed(seed + 7919 * self.rank)
+            torch.manual_seed(seed + 7919 * self.rank)
+        if self.rank == 0:
+            os.makedirs(self.path, exist_ok=True)
+
+    # one epoch, in the reference's random-call order (vamp_model.py:55-61)
+    def _epoch(self, SNR: float, new_channel: bool):
+        if new_channel:
+            W, A = self.channel.generate_as_sparc()
+            self._A = A
+            self._W = W
+            if self.detector == 'vamp':
+                self._svd = torch.linalg.svd(A, full_matrices=False)
+        x, sym, idx = self.data.generate_message()
+        y = self._A @ x + self.channel.awgn(SNR)
+        if self.detector == 'vamp':
+            U, s, Vh = self._svd
+            return self.amp(U, s, Vh, y, SNR, x, sym, idx)
+        if self.detector == 'bamp':
+            return self.amp(self._A, y, SNR, x, sym, idx)
+        return self.amp(self._W, self._A, y, SNR, x, sym, idx)
+
+    @torch.no_grad()
+    def run(self, SNR: float) -> Loss:
+        loss = self._epoch(SNR, True)
+        print(loss.loss)
+        return loss
+
+    def _merge(self) -> None:
+        """Sum the per-rank accumulated metrics (one all-reduce per SNR point)."""
+        if self.world == 1:
+            return
+        keys = ['T'] + [k for k in self.loss.keys if k in self.loss.loss]
+        vals = torch.tensor([float(np.asarray(self.loss.loss.get(k, 0.0), dtype=np.float64)) for k in keys],
+                            dtype=torch.float64)
+        if torch.distributed.get_backend() == 'nccl':
+            vals = vals.to(torch.device('cuda', torch.cuda.current_device()))
+        torch.distributed.all_reduce(vals)
+        vals = vals.cpu().numpy()
+        self.loss.loss['T'] = float(vals[0])
+        for k, v in zip(keys[1:], vals[1:]):
+            self.loss.loss[k] = np.float64(v)
+
+    @torch.no_grad()
+    def simulate(self, epochs: int, final=None, start=None, step: float = 1, res: int = 1):
+        if start is None:
+            start = int(np.ceil(self.min_snr))
+        if final is None:
+            final = start + 20.0
+        EbN0dB_range = np.arange(start, final + step, step)
+        SNRdB_range = EbN0dB_range + 10 * np.log10(self.rate)
+        results = []
+        for SNRdB, EbN0dB in zip(SNRdB_range, EbN0dB_range):
+            if self.rank == 0:
+                print(f'EbN0dB={EbN0dB}')
+            SNR = 10 ** (SNRdB / 10)
+            for i in range(epochs):
+                if (i // res) % self.world != self.rank:      # blocks of `res` epochs share a channel
+                    continue
+                loss = self._epoch(SNR, i % res == 0)
+                self.loss.accumulate(loss)
+            if 'fer' not in self.loss.loss:                   # a rank without epochs at this point
+                for k in self.loss.keys:
+                    self.loss.loss[k] = np.float64(0.0)
+            self._merge()
+            self.loss.average(epochs)
+            fer = self.loss.loss['fer']
+            it = self.loss.loss['T']
+            point = {k: (float(v) if np.ndim(v) == 0 else v) for k, v in self.loss.loss.items()}
+            point.update(EbN0dB=float(EbN0dB), SNRdB=float(SNRdB))
+            results.append(point)
+            if self.rank == 0:
+                print(f'FER={fer}, iter={it}')
+                self.loss.export(SNRdB, EbN0dB, self.path)
+            else:
+                self.loss.loss = {'T': 0}
+            if fer < 1e-3:
+                break
+        return results

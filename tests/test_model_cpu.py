@@ -1,0 +1,100 @@
+"""Monte-Carlo driver (model.py, reference vamp_model.py:45-69) on the CPU: the sweep,
+averaging, JSON export and FER early stop with a stand-in detector, and the rank-sharded
+sweep (world size 2, gloo) merging to the same averages."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from config import Config
+from loss import Loss
+
+
+def _cfg():
+    return Config(16, 2, 32, 1, 1, batch=4, generator_mode='sparc', iterations=5, alphabet='QPSK',
+                  channel_profile='uniform', channel_truncation='tail', device='cpu')
+
+
+class FakeAmp:
+    """Stands in for VAMP.forward: same call signature, fills its Loss like Loss.__call__."""
+
+    def __init__(self, config, fer_until_snr=None):
+        self.L = Loss(config)
+        self.calls = 0
+        self.fer_until_snr = fer_until_snr
+        self.shapes = []
+
+    def __call__(self, U, s, Vh, y, SNR, x, sym, idx):
+        self.calls += 1
+        self.shapes.append((tuple(U.shape), tuple(y.shape), len(sym)))
+        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        fer = 1.0 if (self.fer_until_snr is None or SNR < self.fer_until_snr) else 0.0
+        rates = [fer] + [float(rank + 1)] * 13
+        self.L.dump()
+        self.L.loss = {'T': 0}
+        self.L.record(rates, 3)
+        return self.L
+
+
+def test_simulate_export_and_early_stop(tmp_path):
+    from model import Model
+    cfg = _cfg()
+    amp = FakeAmp(cfg, fer_until_snr=10 ** ((2 + 10 * np.log10(cfg.code_rate)) / 10))
+    m = Model(cfg, 'vamp', path=str(tmp_path), amp=amp, seed=0)
+    res = m.simulate(epochs=3, start=0, final=6.0, step=1)
+    # EbN0 0, 1 have fer 1; EbN0 2 has fer 0 -> exported, then the sweep stops
+    assert [r['EbN0dB'] for r in res] == [0.0, 1.0, 2.0]
+    assert amp.calls == 9
+    assert amp.shapes[0] == ((32, 16), (4, 32, 1), 4 * 2)
+    for e in (0, 1, 2):
+        with open(tmp_path / f'{float(e)}.json') as f:
+            d = json.load(f)
+        assert d['T'] == 3.0 and d['EbN0dB'] == float(e)
+        assert set(['fer', 'ser', 'ver', 'nMSE', 'ber', 'SNRdB', 'rate', 'C', 'ShannonLimitdB']) <= set(d)
+        assert d['ser'] == pytest.approx(1.0)
+    assert not os.path.exists(tmp_path / '3.0.json')
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    torch.distributed.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                                         world_size=world)
+    try:
+        from model import Model
+        cfg = _cfg()
+        amp = FakeAmp(cfg)
+        m = Model(cfg, 'vamp', path=out, amp=amp, seed=3)
+        res = m.simulate(epochs=6, start=0, final=1.0, step=1, res=2)
+        with open(os.path.join(out, f'rank{rank}.json'), 'w') as f:
+            json.dump({'calls': amp.calls, 'res': res}, f)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_simulate_two_ranks_gloo(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method='spawn')
+    r0 = json.load(open(tmp_path / 'rank0.json'))
+    r1 = json.load(open(tmp_path / 'rank1.json'))
+    # 6 epochs in blocks of res=2: rank 0 gets blocks {0, 2} (4 epochs), rank 1 block {1}
+    assert r0['calls'] == 2 * 4 and r1['calls'] == 2 * 2
+    for a, b in zip(r0['res'], r1['res']):
+        assert a == b                        # every rank holds the merged average
+        assert a['T'] == pytest.approx(3.0)
+        assert a['ser'] == pytest.approx((4 * 1.0 + 2 * 2.0) / 6)
+    # only rank 0 writes the JSON files
+    assert sorted(p for p in os.listdir(tmp_path) if p.endswith('.json') and not p.startswith('rank')) == \
+        ['0.0.json', '1.0.json']
