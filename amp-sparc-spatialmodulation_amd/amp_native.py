@@ -40,9 +40,13 @@ class AmpCounts(C.Structure):
                [(n, C.c_double) for n in ('mse', 'msef', 'msem', 'mseL')]
 
 
+ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2   # amp_vamp_args.engine
+
+
 class AmpVampArgs(C.Structure):
     _fields_ = [('U', C.c_void_p), ('s', C.c_void_p), ('Vh', C.c_void_p), ('y', C.c_void_p),
-                ('k', C.c_int32), ('max_iter', C.c_int32), ('noise_var', C.c_double), ('sparsity', C.c_double),
+                ('k', C.c_int32), ('max_iter', C.c_int32), ('engine', C.c_int32), ('pad', C.c_int32),
+                ('noise_var', C.c_double), ('sparsity', C.c_double),
                 ('r', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p), ('status', C.c_void_p),
                 ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
@@ -67,6 +71,8 @@ _K = C.POINTER(AmpConstellation)
 # name -> (restype, argtypes); mirrors include/amp_sparc.h
 SIGNATURES = {
     'amp_vamp_workspace_bytes': (C.c_size_t, [_D, _I, _I]),
+    'amp_vamp_select_engine': (C.c_int, [_D, _I, _I]),
+    'amp_vamp_persist_trace': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P, _P]),
     'amp_vamp_run': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),

@@ -10,38 +10,60 @@
 // complex MAC: nothing is wasted).  One H/V is shared by all B trials,
 // so this is a true GEMM and runs on v_mfma_f32_32x32x2_f32 (exact f32, 64 flop/clk/SIMD).
 //
-// Tile: BM = 32 trials x BN (128 | 256) output columns, 4 waves side by side in N,
-// BK = 32.  Both operand tiles are staged K-contiguous in LDS (row stride 36 floats:
-// conflict-free ds_read_b128 for the 16-lane groups), double-buffered with register
-// prefetch (one barrier per K step).  K is split between the two wave halves
-// (lanes 0-31 take k in [0,16), lanes 32-63 k in [16,32) of each K step) so each lane
-// feeds four MFMAs from one ds_read_b128 per operand.
+// Tile: BM = 32 trials x BN (128 | 256) output columns, 4 waves side by side in N, each
+// wave owning BN/128 accumulators of 32 x 32.
+//  * A (the trials, shared by the 4 waves) is staged ONCE per tile in LDS: the whole
+//    32 x K block (K chunks of 512), so the main loop has no barrier and no LDS store.
+//  * W is never staged: each wave owns its columns alone, so it streams them straight from
+//    L2 in an MFMA-packed layout (below) — one fully coalesced 1 KB global_load_dwordx4
+//    per wave feeds 4 MFMAs — through an 8-deep register ring.
+// MFMA-packed weights: for a 32-column block cb and a group g of 8 reduction indices,
+//   Wp[((cb * kap/8 + g) * 64 + lane) * 4 + s] = Wt[cb*32 + (lane & 31)][8g + 4*(lane >> 5) + s],
+// i.e. MFMA s of group g reduces over k = 8g + s (lanes 0-31) and 8g + 4 + s (lanes 32-63);
+// the A fragment is read with the same k mapping (one ds_read_b128 per group).
 //
-// The accumulators are written to an LDS C tile [32][BN+4] that aliases the staging
-// buffers, where the caller's fused epilogue (LMMSE step, Onsager update, section
-// denoiser, ...) reads whole rows/sections.
+// The accumulators are written to an LDS C tile [32][BN+4] that aliases the A block, where
+// the caller's fused epilogue (LMMSE step, Onsager update, section denoiser, ...) reads
+// whole rows/sections.
 #pragma once
 
 #include "amp_common.h"
 
 namespace amp {
 
-constexpr int GBM = 32;
-constexpr int GBK = 32;
-constexpr int GLDK = GBK + 4;
+constexpr int GBM = 32;       // trials per tile
+constexpr int GBK = 64;       // reduction length granule (kap % GBK == 0)
+constexpr int GKC = 512;      // A chunk staged in LDS
+constexpr int GLDA = GKC + 4; // its row stride (floats): conflict-free ds_read_b128
+constexpr int GRING = 8;      // W groups in flight per wave
 
 template <int BN>
 struct GemmCfg {
     static_assert(BN == 128 || BN == 256, "BN must be 128 or 256");
     static constexpr int NACC = BN / 128;                 // 32x32 accumulators per wave
     static constexpr int WN = BN / 4;                     // columns per wave
-    static constexpr int WLD = BN * (GBK / 4) / AMP_WG;   // W float4 per thread per K step
     static constexpr int LDC = BN + 4;                    // C tile row stride (floats)
-    static constexpr int STAGE_FLOATS = 2 * (GBM + BN) * GLDK;
+    static constexpr int A_FLOATS = GBM * GLDA;
     static constexpr int CTILE_FLOATS = GBM * LDC;
-    static constexpr int LDS_FLOATS = STAGE_FLOATS > CTILE_FLOATS ? STAGE_FLOATS : CTILE_FLOATS;
+    static constexpr int LDS_FLOATS = A_FLOATS;           // C tile + epilogue scratch fit inside
+    static_assert(CTILE_FLOATS + 2048 <= A_FLOATS, "epilogue scratch");
     static constexpr size_t LDS_BYTES = (size_t)LDS_FLOATS * 4;
 };
+
+// Packed index of Wt[n][k] (n = output column, k = reduction index) for a kap-long reduction.
+__host__ __device__ __forceinline__ size_t wpack_index(int n, int k, int kap) {
+    const int cb = n >> 5, jj = n & 31, g = k >> 3, w = k & 7;
+    const int lane = jj + 32 * (w >> 2);
+    return (((size_t)cb * (kap >> 3) + g) * 64 + lane) * 4 + (w & 3);
+}
+
+// Packing for the 16x16x4 form (persistent VAMP engine): 16-column block ct, group g of 16
+// reduction indices; MFMA s of the group reduces over k = 16g + 4*(lane >> 4) + s.
+__host__ __device__ __forceinline__ size_t wpack16_index(int n, int k, int kap) {
+    const int ct = n >> 4, g = k >> 4, w = k & 15;
+    const int lane = (n & 15) + 16 * (w >> 2);
+    return (((size_t)ct * (kap >> 4) + g) * 64 + lane) * 4 + (w & 3);
+}
 
 // Plain A operand: rows of `lda` floats, `ka` valid columns (zero beyond, and for rows >= rows).
 struct ALoadPlain {
@@ -54,15 +76,15 @@ struct ALoadPlain {
 };
 
 // Computes the C tile of rows [row0, row0+32) x cols [col0, col0+BN) into `lds` (as the C
-// tile, row stride GemmCfg<BN>::LDC).  `wt` is [Ncp][kap] with kap % 32 == 0 and col0+BN <= Ncp.
+// tile, row stride GemmCfg<BN>::LDC).  `wp` is the MFMA-packed [Ncp][kap] weight,
+// kap % GBK == 0, col0 % BN == 0, col0 + BN <= Ncp.
 template <int BN, class AL>
-__device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict__ wt, int kap, int row0,
+__device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict__ wp, int kap, int row0,
                                           int col0, float* lds) {
     using C = GemmCfg<BN>;
-    float* As = lds;
-    float* Ws = lds + 2 * GBM * GLDK;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
+    const int G = kap >> 3;   // groups of 8 reduction indices
 
     f32x16 acc[C::NACC];
 #pragma unroll
@@ -70,53 +92,70 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-    const int ar = tid >> 3, akq = (tid & 7) * 4;
-    int woff[C::WLD], wlds[C::WLD];
+    const float4* wcol[C::NACC];
 #pragma unroll
-    for (int j = 0; j < C::WLD; ++j) {
-        const int idx = tid + j * AMP_WG;
-        woff[j] = (col0 + (idx >> 3)) * kap + (idx & 7) * 4;
-        wlds[j] = (idx >> 3) * GLDK + (idx & 7) * 4;
-    }
-    float4 ra = al(row0 + ar, akq);
-    float4 rw[C::WLD];
-#pragma unroll
-    for (int j = 0; j < C::WLD; ++j) rw[j] = *reinterpret_cast<const float4*>(wt + woff[j]);
-    *reinterpret_cast<float4*>(As + ar * GLDK + akq) = ra;
-#pragma unroll
-    for (int j = 0; j < C::WLD; ++j) *reinterpret_cast<float4*>(Ws + wlds[j]) = rw[j];
-    __syncthreads();
+    for (int j = 0; j < C::NACC; ++j)
+        wcol[j] = reinterpret_cast<const float4*>(wp) + ((size_t)((col0 >> 5) + wave * C::NACC + j) * G) * 64 + lane;
 
-    const int nk = kap / GBK;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        // prefetch the next K step (the last step re-reads its own tile: no branch, so the
-        // prefetch registers stay registers)
-        const int k0 = min(kt + 1, nk - 1) * GBK;
-        ra = al(row0 + ar, k0 + akq);
+    for (int kc0 = 0; kc0 < kap; kc0 += GKC) {
+        const int kc = min(GKC, kap - kc0);
+        const int q4 = kc >> 2;   // float4 per A row in this chunk
+        const int g0 = kc0 >> 3, gc = kc >> 3;   // gc % GRING == 0 (kap % 64 == 0)
+        // W ring first: its latency overlaps the A staging
+        float4 ring[GRING][C::NACC];
 #pragma unroll
-        for (int j = 0; j < C::WLD; ++j) rw[j] = *reinterpret_cast<const float4*>(wt + woff[j] + k0);
-        const float* a_s = As + cur * GBM * GLDK + li * GLDK + lh * 16;
-        const float* w_s = Ws + cur * BN * GLDK + (wave * C::WN + li) * GLDK + lh * 16;
+        for (int d = 0; d < GRING; ++d)
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const float4 a4 = *reinterpret_cast<const float4*>(a_s + s4 * 4);
+            for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)(g0 + d) * 64];
+        if (kc0 > 0) __syncthreads();   // every wave is done with the previous chunk
+        // stage A[row0 .. row0+32) x [kc0, kc0+kc) (the loader forms fused prologues): all loads
+        // of a half-batch in flight before its LDS stores
+        constexpr int PER = GBM * (GKC / 4) / AMP_WG;   // float4 per thread for a full chunk
+        const int nq = GBM * q4;
 #pragma unroll
-            for (int j = 0; j < C::NACC; ++j) {
-                const float4 b4 = *reinterpret_cast<const float4*>(w_s + j * 32 * GLDK + s4 * 4);
-                acc[j] = mfma32x32x2(a4.x, b4.x, acc[j]);
-                acc[j] = mfma32x32x2(a4.y, b4.y, acc[j]);
-                acc[j] = mfma32x32x2(a4.z, b4.z, acc[j]);
-                acc[j] = mfma32x32x2(a4.w, b4.w, acc[j]);
+        for (int h = 0; h < PER; h += PER / 2) {
+            float4 t4[PER / 2];
+#pragma unroll
+            for (int i = 0; i < PER / 2; ++i) {
+                const int e = tid + (h + i) * AMP_WG;
+                const int row = e / q4, k4 = e - row * q4;
+                t4[i] = (e < nq) ? al(row0 + row, kc0 + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < PER / 2; ++i) {
+                const int e = tid + (h + i) * AMP_WG;
+                const int row = e / q4, k4 = e - row * q4;
+                if (e < nq) *reinterpret_cast<float4*>(lds + row * GLDA + 4 * k4) = t4[i];
             }
         }
-        const int nb = cur ^ 1;
-        *reinterpret_cast<float4*>(As + nb * GBM * GLDK + ar * GLDK + akq) = ra;
-#pragma unroll
-        for (int j = 0; j < C::WLD; ++j) *reinterpret_cast<float4*>(Ws + nb * BN * GLDK + wlds[j]) = rw[j];
         __syncthreads();
+        // Per group: read the NEXT group's A fragment, issue this group's MFMAs, then refill this
+        // ring slot GRING groups ahead.  The scheduling barrier pins that order (left alone, the
+        // scheduler sinks all refills behind the MFMAs and drains them at once).
+        const float* a_s = lds + li * GLDA + 4 * lh;
+        float4 acur = *reinterpret_cast<const float4*>(a_s);
+        for (int gb = 0; gb < gc; gb += GRING) {
+#pragma unroll
+            for (int d = 0; d < GRING; ++d) {
+                const int g = gb + d;
+                const float4 anext = *reinterpret_cast<const float4*>(a_s + 8 * min(g + 1, gc - 1));
+#pragma unroll
+                for (int j = 0; j < C::NACC; ++j) {
+                    acc[j] = mfma32x32x2(acur.x, ring[d][j].x, acc[j]);
+                    acc[j] = mfma32x32x2(acur.y, ring[d][j].y, acc[j]);
+                    acc[j] = mfma32x32x2(acur.z, ring[d][j].z, acc[j]);
+                    acc[j] = mfma32x32x2(acur.w, ring[d][j].w, acc[j]);
+                }
+                // refill GRING groups ahead (clamped: the tail re-reads its last group)
+                const int gn = min(g + GRING, gc - 1);
+#pragma unroll
+                for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)(g0 + gn) * 64];
+                acur = anext;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
     }
-    // accumulators -> LDS C tile (aliases the staging buffers; the loop ended on a barrier)
+    __syncthreads();   // the C tile aliases the A block
     float* ct = lds;
 #pragma unroll
     for (int j = 0; j < C::NACC; ++j)

@@ -79,8 +79,9 @@ int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true)
 inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
 
 // Expanded-weight builders (amp_weights.hip)
+enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2 };
 int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J,
-                  float* wt, int kap, int ncp, hipStream_t st);
+                  float* wt, int kap, int ncp, hipStream_t st, int packed = WPACK32);
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st);
 template <int BN>

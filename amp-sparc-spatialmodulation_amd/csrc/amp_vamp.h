@@ -1,0 +1,175 @@
+// amp_vamp.h — VAMP state shared by the launch-per-kernel engine (amp_vamp.hip) and the
+// persistent engine (amp_vamp_persist.hip): parameter block, workspace carve, and the batch
+// scalars of one iteration (vamp.py:66-82).
+#pragma once
+
+#include "amp_denoise.h"
+#include "amp_gemm.h"
+#include "amp_host.h"
+
+namespace amp {
+
+constexpr int RWG = 1024;   // threads of the reduction / fix-up workgroup
+
+struct VampK {
+    int B, N, n, k, L, M;
+    int kap0, ncp0, kap1, ncp1, kap2, ncp2, bn2;
+    int nblk2, max_iter;
+    double noise_var, sparsity;
+    const float* Wt0;
+    const float* Wt1;
+    const float* Wt2;
+    const float* s;     // singular values (f32 [k])
+    float* s2;          // s**2 (vamp.py:17)
+    float* ytil;        // [B][2k]
+    float* w;           // [B][2k]
+    float* r;           // [B][2N]  (caller's r)
+    float* xm;          // [B][2N]  (caller's xmmse)
+    float* var0;        // [B][N] caller's var: var of even iterations
+    float* var1;        // [B][N] workspace:    var of odd iterations
+    float* secmax;      // [B*L] per-section max logit (fast path, natural units)
+    float* secabs;      // [B*L] per-section max |logit|
+    Partial* parts;     // [max_iter][nblk2]
+    VampIter* iters;    // [max_iter + 1]: iters[t] drives iteration t
+    amp_status* status;
+    // persistent engine
+    int nwg;            // ceil(B / PBM) workgroups
+    const float* Wq1;   // Vh   16x16x4-packed [2k][2N]
+    const float* Wq2;   // V    16x16x4-packed [2N][2k]
+    Partial* pparts;    // [max_iter][nwg]
+    double* pxch;       // [max_iter][nwg][4] rare-path exchange
+    unsigned* pbar;     // [0] arrivals, [1] abort flag (zeroed before every launch)
+    unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
+    Const c;
+};
+
+struct VampWs {
+    float *Wt0, *Wt1, *Wt2, *s2, *ytil, *w, *var1;
+    float *secmax, *secabs;
+    Partial* parts;
+    VampIter* iters;
+    float *Wq1, *Wq2;
+    Partial* pparts;
+    double* pxch;
+    unsigned* pbar;
+    size_t bytes;
+};
+
+static void vamp_geometry(const amp_dims* d, int k, VampK& P) {
+    P.B = d->B; P.N = d->N; P.n = d->n; P.k = k; P.L = d->L; P.M = d->M;
+    P.kap0 = round_up(2 * d->n, GBK); P.ncp0 = round_up(2 * k, 128);
+    P.kap1 = round_up(2 * d->N, GBK); P.ncp1 = round_up(2 * k, 128);
+    P.bn2 = section_bn(d);
+    P.kap2 = round_up(2 * k, GBK); P.ncp2 = round_up(2 * d->N, P.bn2);
+    P.nblk2 = cdiv(d->B, GBM) * (P.ncp2 / P.bn2);
+}
+
+static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
+    VampK P;
+    vamp_geometry(d, k, P);
+    Carve cv(base);
+    VampWs w;
+    w.Wt0 = cv.take<float>((size_t)P.ncp0 * P.kap0);
+    w.Wt1 = cv.take<float>((size_t)P.ncp1 * P.kap1);
+    w.Wt2 = cv.take<float>((size_t)P.ncp2 * P.kap2);
+    w.s2 = cv.take<float>((size_t)k);
+    w.ytil = cv.take<float>((size_t)d->B * 2 * k);
+    w.w = cv.take<float>((size_t)d->B * 2 * k);
+    w.var1 = cv.take<float>((size_t)d->B * d->N);
+    w.secmax = cv.take<float>((size_t)d->B * d->L);
+    w.secabs = cv.take<float>((size_t)d->B * d->L);
+    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
+    w.iters = cv.take<VampIter>((size_t)max_iter + 1);
+    const int nwg = cdiv(d->B, 16);
+    w.Wq1 = cv.take<float>((size_t)2 * k * 2 * d->N);
+    w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * k);
+    w.pparts = cv.take<Partial>((size_t)max_iter * nwg);
+    w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
+    w.pbar = cv.take<unsigned>(64);
+    w.bytes = cv.off;
+    return w;
+}
+
+__device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1) ? P.var1 : P.var0; }
+
+// ---------------------------------------------------------------------------
+// Batch scalars of iteration t (vamp.py:66-82) from sigma2_tilde; t == 0 uses the
+// Tracker's Python-float sigma2_tilde (vamp.py:26).  Called by one workgroup.
+// ---------------------------------------------------------------------------
+__device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
+    const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
+    double ss = 0.0;
+    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s2[i] + vr));  // vamp.py:68
+    ss = group_sum(ss, 64);
+    double* sl = reinterpret_cast<double*>(lds);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sl[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    ss = 0.0;
+    for (int w = 0; w < (int)(blockDim.x / 64); ++w) ss += sl[w];
+    __syncthreads();
+    const float varL = (float)(ss / (double)P.k) * (float)P.noise_var;                         // vamp.py:71
+    const double eta = (double)P.k / (double)P.N;                                              // vamp.py:28
+    float xtv, s2t32;
+    if (first) {
+        xtv = (float)eta * varL + (float)((1.0 - eta) * s2t64);                                // vamp.py:73
+        s2t32 = (float)s2t64;
+    } else {
+        xtv = (float)eta * varL + (float)(1.0 - eta) * s2t;
+        s2t32 = s2t;
+    }
+    const float alpha = clampf_t(xtv / s2t32, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);    // vamp.py:75-77
+    const float sigma2 = clampf_t((alpha / (1.0f - alpha)) * s2t32, AMP_VAR_MIN, AMP_VAR_MAX);  // vamp.py:80-82
+    it.vr = vr;
+    it.alpha = alpha;
+    it.inv1ma = 1.0f / (1.0f - alpha);
+    it.sigma2 = sigma2;
+    it.inv_sigma2 = 1.0f / sigma2;
+    it.s2t = s2t32;
+}
+
+// The record that drives iteration t+1, from the reduced partials of iteration t: the stop
+// record when allclose held (vamp.py:185-186), else the scalars of vamp.py:85-94 and 66-82.
+// Called uniformly by every thread of one workgroup (vamp_lmmse_scalars reduces over k).
+__device__ inline VampIter vamp_advance(const VampK& P, const VampIter& cur, const PartAcc& pa, int fixed, int t,
+                                        float* lds) {
+    VampIter nx;
+    nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.fixed_all = (fixed < 0) ? 1 : 0; nx.G = pa.maxabs;
+    nx.pad1[0] = nx.pad1[1] = nx.pad1[2] = 0.f;
+    if (pa.notclose == 0) {                                              // vamp.py:185-186
+        nx = cur;
+        nx.stopped = 1;
+        nx.T = t + 1;
+        nx.fixed = fixed;
+    } else {
+        // var.mean() (vamp.py:85): float64 sum of the float32 values, NaN / inf propagate
+        const float mean = (float)(pa.sumvar / ((double)P.B * (double)P.N));
+        const float dxdr = clampf_t(mean / cur.sigma2, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);  // vamp.py:85-87
+        const float ns = 1.0f / (1.0f - dxdr);                                                        // vamp.py:89
+        const float s2t = clampf_t((cur.sigma2 * dxdr) * ns, AMP_VAR_MIN, AMP_VAR_MAX);              // vamp.py:92-94
+        nx.dxdr_prev = dxdr;
+        nx.ns_prev = ns;
+        vamp_lmmse_scalars(P, false, 0.0, s2t, lds, nx);
+    }
+    return nx;
+}
+
+__device__ inline amp_status vamp_make_status(const VampK& P, const VampIter& cur, const VampIter& nx, int fixed) {
+    amp_status s;
+    s.T = nx.stopped ? nx.T : P.max_iter;
+    s.nan_state = fixed != 0 ? 1 : 0;
+    s.stopped = nx.stopped;
+    s.pad = 0;
+    s.last_scalar[0] = cur.s2t; s.last_scalar[1] = cur.alpha; s.last_scalar[2] = cur.sigma2;
+    s.last_scalar[3] = nx.stopped ? cur.dxdr_prev : nx.dxdr_prev;
+    return s;
+}
+
+// ---- persistent engine (amp_vamp_persist.hip) ----
+constexpr int PBM = 16;   // trials per workgroup
+
+bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);
+int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu);
+int device_cu_count();
+
+}  // namespace amp

@@ -19,112 +19,9 @@
 #include <mutex>
 #include <vector>
 
-#include "amp_denoise.h"
-#include "amp_gemm.h"
-#include "amp_host.h"
+#include "amp_vamp.h"
 
 namespace amp {
-
-constexpr int RWG = 1024;   // threads of the reduction / fix-up workgroup
-
-struct VampK {
-    int B, N, n, k, L, M;
-    int kap0, ncp0, kap1, ncp1, kap2, ncp2, bn2;
-    int nblk2, max_iter;
-    double noise_var, sparsity;
-    const float* Wt0;
-    const float* Wt1;
-    const float* Wt2;
-    const float* s;     // singular values (f32 [k])
-    float* s2;          // s**2 (vamp.py:17)
-    float* ytil;        // [B][2k]
-    float* w;           // [B][2k]
-    float* r;           // [B][2N]  (caller's r)
-    float* xm;          // [B][2N]  (caller's xmmse)
-    float* var0;        // [B][N] caller's var: var of even iterations
-    float* var1;        // [B][N] workspace:    var of odd iterations
-    float* secmax;      // [B*L] per-section max logit (fast path, natural units)
-    float* secabs;      // [B*L] per-section max |logit|
-    Partial* parts;     // [max_iter][nblk2]
-    VampIter* iters;    // [max_iter + 1]: iters[t] drives iteration t
-    amp_status* status;
-    Const c;
-};
-
-struct VampWs {
-    float *Wt0, *Wt1, *Wt2, *s2, *ytil, *w, *var1;
-    float *secmax, *secabs;
-    Partial* parts;
-    VampIter* iters;
-    size_t bytes;
-};
-
-static void vamp_geometry(const amp_dims* d, int k, VampK& P) {
-    P.B = d->B; P.N = d->N; P.n = d->n; P.k = k; P.L = d->L; P.M = d->M;
-    P.kap0 = round_up(2 * d->n, GBK); P.ncp0 = round_up(2 * k, 128);
-    P.kap1 = round_up(2 * d->N, GBK); P.ncp1 = round_up(2 * k, 128);
-    P.bn2 = section_bn(d);
-    P.kap2 = round_up(2 * k, GBK); P.ncp2 = round_up(2 * d->N, P.bn2);
-    P.nblk2 = cdiv(d->B, GBM) * (P.ncp2 / P.bn2);
-}
-
-static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
-    VampK P;
-    vamp_geometry(d, k, P);
-    Carve cv(base);
-    VampWs w;
-    w.Wt0 = cv.take<float>((size_t)P.ncp0 * P.kap0);
-    w.Wt1 = cv.take<float>((size_t)P.ncp1 * P.kap1);
-    w.Wt2 = cv.take<float>((size_t)P.ncp2 * P.kap2);
-    w.s2 = cv.take<float>((size_t)k);
-    w.ytil = cv.take<float>((size_t)d->B * 2 * k);
-    w.w = cv.take<float>((size_t)d->B * 2 * k);
-    w.var1 = cv.take<float>((size_t)d->B * d->N);
-    w.secmax = cv.take<float>((size_t)d->B * d->L);
-    w.secabs = cv.take<float>((size_t)d->B * d->L);
-    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
-    w.iters = cv.take<VampIter>((size_t)max_iter + 1);
-    w.bytes = cv.off;
-    return w;
-}
-
-__device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1) ? P.var1 : P.var0; }
-
-// ---------------------------------------------------------------------------
-// Batch scalars of iteration t (vamp.py:66-82) from sigma2_tilde; t == 0 uses the
-// Tracker's Python-float sigma2_tilde (vamp.py:26).  Called by one workgroup.
-// ---------------------------------------------------------------------------
-__device__ void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
-    const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
-    double ss = 0.0;
-    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s2[i] + vr));  // vamp.py:68
-    ss = group_sum(ss, 64);
-    double* sl = reinterpret_cast<double*>(lds);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sl[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    ss = 0.0;
-    for (int w = 0; w < (int)(blockDim.x / 64); ++w) ss += sl[w];
-    __syncthreads();
-    const float varL = (float)(ss / (double)P.k) * (float)P.noise_var;                         // vamp.py:71
-    const double eta = (double)P.k / (double)P.N;                                              // vamp.py:28
-    float xtv, s2t32;
-    if (first) {
-        xtv = (float)eta * varL + (float)((1.0 - eta) * s2t64);                                // vamp.py:73
-        s2t32 = (float)s2t64;
-    } else {
-        xtv = (float)eta * varL + (float)(1.0 - eta) * s2t;
-        s2t32 = s2t;
-    }
-    const float alpha = clampf_t(xtv / s2t32, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);    // vamp.py:75-77
-    const float sigma2 = clampf_t((alpha / (1.0f - alpha)) * s2t32, AMP_VAR_MIN, AMP_VAR_MAX);  // vamp.py:80-82
-    it.vr = vr;
-    it.alpha = alpha;
-    it.inv1ma = 1.0f / (1.0f - alpha);
-    it.sigma2 = sigma2;
-    it.inv_sigma2 = 1.0f / sigma2;
-    it.s2t = s2t32;
-}
 
 __global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
     __shared__ __attribute__((aligned(16))) float lds[64];
@@ -308,36 +205,10 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, Const64 c64, int t) {
         pa.notclose += nc;
         __syncthreads();
     }
-    VampIter nx;
-    nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.fixed_all = (fixed < 0) ? 1 : 0; nx.G = pa.maxabs;
-    nx.pad1[0] = nx.pad1[1] = nx.pad1[2] = 0.f;
-    if (pa.notclose == 0) {                                              // vamp.py:185-186
-        nx = cur;
-        nx.stopped = 1;
-        nx.T = t + 1;
-        nx.fixed = fixed;
-    } else {
-        // var.mean() (vamp.py:85): float64 sum of the float32 values, NaN / inf propagate
-        const float mean = (float)(pa.sumvar / ((double)P.B * (double)P.N));
-        const float dxdr = clampf_t(mean / cur.sigma2, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);  // vamp.py:85-87
-        const float ns = 1.0f / (1.0f - dxdr);                                                        // vamp.py:89
-        const float s2t = clampf_t((cur.sigma2 * dxdr) * ns, AMP_VAR_MIN, AMP_VAR_MAX);              // vamp.py:92-94
-        nx.dxdr_prev = dxdr;
-        nx.ns_prev = ns;
-        vamp_lmmse_scalars(P, false, 0.0, s2t, lds, nx);
-    }
+    const VampIter nx = vamp_advance(P, cur, pa, fixed, t, lds);
     if (threadIdx.x == 0) {
         P.iters[t + 1] = nx;
-        if (nx.stopped || t + 1 == P.max_iter) {
-            amp_status s;
-            s.T = nx.stopped ? nx.T : P.max_iter;
-            s.nan_state = fixed != 0 ? 1 : 0;
-            s.stopped = nx.stopped;
-            s.pad = 0;
-            s.last_scalar[0] = cur.s2t; s.last_scalar[1] = cur.alpha; s.last_scalar[2] = cur.sigma2;
-            s.last_scalar[3] = nx.stopped ? cur.dxdr_prev : nx.dxdr_prev;
-            *P.status = s;
-        }
+        if (nx.stopped || t + 1 == P.max_iter) *P.status = vamp_make_status(P, cur, nx, fixed);
     }
 }
 
@@ -384,6 +255,9 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.var0 = (float*)a->var;
     P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.nwg = cdiv(d->B, PBM);
+    P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
+    P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
     return AMP_OK;
@@ -432,18 +306,28 @@ static void launch_k2(const VampK& P, int t, hipStream_t st) {
 }
 
 
-static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t st) {
+static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t st, bool persistent = false) {
     int rc = vamp_attrs();
     if (rc) return rc;
     // Wt0: y~ = (s * U^H) y        (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     rc = build_cweight((const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, st);
     if (rc) return rc;
-    // Wt1: q = Vh r~               (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
-    rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wt1, P.kap1, P.ncp1, st);
-    if (rc) return rc;
-    // Wt2: V (x~ - q), V = Vh^H    (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
-    rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wt2, P.kap2, P.ncp2, st);
-    if (rc) return rc;
+    if (persistent) {
+        // the same two operators, 16x16x4-packed for the persistent engine
+        rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.k, st,
+                           WPACK16);
+        if (rc) return rc;
+        rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wq2, 2 * P.k, 2 * P.N, st,
+                           WPACK16);
+        if (rc) return rc;
+    } else {
+        // Wt1: q = Vh r~               (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
+        rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wt1, P.kap1, P.ncp1, st);
+        if (rc) return rc;
+        // Wt2: V (x~ - q), V = Vh^H    (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
+        rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wt2, P.kap2, P.ncp2, st);
+        if (rc) return rc;
+    }
     const int g = (int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048);
     hipLaunchKernelGGL(vamp_init_kernel, dim3(g), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("vamp_init");
@@ -476,6 +360,33 @@ static int vamp_finalize_impl(const VampK& P, hipStream_t st) {
 using namespace amp;
 
 extern "C" {
+
+// Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
+// boundary: trace[(wg * max_iter + t) * 8 + phase], phases = start, r~ built, GEMM1, w stored,
+// GEMM2 + r, denoiser + partial, barrier passed, scalars ready; then per workgroup
+// [nwg * max_iter * 8 + 2 * wg] = s_memtime / s_memrealtime at kernel start.
+int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
+                           void* stream) {
+    VampK P;
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    const int ncu = device_cu_count();
+    AMP_REQUIRE(trace && vamp_persist_eligible(d, a->k, ncu), "amp_vamp_persist_trace: not eligible / null trace");
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_prepare_impl(P, a, st, true);
+    if (rc) return rc;
+    P.trace = (unsigned long long*)trace;
+    return vamp_persist_launch(P, c64, st, ncu);
+}
+
+int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine) {
+    if (!d || k <= 0) return AMP_E_ARG;
+    const bool elig = vamp_persist_eligible(d, k, device_cu_count());
+    if (engine == AMP_ENGINE_PERSISTENT) return elig ? AMP_ENGINE_PERSISTENT : AMP_E_ARG;
+    if (engine == AMP_ENGINE_AUTO && elig) return AMP_ENGINE_PERSISTENT;
+    return engine == AMP_ENGINE_AUTO || engine == AMP_ENGINE_LAUNCHES ? AMP_ENGINE_LAUNCHES : AMP_E_ARG;
+}
 
 size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter) {
     if (!d || k <= 0 || max_iter <= 0) return 0;
@@ -515,6 +426,18 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
     int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    AMP_REQUIRE(a->engine >= AMP_ENGINE_AUTO && a->engine <= AMP_ENGINE_PERSISTENT, "amp_vamp_run: engine %d",
+                a->engine);
+    const int ncu = device_cu_count();
+    const bool elig = vamp_persist_eligible(d, a->k, ncu);
+    AMP_REQUIRE(a->engine != AMP_ENGINE_PERSISTENT || elig,
+                "amp_vamp_run: persistent engine needs k == N in {64, 128, 256}, M <= 64 and ceil(B/16) = %d <= "
+                "%d CUs", cdiv(d->B, PBM), ncu);
+    if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
+        rc = vamp_prepare_impl(P, a, st, true);
+        if (rc) return rc;
+        return vamp_persist_launch(P, c64, st, ncu);
+    }
     rc = vamp_prepare_impl(P, a, st);
     if (rc) return rc;
     for (int t = 0; t < P.max_iter; ++t) {
@@ -535,6 +458,25 @@ int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_va
     if (rc) return rc;
     AMP_REQUIRE(ms_out, "amp_vamp_profile: null output");
     hipStream_t st = (hipStream_t)stream;
+    const int ncu = device_cu_count();
+    if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && vamp_persist_eligible(d, a->k, ncu))) {
+        // persistent engine: [0] prepare (weights + y~ GEMM), [1] the vamp_persist launch,
+        // [2] 0, [3] the whole forward
+        hipEvent_t e0, e1, e2;
+        (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventCreate(&e2);
+        (void)hipEventRecord(e0, st);
+        rc = vamp_prepare_impl(P, a, st, true);
+        (void)hipEventRecord(e1, st);
+        if (!rc) rc = vamp_persist_launch(P, c64, st, ncu);
+        (void)hipEventRecord(e2, st);
+        (void)hipStreamSynchronize(st);
+        float m01 = 0.f, m12 = 0.f;
+        (void)hipEventElapsedTime(&m01, e0, e1);
+        (void)hipEventElapsedTime(&m12, e1, e2);
+        ms_out[0] = m01; ms_out[1] = m12; ms_out[2] = 0.f; ms_out[3] = m01 + m12;
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipEventDestroy(e2);
+        return rc;
+    }
     const int n = P.max_iter;
     std::vector<hipEvent_t> ev(3 * n + 2);
     for (auto& e : ev) (void)hipEventCreate(&e);

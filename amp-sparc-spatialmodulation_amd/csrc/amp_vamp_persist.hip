@@ -1,0 +1,437 @@
+// amp_vamp_persist.hip — persistent VAMP engine: the whole iteration loop of
+// VAMP.forward (vamp.py:159-187) in ONE cooperative launch.
+//
+// Each workgroup (256 threads = one wave per SIMD, one workgroup per CU) owns PBM = 16
+// trials for the whole forward; their state lives in LDS across iterations:
+//   r, xmmse (c64 rows), var of this and the previous iteration (ping-pong), the section
+//   max / max|xi| of the last denoiser call, and the GEMM A operand (r~, then w).
+// Per iteration t:
+//   1. A <- r~ = (xmmse - dxdr r) * normScalar                         (vamp.py:89-91)
+//   2. q = Vh r~ on v_mfma_f32_16x16x4_f32; w = scale (y~ + vr q) - q    (vamp.py:67-72)
+//   3. x~ - r~ = V w; r = (x~ - alpha r~) / (1 - alpha)                  (vamp.py:72-79)
+//   4. section denoiser on r (amp_denoise.h)                           (vamp.py:84, 96-119)
+//   5. one grid barrier: every workgroup reduces the same per-workgroup partials in the same
+//      order, so every workgroup derives bit-identical batch scalars (mean var, allclose,
+//      max|xi|, vamp.py:85-94 and 185) with no second exchange.  The rare exact-float64
+//      path (amp_denoise.h: G out of range) takes two more barriers, uniformly.
+// The weights are streamed from L2 by each wave in 16x16x4-packed order (amp_gemm.h,
+// wpack16_index): a wave owns 16*NT output columns, NT independent accumulators.
+// y~ = (s Uh) y comes from the launch engine's GEMM once per forward (amp_vamp.hip).
+//
+// Co-residency: ceil(B/16) <= #CUs workgroups, one per CU by its LDS footprint, launched with
+// hipLaunchCooperativeKernel (which rejects a grid that cannot be resident); every barrier
+// spin is bounded (2 s) and raises an abort word that releases every other workgroup.
+#include <algorithm>
+#include <mutex>
+
+#include "amp_vamp.h"
+
+namespace amp {
+
+constexpr int PWG = 256;
+constexpr int PRING = 4;   // W groups in flight per wave
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the 16-row ds_read_b128 and the
+// accumulator stores conflict-free (row r and r+4 land 16 banks apart).
+struct PLayout {
+    int lda, ldr;
+    int offA, offR, offX, offV0, offV1, offSM, offSA, offScr, total;
+};
+
+__host__ __device__ inline PLayout playout(int N, int k, int L) {
+    PLayout y;
+    y.lda = (2 * N > 2 * k ? 2 * N : 2 * k) + 4;
+    y.ldr = 2 * N + 4;
+    int o = 0;
+    y.offA = o; o += PBM * y.lda;
+    y.offR = o; o += PBM * y.ldr;
+    y.offX = o; o += PBM * y.ldr;
+    y.offV0 = o; o += PBM * N;
+    y.offV1 = o; o += PBM * N;
+    y.offSM = o; o += PBM * L;
+    y.offSA = o; o += PBM * L;
+    o = (o + 3) & ~3;
+    y.offScr = o; o += 1024;
+    y.total = o;
+    return y;
+}
+
+// C[16 x 16*NT] (this wave's columns ct0*16 ...) += A[16 x kap] (LDS, row stride lda) . Wq^T,
+// Wq packed by wpack16_index.  Accumulator t, register r: row 4*(lane>>4) + r, column
+// 16*(ct0 + t) + (lane & 15).
+template <int NT>
+__device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __restrict__ wq, int kap, int ct0,
+                                       f32x4 (&acc)[NT]) {
+    const int lane = threadIdx.x & 63;
+    const int G = kap >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float4* wcol = reinterpret_cast<const float4*>(wq) + (size_t)ct0 * G * 64 + lane;
+    float4 ring[PRING][NT];
+#pragma unroll
+    for (int d = 0; d < PRING; ++d)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ring[d][t] = wcol[((size_t)t * G + d) * 64];
+    const float* a_s = sA + (lane & 15) * lda + 4 * (lane >> 4);
+    float4 acur = *reinterpret_cast<const float4*>(a_s);
+    for (int gb = 0; gb < G; gb += PRING) {
+#pragma unroll
+        for (int d = 0; d < PRING; ++d) {
+            const int g = gb + d;
+            const float4 anext = *reinterpret_cast<const float4*>(a_s + 16 * min(g + 1, G - 1));
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                acc[t] = mfma16x16x4(acur.x, ring[d][t].x, acc[t]);
+                acc[t] = mfma16x16x4(acur.y, ring[d][t].y, acc[t]);
+                acc[t] = mfma16x16x4(acur.z, ring[d][t].z, acc[t]);
+                acc[t] = mfma16x16x4(acur.w, ring[d][t].w, acc[t]);
+            }
+            const int gn = min(g + PRING, G - 1);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) ring[d][t] = wcol[((size_t)t * G + gn) * 64];
+            acur = anext;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// Grid barrier: arrival counter + abort word in pbar (zeroed before the launch).  The
+// workgroup's payload stores precede it in program order (thread 0 stores them or the
+// barrier below orders them); agent-scope release on arrival, acquire after the wait.
+__device__ bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(pbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(pbar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
+                __hip_atomic_store(pbar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *s_flag = ok;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+struct PDenoisePolicy {
+    const float* r;
+    float* x;
+    float* vnew;
+    const float* vprev;
+    float* sm;
+    float* sa;
+    int ldr, M, spr, N;
+    float inv;
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
+        const int row = sec / spr, sj = sec - row * spr;
+        const float2 v = *reinterpret_cast<const float2*>(r + row * ldr + 2 * (sj * M + m));
+        rr = v.x; ri = v.y; it = inv;
+    }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
+        const int row = sec / spr, sj = sec - row * spr;
+        *reinterpret_cast<float2*>(x + row * ldr + 2 * (sj * M + m)) = make_float2(xr, xi);
+        const int vo = row * N + sj * M + m;
+        vnew[vo] = var;
+        pa.sumvar += (double)var;
+        pa.notclose += torch_close(var, vprev[vo]) ? 0u : 1u;     // vamp.py:185
+    }
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
+        sm[sec] = smax;
+        sa[sec] = sabs;
+    }
+};
+
+template <int NT, int KK>
+__global__ __launch_bounds__(PWG, 1) void vamp_persist(VampK P, Const64 c64) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int s_flag;
+    __shared__ double s_d[PWG / 64][4];
+    const PLayout Y = playout(P.N, P.k, P.L);
+    float* sA = lds + Y.offA;
+    float* sR = lds + Y.offR;
+    float* sX = lds + Y.offX;
+    float* sM = lds + Y.offSM;
+    float* sS = lds + Y.offSA;
+    float* scr = lds + Y.offScr;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wg = blockIdx.x, nwg = gridDim.x;
+    const int row0 = wg * PBM, nrows = min(PBM, P.B - row0);
+    const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
+    const int ldr = Y.ldr, lda = Y.lda;
+    const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
+
+    // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
+    {
+        const float p = (float)P.sparsity;
+        for (int e = tid; e < PBM * twoN; e += PWG) {
+            const int row = e / twoN, col = e - row * twoN;
+            sR[row * ldr + col] = 0.f;
+            sX[row * ldr + col] = (row < nrows && (col & 1) == 0) ? p : 0.f;
+        }
+        for (int e = tid; e < PBM * N; e += PWG) lds[Y.offV1 + e] = 1.0f;
+    }
+    // y~ rows and s^2 of this wave's GEMM1 columns, in the accumulator layout
+    float yt[NT][4], s2c[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 16 * (ct0 + t) + (lane & 15);
+        s2c[t] = P.s2[col >> 1];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * (lane >> 4) + r;
+            yt[t][r] = (row < nrows) ? P.ytil[(size_t)(row0 + row) * twok + col] : 0.f;
+        }
+    }
+    VampIter cur = P.iters[0];   // vamp_init_scalars (vamp.py:26, 66-82 at t = 0)
+    unsigned long long* trc = P.trace;
+    auto stamp = [&](int t, int ph) {
+        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * 8 + ph] = __builtin_amdgcn_s_memtime();
+    };
+    if (trc && tid == 0) {
+        trc[(size_t)nwg * P.max_iter * 8 + 2 * wg] = __builtin_amdgcn_s_memtime();
+        trc[(size_t)nwg * P.max_iter * 8 + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    unsigned nbar = 0;
+    int fixed = 0, last_t = 0, aborted = 0;
+    VampIter nx = cur;
+
+    for (int t = 0; t < P.max_iter; ++t) {
+        last_t = t;
+        stamp(t, 0);
+        const float* vprev = lds + ((t & 1) ? Y.offV0 : Y.offV1);
+        float* vnew = lds + ((t & 1) ? Y.offV1 : Y.offV0);
+        // 1. A <- r~ (vamp.py:91; t = 0: dxdr 0, normScalar 1)
+        for (int e = tid; e < PBM * (twoN >> 2); e += PWG) {
+            const int row = e / (twoN >> 2), c4 = 4 * (e - row * (twoN >> 2));
+            const float4 x = *reinterpret_cast<const float4*>(sX + row * ldr + c4);
+            const float4 q = *reinterpret_cast<const float4*>(sR + row * ldr + c4);
+            *reinterpret_cast<float4*>(sA + row * lda + c4) =
+                make_float4((x.x - cur.dxdr_prev * q.x) * cur.ns_prev, (x.y - cur.dxdr_prev * q.y) * cur.ns_prev,
+                            (x.z - cur.dxdr_prev * q.z) * cur.ns_prev, (x.w - cur.dxdr_prev * q.w) * cur.ns_prev);
+        }
+        __syncthreads();
+        stamp(t, 1);
+        // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
+        f32x4 acc[NT];
+        gemm16<NT>(sA, lda, P.Wq1, twoN, ct0, acc);
+        __syncthreads();
+        stamp(t, 2);
+#pragma unroll
+        for (int t2 = 0; t2 < NT; ++t2) {
+            const int col = 16 * (ct0 + t2) + (lane & 15);
+            const float sc = 1.0f / (s2c[t2] + cur.vr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float q = acc[t2][r];
+                sA[(4 * (lane >> 4) + r) * lda + col] = sc * (yt[t2][r] + cur.vr * q) - q;
+            }
+        }
+        __syncthreads();
+        stamp(t, 3);
+        // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
+        gemm16<NT>(sA, lda, P.Wq2, twok, ct0, acc);
+#pragma unroll
+        for (int t2 = 0; t2 < NT; ++t2) {
+            const int col = 16 * (ct0 + t2) + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = (4 * (lane >> 4) + r) * ldr + col;
+                const float rt = (sX[o] - cur.dxdr_prev * sR[o]) * cur.ns_prev;
+                const float xt = acc[t2][r] + rt;
+                sR[o] = (xt - cur.alpha * rt) * cur.inv1ma;
+            }
+        }
+        __syncthreads();
+        stamp(t, 4);
+        // 4. denoiser (vamp.py:84)
+        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, spr, N, cur.inv_sigma2};
+        PartAcc pa;
+        denoise_sections<true, KK>(pol, nrows * spr, M, P.c, pa);
+        part_block_store(pa, P.pparts + (size_t)t * nwg + wg, scr);
+        stamp(t, 5);
+        // 5. batch scalars
+        if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+        stamp(t, 6);
+        PartAcc g = part_reduce_all(P.pparts + (size_t)t * nwg, nwg, scr);
+        fixed = 0;
+        if (part_allnan(g)) {
+            // the reference's G is NaN / inf: every section of this iteration is NaN
+            if (!cur.fixed_all) {
+                const float qn = __int_as_float(0x7fc00000);
+                for (int e = tid; e < nrows * twoN; e += PWG) sX[(e / twoN) * ldr + e % twoN] = qn;
+                for (int e = tid; e < nrows * N; e += PWG) vnew[e] = qn;
+            }
+            g.sumvar = __longlong_as_double(0x7ff8000000000000LL);
+            g.notclose = 1;
+            fixed = -1;
+        } else if (part_danger(g)) {
+            // (a) exact float64 G over the candidate sections of every workgroup
+            const double G32 = g.maxabs, slack = logit_slack(G32);
+            const float inv = cur.inv_sigma2;
+            auto ldf = [=](int s) {
+                const int row = s / spr, sj = s - row * spr;
+                const float* rp = sR + row * ldr + 2 * sj * M;
+                return [=](int m, float& rr, float& ri, float& it) {
+                    rr = rp[2 * m]; ri = rp[2 * m + 1]; it = inv;
+                };
+            };
+            double gm = 0.0;
+            for (int s = tid; s < nrows * spr; s += PWG)
+                if ((double)sS[s] >= G32 - slack) gm = fmax(gm, section_absmax_f64(ldf(s), M, c64));
+            gm = group_max(gm, 64);
+            if (lane == 0) s_d[wave][0] = gm;
+            __syncthreads();
+            if (tid == 0) {
+                double m4 = 0.0;
+                for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
+                P.pxch[((size_t)t * nwg + wg) * 4 + 0] = m4;
+            }
+            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+            double G = 0.0;
+            for (int w = 0; w < nwg; ++w) G = fmax(G, P.pxch[((size_t)t * nwg + w) * 4 + 0]);
+            // (b) exact recompute of this workgroup's sections below the danger line
+            double dsum = 0.0;
+            int dnc = 0, cnt = 0;
+            for (int s = tid; s < nrows * spr; s += PWG) {
+                if (!((double)sM[s] - G < AMP_DANGER + slack)) continue;
+                ++cnt;
+                const int row = s / spr, sj = s - row * spr;
+                float* xp = sX + row * ldr + 2 * sj * M;
+                const int v0 = row * N + sj * M;
+                auto st = [&](int m, float xr, float xi, float var) {
+                    const float old = vnew[v0 + m];
+                    dsum += (double)var - (double)old;
+                    dnc += (torch_close(var, vprev[v0 + m]) ? 0 : 1) - (torch_close(old, vprev[v0 + m]) ? 0 : 1);
+                    xp[2 * m] = xr; xp[2 * m + 1] = xi;
+                    vnew[v0 + m] = var;
+                };
+                exact_section_f64<true>(ldf(s), st, M, c64, G);
+            }
+            dsum = group_sum(dsum, 64);
+            dnc = group_sum(dnc, 64);
+            cnt = group_sum(cnt, 64);
+            __syncthreads();
+            if (lane == 0) { s_d[wave][1] = dsum; s_d[wave][2] = (double)dnc; s_d[wave][3] = (double)cnt; }
+            __syncthreads();
+            if (tid == 0) {
+                double a = 0.0, b = 0.0, c = 0.0;
+                for (int w = 0; w < PWG / 64; ++w) { a += s_d[w][1]; b += s_d[w][2]; c += s_d[w][3]; }
+                P.pxch[((size_t)t * nwg + wg) * 4 + 1] = a;
+                P.pxch[((size_t)t * nwg + wg) * 4 + 2] = b;
+                P.pxch[((size_t)t * nwg + wg) * 4 + 3] = c;
+            }
+            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+            double a = 0.0, b = 0.0, c = 0.0;
+            for (int w = 0; w < nwg; ++w) {
+                const double* q = P.pxch + ((size_t)t * nwg + w) * 4;
+                a += q[1]; b += q[2]; c += q[3];
+            }
+            g.sumvar += a;   // (sum - old) + new, in float64
+            g.notclose = (uint32_t)((long long)g.notclose + (long long)b);
+            g.maxabs = G;
+            fixed = (int)c;
+        }
+        nx = vamp_advance(P, cur, g, fixed, t, scr);
+        stamp(t, 7);
+        if (nx.stopped || t + 1 == P.max_iter) break;
+        cur = nx;
+    }
+    __syncthreads();
+    // outputs: r (decision input, vamp.py:187), xmmse, var of the last executed iteration
+    const float* vlast = lds + ((last_t & 1) ? Y.offV1 : Y.offV0);
+    for (int e = tid; e < nrows * twoN; e += PWG) {
+        const int row = e / twoN, col = e - row * twoN;
+        P.r[(size_t)(row0 + row) * twoN + col] = sR[row * ldr + col];
+        P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldr + col];
+    }
+    for (int e = tid; e < nrows * N; e += PWG) P.var0[(size_t)row0 * N + e] = vlast[e];
+    if (wg == 0 && tid == 0) {
+        amp_status s = vamp_make_status(P, cur, nx, fixed);
+        if (aborted) s.nan_state = -1;
+        *P.status = s;
+    }
+}
+
+static std::once_flag g_pers_once;
+static int g_ncu = 0;
+
+int device_cu_count() {
+    std::call_once(g_pers_once, [] {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&g_ncu, hipDeviceAttributeMultiprocessorCount,
+                                                                      dev) != hipSuccess)
+            g_ncu = 0;
+    });
+    return g_ncu;
+}
+
+bool vamp_persist_eligible(const amp_dims* d, int k, int ncu) {
+    if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
+    if (cdiv(d->B, PBM) > ncu) return false;
+    return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
+}
+
+template <int NT, int KK>
+static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) {
+    const void* fn = (const void*)vamp_persist<NT, KK>;
+    const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) {
+        set_error("vamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    VampK Pc = P;
+    Const64 cc = c64;
+    void* args[] = {(void*)&Pc, (void*)&cc};
+    e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(PWG), args, (unsigned)lds, st);
+    if (e != hipSuccess) {
+        set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, PWG, lds,
+                  hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    return AMP_OK;
+}
+
+template <int NT>
+static int persist_launch_nt(const VampK& P, const Const64& c64, hipStream_t st) {
+    switch (P.c.K) {
+    case 1: return persist_launch_t<NT, 1>(P, c64, st);
+    case 2: return persist_launch_t<NT, 2>(P, c64, st);
+    case 4: return persist_launch_t<NT, 4>(P, c64, st);
+    case 8: return persist_launch_t<NT, 8>(P, c64, st);
+    default: return persist_launch_t<NT, 16>(P, c64, st);
+    }
+}
+
+int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu) {
+    (void)ncu;
+    hipError_t e = hipMemsetAsync(P.pbar, 0, 64 * sizeof(unsigned), st);
+    if (e != hipSuccess) {
+        set_error("vamp_persist: hipMemsetAsync: %s", hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    switch (P.N / 32) {   // NT = 2N / 64 column tiles of 16 per wave
+    case 2: return persist_launch_nt<2>(P, c64, st);
+    case 4: return persist_launch_nt<4>(P, c64, st);
+    case 8: return persist_launch_nt<8>(P, c64, st);
+    default:
+        set_error("vamp_persist: N = %d not supported", P.N);
+        return AMP_E_ARG;
+    }
+}
+
+}  // namespace amp

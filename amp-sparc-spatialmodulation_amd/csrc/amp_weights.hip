@@ -33,12 +33,19 @@ int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled) {
     return AMP_OK;
 }
 
+__device__ __forceinline__ size_t widx(int n, int k, int kap, int packed) {
+    return packed == WPACK32 ? wpack_index(n, k, kap) : packed == WPACK16 ? wpack16_index(n, k, kap)
+                                                                           : (size_t)n * kap + k;
+}
+
 // Wt[2o][2j] = Re X, Wt[2o][2j+1] = -Im X, Wt[2o+1][2j] = Im X, Wt[2o+1][2j+1] = Re X,
 // X[o][j] = rowscale[o] * op(src[o*so + j*sj]), op = conj if `conj`; zero padding up to [ncp][kap].
+// packed: WPACK32 / WPACK16 = the MFMA-packed layouts the GEMM engines stream (amp_gemm.h),
+// WPACK_NONE = row-major.
 // rowscale multiplies like the reference's `s.view(-1,1) * Uh` (f32 x c64 -> per-component products).
 __global__ void build_cweight_kernel(const float2* __restrict__ src, long so, long sj, int conj,
                                      const float* __restrict__ rowscale, int O, int J, float* __restrict__ wt,
-                                     int kap, int ncp) {
+                                     int kap, int ncp, int packed) {
     const long total = (long)(ncp / 2) * (kap / 2);
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / (kap / 2)), j = (int)(e % (kap / 2));
@@ -53,19 +60,17 @@ __global__ void build_cweight_kernel(const float2* __restrict__ src, long so, lo
                 xi = s * xi;
             }
         }
-        float* w0 = wt + (size_t)(2 * o) * kap + 2 * j;
-        float* w1 = w0 + kap;
-        w0[0] = xr;
-        w0[1] = -xi;
-        w1[0] = xi;
-        w1[1] = xr;
+        wt[widx(2 * o, 2 * j, kap, packed)] = xr;
+        wt[widx(2 * o, 2 * j + 1, kap, packed)] = -xi;
+        wt[widx(2 * o + 1, 2 * j, kap, packed)] = xi;
+        wt[widx(2 * o + 1, 2 * j + 1, kap, packed)] = xr;
     }
 }
 
 // Wt[o][j] = |src[o*so + j*sj]|^2 with torch's complex abs (correctly rounded hypot) then an
 // f32 square (bamp.py:18 `H.abs()**2`).
 __global__ void build_abs2_kernel(const float2* __restrict__ src, long so, long sj, int O, int J,
-                                  float* __restrict__ wt, int kap, int ncp) {
+                                  float* __restrict__ wt, int kap, int ncp) {   // always packed
     const long total = (long)ncp * kap;
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / kap), j = (int)(e % kap);
@@ -75,22 +80,33 @@ __global__ void build_abs2_kernel(const float2* __restrict__ src, long so, long 
             const float a = (float)sqrt((double)z.x * z.x + (double)z.y * z.y);
             v = a * a;
         }
-        wt[e] = v;
+        wt[wpack_index(o, j, kap)] = v;
     }
 }
 
+// row-major [ncp][kap] -> MFMA-packed
+__global__ void pack_weight_kernel(const float* __restrict__ src, float* __restrict__ dst, int kap, int ncp) {
+    const long total = (long)ncp * kap;
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x)
+        dst[wpack_index((int)(e / kap), (int)(e % kap), kap)] = src[e];
+}
+
 int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J, float* wt,
-                  int kap, int ncp, hipStream_t st) {
+                  int kap, int ncp, hipStream_t st, int packed) {
+    AMP_REQUIRE(packed == WPACK_NONE || (kap % GBK == 0 && ncp % 128 == 0) ||
+                    (packed == WPACK16 && kap % 16 == 0 && ncp % 16 == 0),
+                "build_cweight: kap %d / ncp %d not tiled", kap, ncp);
     const long total = (long)(ncp / 2) * (kap / 2);
     const int grid = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(build_cweight_kernel, dim3(grid), dim3(256), 0, st, src, so, sj, conj, rowscale, O, J, wt,
-                       kap, ncp);
+                       kap, ncp, packed);
     AMP_LAUNCH_CHECK("build_cweight");
     return AMP_OK;
 }
 
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st) {
+    AMP_REQUIRE(kap % GBK == 0 && ncp % 128 == 0, "build_abs2_weight: kap %d / ncp %d not tiled", kap, ncp);
     const long total = (long)ncp * kap;
     const int grid = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(build_abs2_kernel, dim3(grid), dim3(256), 0, st, src, so, sj, O, J, wt, kap, ncp);
@@ -149,25 +165,35 @@ extern "C" {
 const char* amp_last_error(void) { return amp::g_err; }
 
 const char* amp_build_info(void) {
-    return "amp_sparc gfx950: fp32 MFMA v_mfma_f32_32x32x2_f32 GEMM engine (BM=32, BK=32, BN=128/256), "
+    return "amp_sparc gfx950: fp32 MFMA v_mfma_f32_32x32x2_f32 GEMM engine (BM=32, A block in LDS, "
+           "MFMA-packed weights streamed from L2, BN=128/256), "
            "fused LMMSE/Onsager/section-denoiser epilogues";
 }
 
-// Test/diagnostic entry point: C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T (first ka columns of A valid,
-// first nc columns of C stored).  Requirements: lda % 4 == 0, ka % 4 == 0, kap % 32 == 0, ncp % 128 == 0.
+// Test/diagnostic entry point: C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T with a row-major Wt
+// (first ka columns of A valid, first nc columns of C stored); packs Wt into a stream-ordered
+// temporary first.  Requirements: lda % 4 == 0, ka % 4 == 0, kap % 64 == 0, ncp % 128 == 0.
 int amp_gemm_nt_f32(const void* a, int32_t lda, int32_t rows, int32_t ka, const void* wt, int32_t kap, int32_t ncp,
                     void* c, int32_t ldc, int32_t nc, void* stream) {
-    AMP_REQUIRE(lda % 4 == 0 && ka % 4 == 0 && kap % 32 == 0 && ncp % 128 == 0 && ka <= kap && nc <= ncp,
+    AMP_REQUIRE(lda % 4 == 0 && ka % 4 == 0 && kap % amp::GBK == 0 && ncp % 128 == 0 && ka <= kap && nc <= ncp,
                 "amp_gemm_nt_f32: bad shape (lda %d ka %d kap %d ncp %d nc %d)", lda, ka, kap, ncp, nc);
-    return amp::gemm_store((const float*)a, lda, rows, ka, (const float*)wt, kap, ncp, (float*)c, ldc, nc,
-                           (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    float* wp = nullptr;
+    hipError_t e = hipMallocAsync((void**)&wp, (size_t)kap * ncp * sizeof(float), st);
+    AMP_REQUIRE(e == hipSuccess, "amp_gemm_nt_f32: hipMallocAsync: %s", hipGetErrorString(e));
+    const long total = (long)ncp * kap;
+    hipLaunchKernelGGL(amp::pack_weight_kernel, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0,
+                       st, (const float*)wt, wp, kap, ncp);
+    int rc = amp::gemm_store((const float*)a, lda, rows, ka, wp, kap, ncp, (float*)c, ldc, nc, st);
+    (void)hipFreeAsync(wp, st);
+    return rc;
 }
 
 // Test/diagnostic entry point for the complex weight expansion (see build_cweight_kernel).
 int amp_build_cweight(const void* src, int64_t so, int64_t sj, int32_t conj, const void* rowscale, int32_t O,
                       int32_t J, void* wt, int32_t kap, int32_t ncp, void* stream) {
     return amp::build_cweight((const float2*)src, so, sj, conj, (const float*)rowscale, O, J, (float*)wt, kap, ncp,
-                              (hipStream_t)stream);
+                              (hipStream_t)stream, amp::WPACK_NONE);
 }
 
 }  // extern "C"

@@ -154,9 +154,13 @@ def block_denoise(config: Config, s: torch.Tensor, tau, mode: int):
 
 
 class VAMP(nn.Module):
-    def __init__(self, config: Config) -> None:
+    """``engine``: nat.ENGINE_AUTO (persistent single-launch engine when the shape allows it,
+    else three launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h)."""
+
+    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO) -> None:
         super().__init__()
         self.config = config
+        self.engine = engine
         self.E = config.Na / config.Nr                                   # vamp.py:154
         self.sparsity = config.Na / config.Nt                            # vamp.py:155
         self.layers = nn.ModuleList([VAMPLayer(config, i) for i in range(config.N_Layers)])
@@ -167,6 +171,7 @@ class VAMP(nn.Module):
     def detect(self, U, s, Vh, y, SNR: float) -> Tracker:
         """All iterations on the device, asynchronous (no host sync)."""
         T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
+        T.args.engine = self.engine
         nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
                   'amp_vamp_run')
         return T
@@ -178,6 +183,8 @@ class VAMP(nn.Module):
         # decision on T.r (vamp.py:187); counters land next to the status record
         self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=T.buf.res[64:])
         status, counts = read_result(T.buf.res)                          # the forward's one host sync
+        if status.nan_state < 0:
+            raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')
         self.L.record(self.L.rates_from_counts(counts), int(status.T))
         self.last = T
         return self.L

@@ -79,6 +79,24 @@ def cpu_baseline(cfgname, EbN0, seed, sample_trials):
                        f'T={out["T"]}, numpy oracle incl. decision+metrics, {dt:.1f} s')
 
 
+def traffic_from_profile(persistent):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary of the same
+    command (tools/profile.sh -> tools/prof_summary.py -> profiles/): FETCH_SIZE x 2 (gfx950
+    tallies 128-B requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE.  None when absent."""
+    import glob
+    import re
+    name = 'amp::vamp_persist' if persistent else 'amp::vamp_k2'
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_cfg4_vamp*.txt')))
+    for f in reversed(files):
+        for line in open(f):
+            if line.startswith(name) and 'FETCH_SIZE' in line and 'WRITE_SIZE' in line:
+                fe = re.search(r'FETCH_SIZE=(\d+)KB', line)
+                wr = re.search(r'WRITE_SIZE=(\d+)KB', line)
+                if fe and wr:
+                    return (2 * int(fe.group(1)) + int(wr.group(1))) * 1024
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -89,6 +107,7 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--cpu-sample', type=int, default=4096)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--engine', default='auto', choices=['auto', 'launches', 'persistent'])
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -106,12 +125,14 @@ def main():
     from vamp import VAMP
     import ctypes as C
     import amp_native as nat
+    nat.lib()
 
     Nt, Na, Nr, B, alph, iters = CONFIGS[args.config]
     cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cuda')
     inp = make_inputs(cfg, args.seed + rank, args.ebn0, device)
-    det = VAMP(cfg)
+    engine = {'auto': nat.ENGINE_AUTO, 'launches': nat.ENGINE_LAUNCHES, 'persistent': nat.ENGINE_PERSISTENT}[args.engine]
+    det = VAMP(cfg, engine=engine)
 
     def step():
         return det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
@@ -134,14 +155,24 @@ def main():
     T = int(L.loss['T'])
     ver, ser = float(L.loss['ver']), float(L.loss['ser'])
 
-    # dominant kernel (GEMM2 + fused denoiser) timed with HIP events on the stream it runs on
+    # dominant kernel timed with HIP events on the stream it runs on: the persistent engine's
+    # single vamp_persist launch (T iterations: 2 complex mat-vecs per trial-iteration), or the
+    # launch engine's GEMM2 + fused denoiser kernel (one complex mat-vec per trial)
     Tr = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    persistent = nat.lib().amp_vamp_select_engine(C.byref(Tr.dims), Tr.k, Tr.args.engine) == nat.ENGINE_PERSISTENT
     ms = (C.c_float * 4)()
     nat.check(nat.lib().amp_vamp_profile(C.byref(Tr.dims), C.byref(Tr.const), C.byref(Tr.args), ms, Tr.stream),
               'amp_vamp_profile')
     N, k = Nt, min(Nt, Nr)
-    flops_k2 = 8.0 * B * N * k                     # complex [N x k] . [k] per trial = 8 real flop / CMAC
-    achieved = flops_k2 / (ms[1] * 1e-3) / 1e12
+    flops_mv = 8.0 * B * N * k                     # complex [N x k] . [k] per trial = 8 real flop / CMAC
+    if persistent:
+        kern, flops_launch = 'vamp_persist (whole iteration loop: 2 GEMMs + LMMSE + Onsager + denoiser per iteration)', \
+            2.0 * flops_mv * T
+        kms = {'prepare': ms[0], 'vamp_persist': ms[1], 'forward': ms[3]}
+    else:
+        kern, flops_launch = 'vamp_k2 (GEMM2 + Onsager update + section denoiser)', flops_mv
+        kms = {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}
+    achieved = flops_launch / (ms[1] * 1e-3) / 1e12
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -157,11 +188,10 @@ def main():
                                f'EbN0={args.ebn0} dB, one channel per batch',
                    'global_batch': world * B, 'parallelism': f'trial-shard x{world} (independent epochs)'},
         'detail': {'T': T, 'ver': ver, 'ser': ser, 'trial_iterations_per_s': world * B * T / (el / args.steps),
-                   'kernel_ms': {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}},
+                   'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': None,
-                     'kernel': 'vamp_k2 (GEMM2 + Onsager update + section denoiser)',
-                     'flop_per_launch': flops_k2},
+                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),
+                     'kernel': kern, 'flop_per_launch': flops_launch},
     }
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args.config, args.ebn0, args.seed, args.cpu_sample)

@@ -87,6 +87,8 @@ typedef struct amp_vamp_args {
     const void* y;      /* c64 [B][n] */
     int32_t k;          /* min(n, N) */
     int32_t max_iter;   /* config.N_Layers */
+    int32_t engine;     /* amp_vamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT */
+    int32_t pad;
     double noise_var;   /* Na/Nr/SNR (vamp.py:179) */
     double sparsity;    /* Na/Nt (vamp.py:155) */
     void* r;            /* out c64 [B][N]: decision input T.r (vamp.py:187) */
@@ -97,6 +99,24 @@ typedef struct amp_vamp_args {
     size_t ws_bytes;
 } amp_vamp_args;
 
+/* Engines of amp_vamp_run (same results up to f32 summation order):
+ *  LAUNCHES   three launches per iteration (the layer-level path below);
+ *  PERSISTENT one cooperative launch for the whole loop: each workgroup keeps 16 trials'
+ *             state in LDS across iterations, one grid barrier per iteration carries the
+ *             batch-global scalars (needs k == N, N % 32 == 0, N <= 256, M <= 64 and
+ *             ceil(B/16) workgroups co-resident: B <= 16 x #CUs);
+ *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
+#define AMP_ENGINE_AUTO 0
+#define AMP_ENGINE_LAUNCHES 1
+#define AMP_ENGINE_PERSISTENT 2
+
+/* The engine amp_vamp_run will use for this shape on the current device (LAUNCHES or
+ * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
+int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
+/* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
+ * phase into trace (device, nwg * max_iter * 8 + 2 * nwg uint64; layout in amp_vamp.hip). */
+int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
+                           void* stream);
 size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter);
 int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
 /* Layer-level pieces of amp_vamp_run: prepare = Tracker (vamp.py:13-28);
@@ -106,8 +126,9 @@ int amp_vamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_va
 int amp_vamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t t, void* stream);
 int amp_vamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
- * launches; ms_out[4] = mean GEMM1 / GEMM2+denoiser / reduction kernel time per executed
- * iteration and the whole forward, in milliseconds. */
+ * launches, in milliseconds.  LAUNCHES engine: ms_out[4] = mean GEMM1 / GEMM2+denoiser /
+ * reduction kernel time per executed iteration and the whole forward.  PERSISTENT engine
+ * (as a->engine selects it): prepare (weights + y~ GEMM), the vamp_persist launch, 0, total. */
 int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, float* ms_out,
                      void* stream);
 
@@ -174,7 +195,8 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
 size_t amp_map_decide_workspace_bytes(const amp_dims* d);
 
 /* ---- Building blocks exposed for tests and tools ---- */
-/* C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T on fp32 MFMA (first ka columns of A, first nc of C). */
+/* C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T on fp32 MFMA (first ka columns of A, first nc of C);
+   Wt row-major, kap % 64 == 0, ncp % 128 == 0, lda % 4 == 0. */
 int amp_gemm_nt_f32(const void* a, int32_t lda, int32_t rows, int32_t ka, const void* wt, int32_t kap,
                     int32_t ncp, void* c, int32_t ldc, int32_t nc, void* stream);
 /* Real expansion of a complex operator X[o][j] = rowscale[o] * op(src[o*so + j*sj]) into Wt. */

