@@ -31,13 +31,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Per-workgroup partial results of one detector iteration.  The next kernel on
 // the stream reduces them (kernel boundary = visibility), so no atomics and a
 // fixed summation order: every workgroup that reduces them gets identical bits.
-struct alignas(16) Partial {
+struct alignas(16) Partial {   // 32 B: also the persistent engine's granule pair
     double sumvar;     // sum of var (float64), NaN-propagating
     double maxabs;     // max |xi| over the block (float32 logits; NaN if any input is non-finite)
     double minsecmax;  // min over sections of the section max logit
     uint32_t notclose; // elements failing torch.allclose(var_new, var_prev)
     uint32_t pad;
 };
+static_assert(sizeof(Partial) == 32, "Partial is one 32-byte granule pair");
+
 
 // Device-resident scalar state of one VAMP iteration (vamp.py:66-94).
 struct alignas(16) VampIter {
@@ -100,6 +102,66 @@ template <int O> __device__ __forceinline__ long long xl(long long v) {
 }
 template <int O> __device__ __forceinline__ double xl(double v) { return __longlong_as_double(xl<O>(__double_as_longlong(v))); }
 
+// Compile-time group size: straight-line VALU (DPP for distances 1-8, gfx950's
+// v_permlane16_swap / v_permlane32_swap for 16 and 32), no LDS round trip, no branches, so
+// independent reductions interleave.  op(v, v ^ O) is formed as op(even half, odd half) in
+// every lane, so all lanes of a group end with the same bits.
+template <int O>
+__device__ __forceinline__ void xl_pair(float v, float& lo, float& hi) {
+    if constexpr (O == 16 || O == 32) {
+        const unsigned u = __float_as_uint(v);
+        const auto r = (O == 16) ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                                 : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        lo = __uint_as_float(r[0]);   // the even 16/32-lane half's value, in every lane
+        hi = __uint_as_float(r[1]);   // the odd half's value
+    } else {
+        const float p = xl<O>(v);
+        const bool odd = (threadIdx.x & O) != 0;
+        lo = odd ? p : v;
+        hi = odd ? v : p;
+    }
+}
+template <int O, class Op>
+__device__ __forceinline__ float xl_op(float v, Op op) {
+    if constexpr (O == 16 || O == 32) {
+        float lo, hi;
+        xl_pair<O>(v, lo, hi);
+        return op(lo, hi);
+    } else {
+        return op(v, xl<O>(v));
+    }
+}
+template <int G, class Op>
+__device__ __forceinline__ float group_reduce_c(float v, Op op) {
+    if constexpr (G > 1) v = xl_op<1>(v, op);
+    if constexpr (G > 2) v = xl_op<2>(v, op);
+    if constexpr (G > 4) v = xl_op<4>(v, op);
+    if constexpr (G > 8) v = xl_op<8>(v, op);
+    if constexpr (G > 16) v = xl_op<16>(v, op);
+    if constexpr (G > 32) v = xl_op<32>(v, op);
+    return v;
+}
+template <int G>
+__device__ __forceinline__ float group_fmax_c(float v) { return group_reduce_c<G>(v, [](float a, float b) { return fmaxf(a, b); }); }
+// Sum over the group (same bits in every lane) and, per lane, the sum of every OTHER lane of
+// the group: a sum of non-negative terms when the inputs are, so Z - Z_m needs no subtraction.
+template <int O>
+__device__ __forceinline__ void sum_excl_step(float& tot, float& excl) {
+    float lo, hi;
+    xl_pair<O>(tot, lo, hi);
+    excl += (threadIdx.x & O) ? lo : hi;
+    tot = lo + hi;
+}
+template <int G>
+__device__ __forceinline__ void group_sum_excl_c(float& tot, float& excl) {
+    if constexpr (G > 1) sum_excl_step<1>(tot, excl);
+    if constexpr (G > 2) sum_excl_step<2>(tot, excl);
+    if constexpr (G > 4) sum_excl_step<4>(tot, excl);
+    if constexpr (G > 8) sum_excl_step<8>(tot, excl);
+    if constexpr (G > 16) sum_excl_step<16>(tot, excl);
+    if constexpr (G > 32) sum_excl_step<32>(tot, excl);
+}
+
 template <class T, class Op>
 __device__ __forceinline__ T group_reduce(T v, int G, Op op) {
     if (G > 1) v = op(v, xl<1>(v));
@@ -160,7 +222,7 @@ __device__ __forceinline__ void part_block_store(PartAcc p, Partial* dst, void* 
     if (threadIdx.x == 0) {
         Partial o;
         o.sumvar = s[0].sumvar; o.maxabs = s[0].maxabs; o.minsecmax = s[0].minsecmax; o.notclose = s[0].notclose;
-        for (int w = 1; w < AMP_WG / 64; ++w) {
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
             o.sumvar += s[w].sumvar; o.maxabs = nan_max(o.maxabs, s[w].maxabs);
             o.minsecmax = nan_min(o.minsecmax, s[w].minsecmax); o.notclose += s[w].notclose;
         }

@@ -35,8 +35,228 @@ namespace amp {
 //   void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const;
 //   void section(int sec, float secmax, float secabs) const;     // group lane 0
 // KK: the constellation size as a compile-time constant (1, 2, 4, 8 or 16).
+//
+// M <= 64 form (G = M lanes per section, compile-time): one position per lane, U sections
+// per lane group in flight (independent dependency chains for the scheduler).  Everything is
+// float32: Z and the exclusive sums Z - Z_m by group_sum_excl_c, 1 / Z by v_rcp_f32 (Z >= 1:
+// the section max term is exp(0)).  The constellation is held in VGPRs (uniform values, but
+// as SGPR operands they spill in the big fused kernels).  Section statistics (max logit,
+// max |logit|, non-finite input) are kept per lane in float32 and folded into the float64
+// PartAcc once at the end.
+template <bool kVar, int KK, int U, int G, class P>
+__device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    const int nw = blockDim.x >> 6;
+    float cre[KK], cim[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+        cre[k] = c.re[k]; cim[k] = c.im[k];
+        asm volatile("" : "+v"(cre[k]), "+v"(cim[k]));
+    }
+    float st_abs = 0.f, st_min = INFINITY;
+    bool st_bad = false;
+    for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {   // wave-uniform trip count
+        int sec[U];
+        bool act[U];
+        float xk[U][KK], smax[U], sabs[U];
+        float ur[U], ui[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            sec[u] = base + u * gpw + gid;
+            act[u] = sec[u] < nsec;
+            float rr, ri, it;
+            pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
+            ur[u] = rr * it; ui[u] = ri * it;   // c64 / f32 == multiply by the reciprocal
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (act[u]) st_bad |= !(fabsf(ur[u]) <= FLT_MAX && fabsf(ui[u]) <= FLT_MAX);
+            float lmax = -FLT_MAX, lmin = FLT_MAX;
+#pragma unroll
+            for (int k = 0; k < KK; ++k) {
+                xk[u][k] = fmaf(ur[u], cre[k], ui[u] * cim[k]);
+                lmax = fmaxf(lmax, xk[u][k]);
+                lmin = fminf(lmin, xk[u][k]);
+            }
+            smax[u] = lmax;
+            sabs[u] = fmaxf(lmax, -lmin);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { smax[u] = group_fmax_c<G>(smax[u]); sabs[u] = group_fmax_c<G>(sabs[u]); }
+        float zt[U], ze[U], sr[U], si[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float zm = 0.f, a = 0.f, b = 0.f;
+#pragma unroll
+            for (int k = 0; k < KK; ++k) {
+                const float e = __builtin_amdgcn_exp2f((xk[u][k] - smax[u]) * AMP_LOG2E);
+                xk[u][k] = e;
+                zm += e;
+                a = fmaf(cre[k], e, a);
+                b = fmaf(cim[k], e, b);
+            }
+            zt[u] = zm; ze[u] = 0.f; sr[u] = a; si[u] = b;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float iz = __builtin_amdgcn_rcpf(zt[u]);
+            const float xr = sr[u] * iz, xi = si[u] * iz;
+            float var = 0.f;
+            if (kVar) {
+                float vs = 0.f;
+#pragma unroll
+                for (int k = 0; k < KK; ++k) {
+                    const float dr = xr - cre[k], di = xi - cim[k];
+                    vs = fmaf(fmaf(dr, dr, di * di), xk[u][k], vs);
+                }
+                var = (xr * xr + xi * xi) * (ze[u] * iz) + vs * iz;
+            }
+            if (act[u]) {
+                pol.store(sec[u], g, xr, xi, var, pa);
+                st_abs = nan_max(st_abs, sabs[u]);
+                st_min = nan_min(st_min, smax[u]);
+                if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
+            }
+        }
+    }
+    pa.maxabs = st_bad ? __longlong_as_double(0x7ff8000000000000LL) : nan_max(pa.maxabs, (double)st_abs);
+    pa.minsecmax = nan_min(pa.minsecmax, (double)st_min);
+}
+
+// Packed-math form of denoise_sections_g (KK even): the per-symbol work runs on
+// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 over pairs — two symbols per instruction for
+// the logits and their shift, the (re, im) pair for the sums and the variance — so one
+// position costs ~140 VALU instructions instead of ~300.  Same rounding per element as the
+// scalar form (each packed lane is the same IEEE operation).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <bool kVar, int KK, int U, int G, class P>
+__device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    static_assert(KK % 2 == 0, "packed form needs an even constellation size");
+    constexpr int KH = KK / 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    const int nw = blockDim.x >> 6;
+    f32x2 pre[KH], pim[KH], sym[KK];   // (re_k, re_k+1), (im_k, im_k+1); (re_k, im_k)
+#pragma unroll
+    for (int h = 0; h < KH; ++h) {
+        pre[h] = f32x2{c.re[2 * h], c.re[2 * h + 1]};
+        pim[h] = f32x2{c.im[2 * h], c.im[2 * h + 1]};
+        asm volatile("" : "+v"(pre[h]), "+v"(pim[h]));
+    }
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+        sym[k] = f32x2{c.re[k], c.im[k]};
+        asm volatile("" : "+v"(sym[k]));
+    }
+    float st_abs = 0.f, st_min = INFINITY;
+    bool st_bad = false;
+    for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {   // wave-uniform trip count
+        int sec[U];
+        bool act[U];
+        f32x2 xk[U][KH];
+        float smax[U], sabs[U], ur[U], ui[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            sec[u] = base + u * gpw + gid;
+            act[u] = sec[u] < nsec;
+            float rr, ri, it;
+            pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
+            ur[u] = rr * it; ui[u] = ri * it;   // c64 / f32 == multiply by the reciprocal
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (act[u]) st_bad |= !(fabsf(ur[u]) <= FLT_MAX && fabsf(ui[u]) <= FLT_MAX);
+            const f32x2 u2 = f32x2{ur[u], ur[u]}, v2 = f32x2{ui[u], ui[u]};
+            float lmax = -FLT_MAX, lmin = FLT_MAX;
+#pragma unroll
+            for (int h = 0; h < KH; ++h) {
+                xk[u][h] = __builtin_elementwise_fma(u2, pre[h], v2 * pim[h]);
+                lmax = fmaxf(lmax, fmaxf(xk[u][h].x, xk[u][h].y));
+                lmin = fminf(lmin, fminf(xk[u][h].x, xk[u][h].y));
+            }
+            smax[u] = lmax;
+            sabs[u] = fmaxf(lmax, -lmin);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { smax[u] = group_fmax_c<G>(smax[u]); sabs[u] = group_fmax_c<G>(sabs[u]); }
+        float zt[U], ze[U];
+        f32x2 s2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const f32x2 m2 = f32x2{smax[u], smax[u]};
+            const f32x2 l2 = f32x2{AMP_LOG2E, AMP_LOG2E};
+            f32x2 z2 = f32x2{0.f, 0.f}, a2 = f32x2{0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < KH; ++h) {
+                const f32x2 d = (xk[u][h] - m2) * l2;
+                const f32x2 e = f32x2{__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+                xk[u][h] = e;
+                z2 += e;
+                a2 = __builtin_elementwise_fma(sym[2 * h], f32x2{e.x, e.x}, a2);
+                a2 = __builtin_elementwise_fma(sym[2 * h + 1], f32x2{e.y, e.y}, a2);
+            }
+            zt[u] = z2.x + z2.y; ze[u] = 0.f; s2[u] = a2;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float iz = __builtin_amdgcn_rcpf(zt[u]);
+            const f32x2 x2 = s2[u] * f32x2{iz, iz};
+            float var = 0.f;
+            if (kVar) {
+                f32x2 v2 = f32x2{0.f, 0.f};
+#pragma unroll
+                for (int h = 0; h < KH; ++h) {
+                    const f32x2 d0 = x2 - sym[2 * h], d1 = x2 - sym[2 * h + 1];
+                    v2 = __builtin_elementwise_fma(d0 * d0, f32x2{xk[u][h].x, xk[u][h].x}, v2);
+                    v2 = __builtin_elementwise_fma(d1 * d1, f32x2{xk[u][h].y, xk[u][h].y}, v2);
+                }
+                var = (x2.x * x2.x + x2.y * x2.y) * (ze[u] * iz) + (v2.x + v2.y) * iz;
+            }
+            if (act[u]) {
+                pol.store(sec[u], g, x2.x, x2.y, var, pa);
+                st_abs = nan_max(st_abs, sabs[u]);
+                st_min = nan_min(st_min, smax[u]);
+                if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
+            }
+        }
+    }
+    pa.maxabs = st_bad ? __longlong_as_double(0x7ff8000000000000LL) : nan_max(pa.maxabs, (double)st_abs);
+    pa.minsecmax = nan_min(pa.minsecmax, (double)st_min);
+}
+
+// Runtime M (a power of two <= 64) -> the compile-time group size; PK selects the packed form.
+template <bool kVar, int KK, int U, int G, bool PK, class P>
+__device__ __forceinline__ void denoise_sections_sel(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    if constexpr (PK && KK % 2 == 0) denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa);
+    else denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa);
+}
+template <bool kVar, int KK, int U, bool PK = true, class P>
+__device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+    switch (M) {
+    case 64: denoise_sections_sel<kVar, KK, U, 64, PK>(pol, nsec, c, pa); break;
+    case 32: denoise_sections_sel<kVar, KK, U, 32, PK>(pol, nsec, c, pa); break;
+    case 16: denoise_sections_sel<kVar, KK, U, 16, PK>(pol, nsec, c, pa); break;
+    case 8: denoise_sections_sel<kVar, KK, U, 8, PK>(pol, nsec, c, pa); break;
+    case 4: denoise_sections_sel<kVar, KK, U, 4, PK>(pol, nsec, c, pa); break;
+    case 2: denoise_sections_sel<kVar, KK, U, 2, PK>(pol, nsec, c, pa); break;
+    default: denoise_sections_sel<kVar, KK, U, 1, PK>(pol, nsec, c, pa); break;
+    }
+}
+
 template <bool kVar, int KK, class P>
 __device__ __forceinline__ void denoise_sections(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+    if (M <= 64) {
+        denoise_sections_u<kVar, KK, 1>(pol, nsec, M, c, pa);
+        return;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int G = M < 64 ? M : 64;
     const int PPL = M / G;
@@ -49,57 +269,7 @@ __device__ __forceinline__ void denoise_sections(const P& pol, int nsec, int M, 
         const int ss = act ? sec : nsec - 1;
         float lmax = -FLT_MAX, lmin = FLT_MAX;
         bool bad = false;
-        if (PPL == 1) {
-            float rr, ri, it;
-            pol.load(ss, g, rr, ri, it);
-            const float ur = rr * it, ui = ri * it;   // c64 / f32 == multiply by the reciprocal
-            bad = !(fabsf(ur) <= FLT_MAX && fabsf(ui) <= FLT_MAX);
-            float xk[KK];
-#pragma unroll
-            for (int k = 0; k < KK; ++k) {
-                {
-                    xk[k] = fmaf(ur, c.re[k], ui * c.im[k]);
-                    lmax = fmaxf(lmax, xk[k]);
-                    lmin = fminf(lmin, xk[k]);
-                }
-            }
-            const float smax = group_fmax(lmax, G);
-            float zm = 0.f, sr = 0.f, si = 0.f;
-#pragma unroll
-            for (int k = 0; k < KK; ++k) {
-                {
-                    const float e = __builtin_amdgcn_exp2f((xk[k] - smax) * AMP_LOG2E);
-                    xk[k] = e;
-                    zm += e;
-                    sr = fmaf(c.re[k], e, sr);
-                    si = fmaf(c.im[k], e, si);
-                }
-            }
-            const double z = group_sum((double)zm, G);
-            const double iz = 1.0 / z;
-            const float xr = (float)((double)sr * iz), xi = (float)((double)si * iz);
-            float var = 0.f;
-            if (kVar) {
-                const float omp = (float)((z - (double)zm) * iz);
-                float vs = 0.f;
-#pragma unroll
-                for (int k = 0; k < KK; ++k) {
-                    {
-                        const float dr = xr - c.re[k], di = xi - c.im[k];
-                        vs = fmaf(fmaf(dr, dr, di * di), xk[k], vs);
-                    }
-                }
-                var = (xr * xr + xi * xi) * omp + (float)((double)vs * iz);
-            }
-            if (act) pol.store(sec, g, xr, xi, var, pa);
-            const float sabs = group_fmax(fmaxf(lmax, -lmin), G);
-            if (act) {
-                const double sm = (double)smax, sa = (double)sabs;
-                pa.maxabs = bad ? __longlong_as_double(0x7ff8000000000000LL) : nan_max(pa.maxabs, sa);
-                pa.minsecmax = nan_min(pa.minsecmax, sm);
-                if (g == 0) pol.section(sec, (float)sm, (float)sa);
-            }
-        } else {
+        {
             // M > 64: PPL positions per lane, logits recomputed per pass.
             for (int p = 0; p < PPL; ++p) {
                 float rr, ri, it;

@@ -36,7 +36,7 @@ struct VampK {
     int nwg;            // ceil(B / PBM) workgroups
     const float* Wq1;   // Vh   16x16x4-packed [2k][2N]
     const float* Wq2;   // V    16x16x4-packed [2N][2k]
-    Partial* pparts;    // [max_iter][nwg]
+    Partial* pparts;    // [max_iter][nwg] 32-B granule pairs (amp_vamp_persist.hip), right after pbar
     double* pxch;       // [max_iter][nwg][4] rare-path exchange
     unsigned* pbar;     // [0] arrivals, [1] abort flag (zeroed before every launch)
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
@@ -83,9 +83,9 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     const int nwg = cdiv(d->B, 16);
     w.Wq1 = cv.take<float>((size_t)2 * k * 2 * d->N);
     w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * k);
-    w.pparts = cv.take<Partial>((size_t)max_iter * nwg);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
-    w.pbar = cv.take<unsigned>(64);
+    w.pbar = cv.take<unsigned>(64);                          // 256 B: pbar and the granules that
+    w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // follow it are zeroed by one memset
     w.bytes = cv.off;
     return w;
 }
@@ -166,6 +166,35 @@ __device__ inline amp_status vamp_make_status(const VampK& P, const VampIter& cu
 }
 
 // ---- persistent engine (amp_vamp_persist.hip) ----
+// Denoiser policy over the LDS-resident rows of one persistent workgroup (vamp.py:84, 185).
+struct PDenoisePolicy {
+    const float* r;
+    float* x;
+    float* vnew;
+    const float* vprev;
+    float* sm;
+    float* sa;
+    int ldr, M, lspr, N;   // sections per row = 1 << lspr (N, M powers of two)
+    float inv;
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
+        const int row = sec >> lspr, sj = sec & ((1 << lspr) - 1);
+        const float2 v = *reinterpret_cast<const float2*>(r + row * ldr + 2 * (sj * M + m));
+        rr = v.x; ri = v.y; it = inv;
+    }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
+        const int row = sec >> lspr, sj = sec & ((1 << lspr) - 1);
+        *reinterpret_cast<float2*>(x + row * ldr + 2 * (sj * M + m)) = make_float2(xr, xi);
+        const int vo = row * N + sj * M + m;
+        vnew[vo] = var;
+        pa.sumvar += (double)var;
+        pa.notclose += torch_close(var, vprev[vo]) ? 0u : 1u;     // vamp.py:185
+    }
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
+        sm[sec] = smax;
+        sa[sec] = sabs;
+    }
+};
+
 constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);

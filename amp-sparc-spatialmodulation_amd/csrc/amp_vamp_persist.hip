@@ -21,6 +21,8 @@
 // Co-residency: ceil(B/16) <= #CUs workgroups, one per CU by its LDS footprint, launched with
 // hipLaunchCooperativeKernel (which rejects a grid that cannot be resident); every barrier
 // spin is bounded (2 s) and raises an abort word that releases every other workgroup.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <mutex>
 
@@ -28,7 +30,6 @@
 
 namespace amp {
 
-constexpr int PWG = 256;
 constexpr int PRING = 4;   // W groups in flight per wave
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -127,36 +128,102 @@ __device__ bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
     return *s_flag != 0;
 }
 
-struct PDenoisePolicy {
-    const float* r;
-    float* x;
-    float* vnew;
-    const float* vprev;
-    float* sm;
-    float* sa;
-    int ldr, M, spr, N;
-    float inv;
-    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const {
-        const int row = sec / spr, sj = sec - row * spr;
-        const float2 v = *reinterpret_cast<const float2*>(r + row * ldr + 2 * (sj * M + m));
-        rr = v.x; ri = v.y; it = inv;
-    }
-    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
-        const int row = sec / spr, sj = sec - row * spr;
-        *reinterpret_cast<float2*>(x + row * ldr + 2 * (sj * M + m)) = make_float2(xr, xi);
-        const int vo = row * N + sj * M + m;
-        vnew[vo] = var;
-        pa.sumvar += (double)var;
-        pa.notclose += torch_close(var, vprev[vo]) ? 0u : 1u;     // vamp.py:185
-    }
-    __device__ __forceinline__ void section(int sec, float smax, float sabs) const {
-        sm[sec] = smax;
-        sa[sec] = sabs;
-    }
-};
+// ---- per-iteration partials: data-tagged granules (no fences, no counter) ----
+// Each workgroup publishes its block partial as two 16-byte granules, each ONE write-through
+// (`sc1`) buffer store carrying the tag t + 1 in its last word:
+//   g0 = {sumvar lo, sumvar hi, notclose, tag},  g1 = {maxabs (f32 bits), minsecmax (f32 bits), 0, tag}
+// (maxabs / minsecmax are float32 values or NaN / inf: exact in f32).  Every workgroup then
+// sweeps all nwg granule pairs with `sc1` loads (L2/fabric-served, never a stale L1 line)
+// until every tag matches, and reduces them in one fixed order, so every workgroup derives
+// bit-identical batch scalars.  The granule block is zeroed before every launch (tag 0 never
+// matches).  MI355X_MICROARCH.md § visibility (R2 granules, allgather).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <int NT, int KK>
-__global__ __launch_bounds__(PWG, 1) void vamp_persist(VampK P, Const64 c64) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void part_publish(PartAcc p, __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned tag,
+                                             void* lds_scratch) {
+    part_wave_reduce(p);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    __syncthreads();
+    if (lane == 0) {
+        s[wave].sumvar = p.sumvar; s[wave].maxabs = p.maxabs;
+        s[wave].minsecmax = p.minsecmax; s[wave].notclose = p.notclose;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sv = s[0].sumvar, mx = s[0].maxabs, mn = s[0].minsecmax;
+        uint32_t nc = s[0].notclose;
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
+            sv += s[w].sumvar; mx = nan_max(mx, s[w].maxabs); mn = nan_min(mn, s[w].minsecmax); nc += s[w].notclose;
+        }
+        const unsigned long long b = (unsigned long long)__double_as_longlong(sv);
+        const u32x4 g0 = {(unsigned)b, (unsigned)(b >> 32), nc, tag};
+        const u32x4 g1 = {__float_as_uint((float)mx), __float_as_uint((float)mn), 0u, tag};
+        __builtin_amdgcn_raw_buffer_store_b128(g0, rs, (int)off, 0, 16);        // aux 16 = sc1
+        __builtin_amdgcn_raw_buffer_store_b128(g1, rs, (int)off + 16, 0, 16);
+    }
+}
+
+// Wave 0 sweeps the nwg (<= 256) granule pairs of one iteration; the result lands in every
+// thread.  A bounded spin (2 s) raises the abort word, as grid_sync does.
+__device__ __forceinline__ bool part_gather(__amdgpu_buffer_rsrc_t rs, unsigned off0, int nwg, unsigned tag,
+                                            unsigned* abort_word, PartAcc& out, void* lds_scratch, int* s_flag) {
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    if ((threadIdx.x >> 6) == 0) {
+        const int lane = threadIdx.x & 63;
+        u32x4 a[4], b[4];
+        int ok_all = 1;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int w = lane + 64 * q;
+                if (w < nwg) {
+                    a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off0 + 32u * w), 0, 16);
+                    b[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off0 + 32u * w + 16), 0, 16);
+                    ok &= (a[q].w == tag) & (b[q].w == tag);
+                }
+            }
+            if (__all(ok)) break;
+            if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                __builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
+                __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok_all = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        PartAcc p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (lane + 64 * q < nwg) {
+                p.sumvar += __longlong_as_double((long long)(((unsigned long long)a[q].y << 32) | a[q].x));
+                p.maxabs = nan_max(p.maxabs, (double)__uint_as_float(b[q].x));
+                p.minsecmax = nan_min(p.minsecmax, (double)__uint_as_float(b[q].y));
+                p.notclose += a[q].z;
+            }
+        }
+        part_wave_reduce(p);
+        if (lane == 0) {
+            s[0].sumvar = p.sumvar; s[0].maxabs = p.maxabs; s[0].minsecmax = p.minsecmax; s[0].notclose = p.notclose;
+            *s_flag = ok_all;
+        }
+    }
+    __syncthreads();
+    out.sumvar = s[0].sumvar; out.maxabs = s[0].maxabs; out.minsecmax = s[0].minsecmax; out.notclose = s[0].notclose;
+    const bool ok = *s_flag != 0;
+    __syncthreads();
+    return ok;
+}
+
+template <int NT, int KK, int NWV>
+__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64) {
+    constexpr int PWG = 64 * NWV;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
     __shared__ double s_d[PWG / 64][4];
@@ -206,6 +273,7 @@ __global__ __launch_bounds__(PWG, 1) void vamp_persist(VampK P, Const64 c64) {
         trc[(size_t)nwg * P.max_iter * 8 + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
     }
     unsigned nbar = 0;
+    const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
     int fixed = 0, last_t = 0, aborted = 0;
     VampIter nx = cur;
 
@@ -258,15 +326,18 @@ __global__ __launch_bounds__(PWG, 1) void vamp_persist(VampK P, Const64 c64) {
         __syncthreads();
         stamp(t, 4);
         // 4. denoiser (vamp.py:84)
-        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, spr, N, cur.inv_sigma2};
+        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         PartAcc pa;
-        denoise_sections<true, KK>(pol, nrows * spr, M, P.c, pa);
-        part_block_store(pa, P.pparts + (size_t)t * nwg + wg, scr);
+        denoise_sections_u<true, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
+        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, (unsigned)t + 1u, scr);
         stamp(t, 5);
-        // 5. batch scalars
-        if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+        // 5. batch scalars: every workgroup gathers and reduces every partial
+        PartAcc g;
+        if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, (unsigned)t + 1u, P.pbar + 1, g, scr, &s_flag)) {
+            aborted = 1;
+            break;
+        }
         stamp(t, 6);
-        PartAcc g = part_reduce_all(P.pparts + (size_t)t * nwg, nwg, scr);
         fixed = 0;
         if (part_allnan(g)) {
             // the reference's G is NaN / inf: every section of this iteration is NaN
@@ -385,9 +456,20 @@ bool vamp_persist_eligible(const amp_dims* d, int k, int ncu) {
     return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
 }
 
-template <int NT, int KK>
+// Waves per workgroup (one workgroup per CU): 4 = one wave per SIMD, 8 = two (the second
+// wave hides LDS / cross-lane latency in the denoiser and keeps more weight loads in flight).
+static int persist_waves() {
+    static int w = [] {
+        const char* e = getenv("AMP_PERSIST_WAVES");
+        const int v = e ? atoi(e) : 4;
+        return (v == 8) ? 8 : 4;
+    }();
+    return w;
+}
+
+template <int NT, int KK, int NWV>
 static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) {
@@ -397,41 +479,52 @@ static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) 
     VampK Pc = P;
     Const64 cc = c64;
     void* args[] = {(void*)&Pc, (void*)&cc};
-    e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(PWG), args, (unsigned)lds, st);
+    e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
     if (e != hipSuccess) {
-        set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, PWG, lds,
+        set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
                   hipGetErrorString(e));
         return AMP_E_LAUNCH;
     }
     return AMP_OK;
 }
 
-template <int NT>
+template <int NT, int NWV>
 static int persist_launch_nt(const VampK& P, const Const64& c64, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1>(P, c64, st);
-    case 2: return persist_launch_t<NT, 2>(P, c64, st);
-    case 4: return persist_launch_t<NT, 4>(P, c64, st);
-    case 8: return persist_launch_t<NT, 8>(P, c64, st);
-    default: return persist_launch_t<NT, 16>(P, c64, st);
+    case 1: return persist_launch_t<NT, 1, NWV>(P, c64, st);
+    case 2: return persist_launch_t<NT, 2, NWV>(P, c64, st);
+    case 4: return persist_launch_t<NT, 4, NWV>(P, c64, st);
+    case 8: return persist_launch_t<NT, 8, NWV>(P, c64, st);
+    default: return persist_launch_t<NT, 16, NWV>(P, c64, st);
     }
 }
 
 int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu) {
     (void)ncu;
-    hipError_t e = hipMemsetAsync(P.pbar, 0, 64 * sizeof(unsigned), st);
+    // barrier words + granule block: one contiguous, 256-B aligned, zeroed block (amp_vamp.h carve)
+    hipError_t e = hipMemsetAsync(P.pbar, 0, 64 * sizeof(unsigned) + (size_t)P.max_iter * P.nwg * sizeof(Partial), st);
     if (e != hipSuccess) {
         set_error("vamp_persist: hipMemsetAsync: %s", hipGetErrorString(e));
         return AMP_E_LAUNCH;
     }
-    switch (P.N / 32) {   // NT = 2N / 64 column tiles of 16 per wave
-    case 2: return persist_launch_nt<2>(P, c64, st);
-    case 4: return persist_launch_nt<4>(P, c64, st);
-    case 8: return persist_launch_nt<8>(P, c64, st);
-    default:
-        set_error("vamp_persist: N = %d not supported", P.N);
-        return AMP_E_ARG;
+    // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
+    if (persist_waves() == 4) {
+        switch (P.N) {
+        case 64: return persist_launch_nt<2, 4>(P, c64, st);
+        case 128: return persist_launch_nt<4, 4>(P, c64, st);
+        case 256: return persist_launch_nt<8, 4>(P, c64, st);
+        default: break;
+        }
+    } else {
+        switch (P.N) {
+        case 64: return persist_launch_nt<1, 8>(P, c64, st);
+        case 128: return persist_launch_nt<2, 8>(P, c64, st);
+        case 256: return persist_launch_nt<4, 8>(P, c64, st);
+        default: break;
+        }
     }
+    set_error("vamp_persist: N = %d not supported", P.N);
+    return AMP_E_ARG;
 }
 
 }  // namespace amp

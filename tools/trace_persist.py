@@ -16,7 +16,7 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch        # noqa: E402
 
-PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser + partial', 'grid barrier', 'reduce + scalars']
+PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser + partial', 'partial gather', 'scalars']
 
 
 def main():
