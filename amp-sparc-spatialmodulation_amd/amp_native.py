@@ -126,6 +126,21 @@ def lib():
     return _lib
 
 
+def unload():
+    """Synchronise and dlclose the library while the HIP runtime (and any attached profiler) is
+    still up: its code objects are then unregistered before interpreter teardown instead of
+    from the loader's exit-time destructors, which ran after rocprofv3 had finalised and
+    crashed it (observed on the box, r01)."""
+    global _lib
+    if _lib is None:
+        return
+    torch.cuda.synchronize()
+    WORKSPACE.clear()
+    import _ctypes
+    _ctypes.dlclose(_lib._handle)
+    _lib = None
+
+
 def check(rc: int, what: str):
     if rc != 0:
         raise AmpError(f'{what} failed ({rc}): {lib().amp_last_error().decode()}')
@@ -176,6 +191,9 @@ class Workspace:
             b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             self._bufs[k] = b
         return b
+
+    def clear(self):
+        self._bufs.clear()
 
 
 WORKSPACE = Workspace()

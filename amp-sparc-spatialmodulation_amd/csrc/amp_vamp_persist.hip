@@ -18,9 +18,10 @@
 // wpack16_index): a wave owns 16*NT output columns, NT independent accumulators.
 // y~ = (s Uh) y comes from the launch engine's GEMM once per forward (amp_vamp.hip).
 //
-// Co-residency: ceil(B/16) <= #CUs workgroups, one per CU by its LDS footprint, launched with
-// hipLaunchCooperativeKernel (which rejects a grid that cannot be resident); every barrier
-// spin is bounded (2 s) and raises an abort word that releases every other workgroup.
+// Co-residency: ceil(B/16) <= #CUs workgroups, one per CU by its LDS footprint; the launch
+// checks occupancy x CUs >= grid first (or uses hipLaunchCooperativeKernel, which makes the
+// same check); every barrier spin is bounded (2 s) and raises an abort word that releases
+// every other workgroup.
 #include <stdlib.h>
 
 #include <algorithm>
@@ -63,42 +64,54 @@ __host__ __device__ inline PLayout playout(int N, int k, int L) {
     return y;
 }
 
-// C[16 x 16*NT] (this wave's columns ct0*16 ...) += A[16 x kap] (LDS, row stride lda) . Wq^T,
+// C[16 x 16*NT] (this wave's columns ct0*16 ...) += A[16 x 16*G] (LDS, row stride lda) . Wq^T,
 // Wq packed by wpack16_index.  Accumulator t, register r: row 4*(lane>>4) + r, column
-// 16*(ct0 + t) + (lane & 15).
-template <int NT>
-__device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __restrict__ wq, int kap, int ct0,
+// 16*(ct0 + t) + (lane & 15).  Fully unrolled over the G reduction groups so every wait on the
+// weight ring is a counted `s_waitcnt vmcnt(n)` (a rolled loop drained it to vmcnt(0) at the
+// back edge: ~25 % of the GEMM time at cfg4, r01 trace); the A row of group g+1 is read from
+// LDS one group ahead.
+template <int NT, int G>
+__device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __restrict__ wq, int ct0,
                                        f32x4 (&acc)[NT]) {
+    constexpr int R = G < PRING ? G : PRING;
     const int lane = threadIdx.x & 63;
-    const int G = kap >> 4;
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float4* wcol = reinterpret_cast<const float4*>(wq) + (size_t)ct0 * G * 64 + lane;
-    float4 ring[PRING][NT];
+    // one buffer resource per wave (base = this wave's first column tile); every load is
+    // lane * 16 + a compile-time byte offset (SGPR), so the unrolled ring holds no addresses
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);   // wave-uniform: SGPR resource, no waterfall
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(wq) + (size_t)ct0u * G * 256, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = lane * 16;
+    auto wload = [&](int t, int g) {
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, (t * G + g) * 1024, 0);
+        return make_float4(v.x, v.y, v.z, v.w);
+    };
+    float4 ring[R][NT];
 #pragma unroll
-    for (int d = 0; d < PRING; ++d)
+    for (int d = 0; d < R; ++d)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) ring[d][t] = wcol[((size_t)t * G + d) * 64];
+        for (int t = 0; t < NT; ++t) ring[d][t] = wload(t, d);
     const float* a_s = sA + (lane & 15) * lda + 4 * (lane >> 4);
     float4 acur = *reinterpret_cast<const float4*>(a_s);
-    for (int gb = 0; gb < G; gb += PRING) {
 #pragma unroll
-        for (int d = 0; d < PRING; ++d) {
-            const int g = gb + d;
-            const float4 anext = *reinterpret_cast<const float4*>(a_s + 16 * min(g + 1, G - 1));
+    for (int g = 0; g < G; ++g) {
+        const int d = g % R;
+        const float4 anext = *reinterpret_cast<const float4*>(a_s + 16 * (g + 1 < G ? g + 1 : g));
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                acc[t] = mfma16x16x4(acur.x, ring[d][t].x, acc[t]);
-                acc[t] = mfma16x16x4(acur.y, ring[d][t].y, acc[t]);
-                acc[t] = mfma16x16x4(acur.z, ring[d][t].z, acc[t]);
-                acc[t] = mfma16x16x4(acur.w, ring[d][t].w, acc[t]);
-            }
-            const int gn = min(g + PRING, G - 1);
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.x, ring[d][t].x, acc[t]);
 #pragma unroll
-            for (int t = 0; t < NT; ++t) ring[d][t] = wcol[((size_t)t * G + gn) * 64];
-            acur = anext;
-            __builtin_amdgcn_sched_barrier(0);
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.y, ring[d][t].y, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.z, ring[d][t].z, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.w, ring[d][t].w, acc[t]);
+        if (g + R < G) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) ring[d][t] = wload(t, g + R);
         }
+        acur = anext;
+        __builtin_amdgcn_sched_barrier(0);   // keep the ring depth: no hoisting of later groups' loads
     }
 }
 
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         stamp(t, 1);
         // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
         f32x4 acc[NT];
-        gemm16<NT>(sA, lda, P.Wq1, twoN, ct0, acc);
+        gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
         __syncthreads();
         stamp(t, 2);
 #pragma unroll
@@ -311,7 +324,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         __syncthreads();
         stamp(t, 3);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
-        gemm16<NT>(sA, lda, P.Wq2, twok, ct0, acc);
+        gemm16<NT, NT * NWV>(sA, lda, P.Wq2, ct0, acc);
 #pragma unroll
         for (int t2 = 0; t2 < NT; ++t2) {
             const int col = 16 * (ct0 + t2) + (lane & 15);
@@ -467,6 +480,17 @@ static int persist_waves() {
     return w;
 }
 
+// Launch path: a plain launch after an explicit co-residency check (default), or
+// hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).  The cooperative path made processes
+// crash in exit-time teardown under rocprofv3 on the box (r01), the plain one does not.
+static bool persist_coop() {
+    static bool c = [] {
+        const char* e = getenv("AMP_PERSIST_LAUNCH");
+        return e && e[0] == 'c';
+    }();
+    return c;
+}
+
 template <int NT, int KK, int NWV>
 static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) {
     const void* fn = (const void*)vamp_persist<NT, KK, NWV>;
@@ -476,13 +500,31 @@ static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) 
         set_error("vamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
         return AMP_E_LAUNCH;
     }
-    VampK Pc = P;
-    Const64 cc = c64;
-    void* args[] = {(void*)&Pc, (void*)&cc};
-    e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
+    if (persist_coop()) {
+        VampK Pc = P;
+        Const64 cc = c64;
+        void* args[] = {(void*)&Pc, (void*)&cc};
+        e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
+        if (e != hipSuccess) {
+            set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
+                      hipGetErrorString(e));
+            return AMP_E_LAUNCH;
+        }
+        return AMP_OK;
+    }
+    // plain launch: co-residency checked here (resident workgroups per CU x CUs >= grid), the
+    // check hipLaunchCooperativeKernel would make; the bounded barrier spins stay as the backstop
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * NWV, lds);
+    if (e != hipSuccess || per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
+        set_error("vamp_persist: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", P.nwg, per_cu,
+                  device_cu_count());
+        return AMP_E_LAUNCH;
+    }
+    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, c64);
+    e = hipGetLastError();
     if (e != hipSuccess) {
-        set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
-                  hipGetErrorString(e));
+        set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
         return AMP_E_LAUNCH;
     }
     return AMP_OK;

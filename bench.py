@@ -176,6 +176,7 @@ def main():
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
+        nat.unload()
         return
     ms_step = el / args.steps * 1e3
     value = world * B / (el / args.steps)
@@ -198,6 +199,7 @@ def main():
     print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()
+    nat.unload()
 
 
 if __name__ == '__main__':
