@@ -120,8 +120,15 @@ class Config:
         return d
 
     def constellation(self):
+        """The amp_constellation struct of the current alphabet (memoised on its contents, so
+        an alphabet injected after construction is picked up)."""
         from amp_native import make_constellation
-        return make_constellation(self.symbols, self.gray, self.symbol_bits)
+        key = (np.asarray(self.symbols).tobytes(), tuple(self.gray), self.symbol_bits)
+        memo = getattr(self, '_const_memo', None)
+        if memo is None or memo[0] != key:
+            memo = (key, make_constellation(self.symbols, self.gray, self.symbol_bits))
+            self._const_memo = memo
+        return memo[1]
 
     def snr(self, EbN0dB: float) -> float:
         """Linear SNR of an EbN0 point as the drivers compute it (vamp_model.py:50-54)."""

@@ -82,6 +82,20 @@ inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256;
 enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2 };
 int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J,
                   float* wt, int kap, int ncp, hipStream_t st, int packed = WPACK32);
+// One job of build_cweights: the expanded weight of X[o][j] = rowscale_o *
+// (conj ? conj : id)(src[o * so + j * sj]), o < O, j < J, [ncp][kap] in layout `packed`.
+struct CWeightJob {
+    const float2* src;
+    long so, sj;
+    int conj;
+    const float* rowscale;
+    int O, J;
+    float* wt;
+    int kap, ncp;
+    int packed;
+};
+// Up to 4 jobs in ONE launch; the same launch zeroes `nzero` words at `zero` (or none).
+int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st);
 template <int BN>

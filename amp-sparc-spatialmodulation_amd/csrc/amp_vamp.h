@@ -38,7 +38,11 @@ struct VampK {
     const float* Wq2;   // V    16x16x4-packed [2N][2k]
     Partial* pparts;    // [max_iter][nwg] 32-B granule pairs (amp_vamp_persist.hip), right after pbar
     double* pxch;       // [max_iter][nwg][4] rare-path exchange
-    unsigned* pbar;     // [0] arrivals, [1] abort flag (zeroed before every launch)
+    unsigned* pbar;     // [0] arrivals, [1] abort flag (zeroed by the prepare launch)
+    unsigned gen;       // launch generation: granule tags are gen * (max_iter + 1) + t + 1
+    int ytil_in_kernel; // y~ = (s Uh) y computed by the persistent kernel itself (n == 2N)
+    const float* Wq0;   // s Uh 16x16x4-packed [2k][2n] (ytil_in_kernel)
+    const float* y;     // [B][2n] received signal (ytil_in_kernel)
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
     Const c;
 };
@@ -48,7 +52,7 @@ struct VampWs {
     float *secmax, *secabs;
     Partial* parts;
     VampIter* iters;
-    float *Wq1, *Wq2;
+    float *Wq0, *Wq1, *Wq2;
     Partial* pparts;
     double* pxch;
     unsigned* pbar;
@@ -81,6 +85,7 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
     w.iters = cv.take<VampIter>((size_t)max_iter + 1);
     const int nwg = cdiv(d->B, 16);
+    w.Wq0 = cv.take<float>((size_t)2 * k * 2 * d->n);
     w.Wq1 = cv.take<float>((size_t)2 * k * 2 * d->N);
     w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * k);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
@@ -99,7 +104,7 @@ __device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1
 __device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
     const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
     double ss = 0.0;
-    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s2[i] + vr));  // vamp.py:68
+    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s[i] * P.s[i] + vr));  // vamp.py:17, 68
     ss = group_sum(ss, 64);
     double* sl = reinterpret_cast<double*>(lds);
     __syncthreads();
@@ -126,6 +131,19 @@ __device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t
     it.sigma2 = sigma2;
     it.inv_sigma2 = 1.0f / sigma2;
     it.s2t = s2t32;
+}
+
+// The record that drives iteration 0 (vamp.py:22-26, 66-82 with the Tracker's Python-float
+// sigma2_tilde).  Called uniformly by every thread of one workgroup.
+__device__ inline VampIter vamp_first_iter(const VampK& P, float* lds) {
+    VampIter it;
+    it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0; it.G = 0.0;
+    it.pad1[0] = it.pad1[1] = it.pad1[2] = 0.f;
+    it.dxdr_prev = 0.f;   // r~ = (xmmse - 0 * r) * 1 = sparsity at t = 0 (vamp.py:25)
+    it.ns_prev = 1.f;
+    const double p = P.sparsity;
+    vamp_lmmse_scalars(P, true, p * p * (1 - p) + (1 - p) * (1 - p) * p, 0.f, lds, it);   // vamp.py:26
+    return it;
 }
 
 // The record that drives iteration t+1, from the reduced partials of iteration t: the stop
@@ -198,6 +216,7 @@ struct PDenoisePolicy {
 constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);
+bool vamp_persist_ytil_in_kernel(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu);
 int device_cu_count();
 

@@ -16,6 +16,7 @@
 //               scalars of iteration t+1 (vamp.py:85-94, 66-82) or the stop record
 //               (vamp.py:185-186).  Later iterations of a stopped loop are no-ops.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -25,13 +26,7 @@ namespace amp {
 
 __global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
     __shared__ __attribute__((aligned(16))) float lds[64];
-    VampIter it;
-    it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0; it.G = 0.0;
-    it.pad1[0] = it.pad1[1] = it.pad1[2] = 0.f;
-    it.dxdr_prev = 0.f;   // r~ = (xmmse - 0 * r) * 1 = sparsity at t = 0 (vamp.py:25)
-    it.ns_prev = 1.f;
-    const double p = P.sparsity;
-    vamp_lmmse_scalars(P, true, p * p * (1 - p) + (1 - p) * (1 - p) * p, 0.f, lds, it);   // vamp.py:26
+    const VampIter it = vamp_first_iter(P, lds);
     if (threadIdx.x == 0) P.iters[0] = it;
 }
 
@@ -256,7 +251,10 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.nwg = cdiv(d->B, PBM);
-    P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
+    P.Wq0 = w.Wq0; P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
+    P.gen = 0;
+    P.ytil_in_kernel = 0;
+    P.y = (const float*)a->y;
     P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
@@ -306,34 +304,58 @@ static void launch_k2(const VampK& P, int t, hipStream_t st) {
 }
 
 
-static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t st, bool persistent = false) {
+static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t st) {
     int rc = vamp_attrs();
     if (rc) return rc;
     // Wt0: y~ = (s * U^H) y        (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     rc = build_cweight((const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, st);
     if (rc) return rc;
-    if (persistent) {
-        // the same two operators, 16x16x4-packed for the persistent engine
-        rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.k, st,
-                           WPACK16);
-        if (rc) return rc;
-        rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wq2, 2 * P.k, 2 * P.N, st,
-                           WPACK16);
-        if (rc) return rc;
-    } else {
-        // Wt1: q = Vh r~               (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
-        rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wt1, P.kap1, P.ncp1, st);
-        if (rc) return rc;
-        // Wt2: V (x~ - q), V = Vh^H    (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
-        rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wt2, P.kap2, P.ncp2, st);
-        if (rc) return rc;
-    }
+    // Wt1: q = Vh r~               (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
+    rc = build_cweight((const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wt1, P.kap1, P.ncp1, st);
+    if (rc) return rc;
+    // Wt2: V (x~ - q), V = Vh^H    (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
+    rc = build_cweight((const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wt2, P.kap2, P.ncp2, st);
+    if (rc) return rc;
     const int g = (int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048);
     hipLaunchKernelGGL(vamp_init_kernel, dim3(g), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("vamp_init");
     hipLaunchKernelGGL(vamp_init_scalars, dim3(1), dim3(RWG), 0, st, P);
     AMP_LAUNCH_CHECK("vamp_init_scalars");
     // y~ = (s * U^H) y as a GEMM over the batch
+    return gemm_store((const float*)a->y, 2 * P.n, P.B, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k, 2 * P.k, st);
+}
+
+// Persistent engine: ONE launch builds the 16x16x4-packed operators (Vh, V), the y~ operator
+// s Uh and zeroes the barrier words; the Tracker's initial state and the iteration-0 scalars
+// are formed inside vamp_persist.  y~ = (s Uh) y comes from gemm_store by default: forming it
+// inside vamp_persist (AMP_YTIL_IN_KERNEL=1, n == 2N) saves ~20 us per forward but sums in
+// another order, which flips the allclose early exit of a cfg2 QPSK 9 dB golden (T 4 vs the
+// reference's 3; the exit there is decided by float32 rounding of y~).
+static bool ytil_in_kernel_requested() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_YTIL_IN_KERNEL");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st) {
+    static std::atomic<unsigned> gen{0};
+    P.gen = ++gen;
+    P.ytil_in_kernel = (ytil_in_kernel_requested() && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
+    const bool yk = P.ytil_in_kernel != 0;
+    CWeightJob j[3];
+    //   q = Vh r~        (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
+    j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.k, WPACK16};
+    //   V (x~ - q)       (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
+    j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wq2, 2 * P.k, 2 * P.N, WPACK16};
+    //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
+    j[2] = yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
+              : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
+    int rc = build_cweights(j, 3, P.pbar, 64, st);
+    if (rc || yk) return rc;
+    rc = vamp_attrs();
+    if (rc) return rc;
     return gemm_store((const float*)a->y, 2 * P.n, P.B, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k, 2 * P.k, st);
 }
 
@@ -374,7 +396,7 @@ int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const 
     const int ncu = device_cu_count();
     AMP_REQUIRE(trace && vamp_persist_eligible(d, a->k, ncu), "amp_vamp_persist_trace: not eligible / null trace");
     hipStream_t st = (hipStream_t)stream;
-    rc = vamp_prepare_impl(P, a, st, true);
+    rc = vamp_persist_prepare(P, a, st);
     if (rc) return rc;
     P.trace = (unsigned long long*)trace;
     return vamp_persist_launch(P, c64, st, ncu);
@@ -434,7 +456,7 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
                 "amp_vamp_run: persistent engine needs k == N in {64, 128, 256}, M <= 64 and ceil(B/16) = %d <= "
                 "%d CUs", cdiv(d->B, PBM), ncu);
     if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
-        rc = vamp_prepare_impl(P, a, st, true);
+        rc = vamp_persist_prepare(P, a, st);
         if (rc) return rc;
         return vamp_persist_launch(P, c64, st, ncu);
     }
@@ -465,7 +487,7 @@ int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_va
         hipEvent_t e0, e1, e2;
         (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventCreate(&e2);
         (void)hipEventRecord(e0, st);
-        rc = vamp_prepare_impl(P, a, st, true);
+        rc = vamp_persist_prepare(P, a, st);
         (void)hipEventRecord(e1, st);
         if (!rc) rc = vamp_persist_launch(P, c64, st, ncu);
         (void)hipEventRecord(e2, st);

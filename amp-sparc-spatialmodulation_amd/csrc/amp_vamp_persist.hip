@@ -254,6 +254,44 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
     const int ldr = Y.ldr, lda = Y.lda;
     const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
 
+    // y~ rows and s^2 of this wave's GEMM1 columns, in the accumulator layout
+    float yt[NT][4], s2c[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 16 * (ct0 + t) + (lane & 15);
+        const float sv = P.s[col >> 1];
+        s2c[t] = sv * sv;                                   // vamp.py:17
+    }
+    if (P.ytil_in_kernel) {
+        // y~ = (s Uh) y (vamp.py:22) for this workgroup's rows: y staged in LDS over the A/R/X
+        // region (row stride 2n + 4 = 4N + 4), GEMM on the packed s Uh operand (K = 2n = 4N)
+        const int ldy = 4 * N + 4;
+        for (int e = tid; e < PBM * N; e += PWG) {          // float4 units: 4N floats per row
+            const int row = e / N, c4 = 4 * (e - row * N);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 4 * N + c4);
+            *reinterpret_cast<float4*>(lds + row * ldy + c4) = v;
+        }
+        __syncthreads();
+        f32x4 acc[NT];
+        gemm16<NT, 2 * NT * NWV>(lds, ldy, P.Wq0, ct0, acc);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yt[t][r] = acc[t][r];
+        __syncthreads();
+    } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int col = 16 * (ct0 + t) + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * (lane >> 4) + r;
+                yt[t][r] = (row < nrows) ? P.ytil[(size_t)(row0 + row) * twok + col] : 0.f;
+            }
+        }
+    }
+    VampIter cur = vamp_first_iter(P, scr);   // vamp.py:26, 66-82 at t = 0
     // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
     {
         const float p = (float)P.sparsity;
@@ -264,19 +302,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         }
         for (int e = tid; e < PBM * N; e += PWG) lds[Y.offV1 + e] = 1.0f;
     }
-    // y~ rows and s^2 of this wave's GEMM1 columns, in the accumulator layout
-    float yt[NT][4], s2c[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int col = 16 * (ct0 + t) + (lane & 15);
-        s2c[t] = P.s2[col >> 1];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 4 * (lane >> 4) + r;
-            yt[t][r] = (row < nrows) ? P.ytil[(size_t)(row0 + row) * twok + col] : 0.f;
-        }
-    }
-    VampIter cur = P.iters[0];   // vamp_init_scalars (vamp.py:26, 66-82 at t = 0)
+
     unsigned long long* trc = P.trace;
     auto stamp = [&](int t, int ph) {
         if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * 8 + ph] = __builtin_amdgcn_s_memtime();
@@ -342,11 +368,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         PartAcc pa;
         denoise_sections_u<true, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
-        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, (unsigned)t + 1u, scr);
+        const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
+        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
         stamp(t, 5);
         // 5. batch scalars: every workgroup gathers and reduces every partial
         PartAcc g;
-        if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, (unsigned)t + 1u, P.pbar + 1, g, scr, &s_flag)) {
+        if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, tag, P.pbar + 1, g, scr, &s_flag)) {
             aborted = 1;
             break;
         }
@@ -463,6 +490,11 @@ int device_cu_count() {
     return g_ncu;
 }
 
+bool vamp_persist_ytil_in_kernel(const VampK& P) {
+    // y staged over the A/R/X region: 16 rows of 2n + 4 floats with n == 2N
+    return P.n == 2 * P.N && PBM * (2 * P.n + 4) <= playout(P.N, P.k, P.L).offV0;
+}
+
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
     if (cdiv(d->B, PBM) > ncu) return false;
@@ -543,12 +575,7 @@ static int persist_launch_nt(const VampK& P, const Const64& c64, hipStream_t st)
 
 int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu) {
     (void)ncu;
-    // barrier words + granule block: one contiguous, 256-B aligned, zeroed block (amp_vamp.h carve)
-    hipError_t e = hipMemsetAsync(P.pbar, 0, 64 * sizeof(unsigned) + (size_t)P.max_iter * P.nwg * sizeof(Partial), st);
-    if (e != hipSuccess) {
-        set_error("vamp_persist: hipMemsetAsync: %s", hipGetErrorString(e));
-        return AMP_E_LAUNCH;
-    }
+    // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
     if (persist_waves() == 4) {
         switch (P.N) {

@@ -104,6 +104,58 @@ int build_cweight(const float2* src, long so, long sj, int conj, const float* ro
     return AMP_OK;
 }
 
+struct CWeightJobs {
+    CWeightJob j[4];
+    unsigned* zero;
+    int nzero;
+};
+
+__global__ void build_cweights_kernel(CWeightJobs P) {
+    const CWeightJob J = P.j[blockIdx.y];
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < P.nzero; i += blockDim.x) P.zero[i] = 0u;
+    const long total = (long)(J.ncp / 2) * (J.kap / 2);
+    for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int o = (int)(e / (J.kap / 2)), j = (int)(e % (J.kap / 2));
+        float xr = 0.f, xi = 0.f;
+        if (o < J.O && j < J.J) {
+            const float2 v = J.src[o * J.so + j * J.sj];
+            xr = v.x;
+            xi = J.conj ? -v.y : v.y;
+            if (J.rowscale) {
+                const float s = J.rowscale[o];
+                xr = s * xr;
+                xi = s * xi;
+            }
+        }
+        J.wt[widx(2 * o, 2 * j, J.kap, J.packed)] = xr;
+        J.wt[widx(2 * o, 2 * j + 1, J.kap, J.packed)] = -xi;
+        J.wt[widx(2 * o + 1, 2 * j, J.kap, J.packed)] = xi;
+        J.wt[widx(2 * o + 1, 2 * j + 1, J.kap, J.packed)] = xr;
+    }
+}
+
+int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st) {
+    AMP_REQUIRE(njobs >= 1 && njobs <= 4, "build_cweights: %d jobs", njobs);
+    CWeightJobs P;
+    long most = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const CWeightJob& J = jobs[i];
+        AMP_REQUIRE(2 * J.J <= J.kap && 2 * J.O <= J.ncp &&
+                        (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
+                         (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0)),
+                    "build_cweights: job %d kap %d / ncp %d not tiled for layout %d", i, J.kap, J.ncp, J.packed);
+        P.j[i] = J;
+        most = std::max(most, (long)(J.ncp / 2) * (J.kap / 2));
+    }
+    P.zero = zero;
+    P.nzero = zero ? nzero : 0;
+    const int grid = (int)std::min<long>((most + 255) / 256, 2048);
+    hipLaunchKernelGGL(build_cweights_kernel, dim3(grid, njobs), dim3(256), 0, st, P);
+    AMP_LAUNCH_CHECK("build_cweights");
+    return AMP_OK;
+}
+
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st) {
     AMP_REQUIRE(kap % GBK == 0 && ncp % 128 == 0, "build_abs2_weight: kap %d / ncp %d not tiled", kap, ncp);
