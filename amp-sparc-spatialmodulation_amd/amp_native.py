@@ -51,6 +51,11 @@ class AmpVampArgs(C.Structure):
                 ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
 
+class AmpVampDecideArgs(C.Structure):
+    _fields_ = [('x', C.c_void_p), ('sym', C.c_void_p), ('idx', C.c_void_p), ('ibits_trunc', C.c_int32),
+                ('pad', C.c_int32), ('counts', C.c_void_p)]
+
+
 class AmpBampArgs(C.Structure):
     _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('pad', C.c_int32),
                 ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p),
@@ -78,6 +83,7 @@ SIGNATURES = {
     'amp_vamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
     'amp_vamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_profile': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(C.c_float), _P]),
+    'amp_vamp_detect_count': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),

@@ -13,21 +13,10 @@
 #include <algorithm>
 
 #include "amp_common.h"
+#include "amp_decide.h"
 #include "amp_host.h"
 
 namespace amp {
-
-struct DecConst {
-    int K, sbits;
-    double re[AMP_MAX_K], im[AMP_MAX_K];
-    float re32[AMP_MAX_K], im32[AMP_MAX_K];   // complex64 casts of the points (xhat values)
-    int gray[AMP_MAX_K];
-};
-
-struct alignas(16) DecPart {
-    long long ier, ser, iber, sber;
-    double mse, msef, msem, mseL;
-};
 
 struct DecK {
     int B, L, M, Na, Lin, S;
@@ -45,84 +34,34 @@ struct DecK {
     DecConst c;
 };
 
-__device__ __forceinline__ bool dec_better(double v, int i, bool n, double bv, int bi, bool bn) {
-    // does candidate (v, i, n) beat the incumbent (bv, bi, bn)?  NaN first, then larger value,
-    // then smaller flat index (np.argmax: first occurrence of the maximum; NaN counts as maximum)
-    if (n) return !bn || i < bi;
-    if (bn) return false;
-    return v > bv || (v == bv && i < bi);
-}
-
+template <int KK, int G>
 __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
+    // one section per group of G = min(M, 64) lanes (coalesced loads of consecutive positions)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int M = P.M, K = P.c.K;
-    const int G = M < 64 ? M : 64, PPL = M / G, gpw = 64 / G;
-    const int gid = lane / G, g = lane - gid * G;
-    long long ier = 0, ser = 0, iber = 0, sber = 0;
-    double mse = 0, msef = 0, msem = 0, mseL = 0;
-    const long long ibmask = (P.ibits >= 63) ? -1LL : ((1LL << P.ibits) - 1);
-    const long long sbmask = (1LL << P.c.sbits) - 1;
+    const int M = P.M;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    DecPart q = decpart_zero();
+    const long long ibmask = dec_ibmask(P.ibits);
     const int stride = gridDim.x * (AMP_WG / 64) * gpw;
-    for (int base = (blockIdx.x * (AMP_WG / 64) + wave) * gpw; base < P.S; base += stride) {
+    for (int base = (blockIdx.x * (AMP_WG / 64) + wave) * gpw; base < P.S; base += stride) {   // wave-uniform
         const int s = base + gid;
         const bool act = s < P.S;
-        const int ss = act ? s : P.S - 1;
-        double bv = -INFINITY;
-        int bi = 0x7fffffff;
-        bool bn = false;
-        for (int p = 0; p < PPL; ++p) {
-            const int m = g + p * G;
-            const float2 xv = P.xmap[(size_t)ss * M + m];
-            const double xr = (double)xv.x, xi = (double)xv.y;
-            for (int k = 0; k < K; ++k) {
-                const double v = __fma_rn(xr, P.c.re[k], __dmul_rn(xi, P.c.im[k]));
-                const bool vn = v != v;
-                const int f = m * K + k;
-                if (dec_better(v, f, vn, bv, bi, bn)) { bv = v; bi = f; bn = vn; }
-            }
-        }
-        for (int o = G >> 1; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(bv, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            const bool on = __shfl_xor((int)bn, o, 64) != 0;
-            if (dec_better(ov, oi, on, bv, bi, bn)) { bv = ov; bi = oi; bn = on; }
-        }
-        const int mh = bi / K, kh = bi - mh * K;
-        // xhat vs x over the section (loss.py:133 count_nonzero(xhat - x)), and the nMSE sum on xmmse
-        int mm = 0;
-        double se = 0.0;
-        for (int p = 0; p < PPL; ++p) {
-            const int m = g + p * G;
-            const size_t o = (size_t)ss * M + m;
-            const float2 xv = P.x[o];
-            const float hr = (m == mh) ? P.c.re32[kh] : 0.f, hi = (m == mh) ? P.c.im32[kh] : 0.f;
-            mm |= (hr - xv.x != 0.f || hi - xv.y != 0.f) ? 1 : 0;
-            const float2 e = P.xmmse[o];
-            const float dr = e.x - xv.x, di = e.y - xv.y;
-            se += (double)dr * dr + (double)di * di;
-        }
-        for (int o = G >> 1; o > 0; o >>= 1) {
-            mm |= __shfl_xor(mm, o, 64);
-            se += __shfl_xor(se, o, 64);
-        }
+        const size_t o0 = (size_t)(act ? s : P.S - 1) * M;
+        auto ld = [&](int m, float2& xv, float2& xt, float2& xe) {
+            xv = P.xmap[o0 + m]; xt = P.x[o0 + m]; xe = P.xmmse[o0 + m];
+        };
+        int bi, mm;
+        double se;
+        decide_section<KK, G, false>(P.c, M, g, ld, bi, mm, se);
         if (act && g == 0) {
             P.mism[s] = (unsigned char)mm;
             if (P.dec) P.dec[s] = bi;
-            const long long ih = (long long)s * M + mh;           // flat index of the chosen entry
-            const long long it = P.idx[s];
-            const long long sh = P.c.gray[kh];
-            const long long st = P.sym[s];
-            ier += (ih != it);
-            ser += (sh != st);
-            iber += __popcll((unsigned long long)((ih ^ it) & ibmask));
-            sber += __popcll((unsigned long long)((sh ^ st) & sbmask));
-            const int lin = (s % P.L) / P.Na;
-            mse += se;
-            if (lin == 0) msef += se;
-            if (lin == P.Lin / 2) msem += se;
-            if (lin == P.Lin - 1) mseL += se;
+            count_section(P.c, s, M, P.L, P.Na, P.Lin, bi, se, P.sym[s], P.idx[s], ibmask, q);
         }
     }
+    long long ier = q.ier, ser = q.ser, iber = q.iber, sber = q.sber;
+    double mse = q.mse, msef = q.msef, msem = q.msem, mseL = q.mseL;
     // workgroup reduction (fixed order)
     ier = group_sum(ier, 64); ser = group_sum(ser, 64); iber = group_sum(iber, 64); sber = group_sum(sber, 64);
     mse = group_sum(mse, 64); msef = group_sum(msef, 64); msem = group_sum(msem, 64); mseL = group_sum(mseL, 64);
@@ -197,6 +136,30 @@ static int decide_nblk(const amp_dims* d) {
     return std::max(1, std::min(cdiv(d->B * d->L, per), 2048));
 }
 
+template <int KK>
+static void launch_decide_k(const DecK& P, int M, hipStream_t st) {
+    const dim3 g(P.nblk), b(AMP_WG);
+    switch (M) {
+    case 1: hipLaunchKernelGGL((map_decide_kernel<KK, 1>), g, b, 0, st, P); break;
+    case 2: hipLaunchKernelGGL((map_decide_kernel<KK, 2>), g, b, 0, st, P); break;
+    case 4: hipLaunchKernelGGL((map_decide_kernel<KK, 4>), g, b, 0, st, P); break;
+    case 8: hipLaunchKernelGGL((map_decide_kernel<KK, 8>), g, b, 0, st, P); break;
+    case 16: hipLaunchKernelGGL((map_decide_kernel<KK, 16>), g, b, 0, st, P); break;
+    case 32: hipLaunchKernelGGL((map_decide_kernel<KK, 32>), g, b, 0, st, P); break;
+    default: hipLaunchKernelGGL((map_decide_kernel<KK, 64>), g, b, 0, st, P); break;   // M >= 64 (power of 2)
+    }
+}
+
+static void launch_decide(const DecK& P, int M, hipStream_t st) {
+    switch (P.c.K) {
+    case 1: launch_decide_k<1>(P, M, st); break;
+    case 2: launch_decide_k<2>(P, M, st); break;
+    case 4: launch_decide_k<4>(P, M, st); break;
+    case 8: launch_decide_k<8>(P, M, st); break;
+    default: launch_decide_k<16>(P, M, st); break;
+    }
+}
+
 }  // namespace amp
 
 using namespace amp;
@@ -230,18 +193,9 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
     P.parts = cv.take<DecPart>((size_t)P.nblk);
     P.out = (amp_counts*)counts;
     P.dec = (int*)decisions;
-    P.c.K = c->K;
-    P.c.sbits = c->symbol_bits;
-    for (int i = 0; i < AMP_MAX_K; ++i) {
-        const bool v = i < c->K;
-        P.c.re[i] = v ? c->re64[i] : 0.0;
-        P.c.im[i] = v ? c->im64[i] : 0.0;
-        P.c.re32[i] = v ? (float)c->re64[i] : 0.f;
-        P.c.im32[i] = v ? (float)c->im64[i] : 0.f;
-        P.c.gray[i] = v ? c->gray[i] : 0;
-    }
+    P.c = to_decconst(c);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(map_decide_kernel, dim3(P.nblk), dim3(AMP_WG), 0, st, P);
+    launch_decide(P, d->M, st);
     AMP_LAUNCH_CHECK("map_decide");
     hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(1024), 0, st, P);
     AMP_LAUNCH_CHECK("map_count");

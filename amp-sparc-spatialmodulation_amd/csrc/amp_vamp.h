@@ -3,6 +3,7 @@
 // scalars of one iteration (vamp.py:66-82).
 #pragma once
 
+#include "amp_decide.h"
 #include "amp_denoise.h"
 #include "amp_gemm.h"
 #include "amp_host.h"
@@ -43,6 +44,13 @@ struct VampK {
     int ytil_in_kernel; // y~ = (s Uh) y computed by the persistent kernel itself (n == 2N)
     const float* Wq0;   // s Uh 16x16x4-packed [2k][2n] (ytil_in_kernel)
     const float* y;     // [B][2n] received signal (ytil_in_kernel)
+    // fused decision + counters (amp_vamp_detect_count), persistent engine only
+    int dec_on, ibits, Na, Lin;
+    const float2* xtrue;        // [B][N] transmitted x
+    const long long* sym;       // [B*L] gray labels
+    const long long* idx;       // [B*L] flat nonzero indices
+    DecWG* dwg;                 // [nwg] per-workgroup records
+    amp_counts* counts;         // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
     Const c;
 };
@@ -56,10 +64,12 @@ struct VampWs {
     Partial* pparts;
     double* pxch;
     unsigned* pbar;
+    DecWG* dwg;
     size_t bytes;
 };
 
 static void vamp_geometry(const amp_dims* d, int k, VampK& P) {
+    P.Na = d->Na; P.Lin = d->Lin;
     P.B = d->B; P.N = d->N; P.n = d->n; P.k = k; P.L = d->L; P.M = d->M;
     P.kap0 = round_up(2 * d->n, GBK); P.ncp0 = round_up(2 * k, 128);
     P.kap1 = round_up(2 * d->N, GBK); P.ncp1 = round_up(2 * k, 128);
@@ -91,6 +101,7 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(64);                          // 256 B: pbar and the granules that
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // follow it are zeroed by one memset
+    w.dwg = cv.take<DecWG>((size_t)nwg);
     w.bytes = cv.off;
     return w;
 }
@@ -217,7 +228,7 @@ constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
-int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu);
+int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);
 int device_cu_count();
 
 }  // namespace amp

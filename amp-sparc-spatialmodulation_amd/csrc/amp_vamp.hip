@@ -254,6 +254,8 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.Wq0 = w.Wq0; P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
     P.gen = 0;
     P.ytil_in_kernel = 0;
+    P.dec_on = 0; P.ibits = 0; P.xtrue = nullptr; P.sym = nullptr; P.idx = nullptr; P.counts = nullptr;
+    P.dwg = w.dwg;
     P.y = (const float*)a->y;
     P.trace = nullptr;
     P.c = to_const(c);
@@ -399,7 +401,7 @@ int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const 
     rc = vamp_persist_prepare(P, a, st);
     if (rc) return rc;
     P.trace = (unsigned long long*)trace;
-    return vamp_persist_launch(P, c64, st, ncu);
+    return vamp_persist_launch(P, c64, DecConst{}, st, ncu);
 }
 
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine) {
@@ -458,7 +460,7 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
     if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
         rc = vamp_persist_prepare(P, a, st);
         if (rc) return rc;
-        return vamp_persist_launch(P, c64, st, ncu);
+        return vamp_persist_launch(P, c64, DecConst{}, st, ncu);
     }
     rc = vamp_prepare_impl(P, a, st);
     if (rc) return rc;
@@ -467,6 +469,31 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
         if (rc) return rc;
     }
     return vamp_finalize_impl(P, st);
+}
+
+int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                          const amp_vamp_decide_args* dec, void* stream) {
+    VampK P;
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts, "amp_vamp_detect_count: null pointer argument");
+    AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_vamp_detect_count: ibits_trunc out of range");
+    AMP_REQUIRE(d->Lin * d->Na * d->M == d->N, "amp_vamp_detect_count: inconsistent dims");
+    const int ncu = device_cu_count();
+    AMP_REQUIRE(a->engine != AMP_ENGINE_LAUNCHES && vamp_persist_eligible(d, a->k, ncu),
+                "amp_vamp_detect_count: needs the persistent engine (k == N in {64, 128, 256}, M <= 64, "
+                "ceil(B/16) = %d <= %d CUs)", cdiv(d->B, PBM), ncu);
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_persist_prepare(P, a, st);
+    if (rc) return rc;
+    P.dec_on = 1;
+    P.ibits = dec->ibits_trunc;
+    P.xtrue = (const float2*)dec->x;
+    P.sym = (const long long*)dec->sym;
+    P.idx = (const long long*)dec->idx;
+    P.counts = (amp_counts*)dec->counts;
+    return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 
 // Measurement helper (bench.py): one full forward with hipEvents between the launches on
@@ -489,7 +516,7 @@ int amp_vamp_profile(const amp_dims* d, const amp_constellation* c, const amp_va
         (void)hipEventRecord(e0, st);
         rc = vamp_persist_prepare(P, a, st);
         (void)hipEventRecord(e1, st);
-        if (!rc) rc = vamp_persist_launch(P, c64, st, ncu);
+        if (!rc) rc = vamp_persist_launch(P, c64, DecConst{}, st, ncu);
         (void)hipEventRecord(e2, st);
         (void)hipStreamSynchronize(st);
         float m01 = 0.f, m12 = 0.f;

@@ -234,8 +234,126 @@ __device__ __forceinline__ bool part_gather(__amdgpu_buffer_rsrc_t rs, unsigned 
     return ok;
 }
 
+// Fused MAP decision + error counters (Loss.error_rate, loss.py:67-179, via amp_decide.h) on
+// this workgroup's rows while r (the decision input, vamp.py:187) and xmmse are still in LDS;
+// per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
+// mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
+template <int PWG, int KK>
+__device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
+                                int nrows, float* sT, void* lab_lds, void* scr) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int M = P.M, L = P.L, N = P.N;
+    const int S = nrows * L;
+    // one coalesced bulk load of this workgroup's truth rows and labels into LDS (a per-section
+    // global load inside the decision loop left every round waiting on HBM latency)
+    long long* lsym = reinterpret_cast<long long*>(lab_lds);
+    long long* lidx = lsym + S;
+    unsigned char* mism = reinterpret_cast<unsigned char*>(lidx + S);
+    {
+        // PBM rows of 2N floats = PBM * N / 2 float4: all loads in flight before the LDS stores
+        constexpr int CH = 8;
+        const int tot = nrows * (N >> 1);
+        for (int e0 = 0; e0 < tot; e0 += PWG * CH) {
+            float4 v[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int e = e0 + u * PWG + tid;
+                if (e < tot) {
+                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
+                    v[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.xtrue) +
+                                                            (size_t)(row0 + row) * 2 * N + c4);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int e = e0 + u * PWG + tid;
+                if (e < tot) {
+                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
+                    *reinterpret_cast<float4*>(sT + row * ldr + c4) = v[u];
+                }
+            }
+        }
+    }
+    for (int e = tid; e < S; e += PWG) {
+        lsym[e] = P.sym[(size_t)row0 * L + e];
+        lidx[e] = P.idx[(size_t)row0 * L + e];
+    }
+    __syncthreads();
+    const long long ibmask = dec_ibmask(P.ibits);
+    DecPart q = decpart_zero();
+    // one section per group of DG = 4 lanes (two DPP steps per reduction), float32 prefilter
+    constexpr int DG = 4;
+    const int g = lane % DG;
+    for (int base = wave * (64 / DG); base < S; base += (PWG / 64) * (64 / DG)) {   // wave-uniform
+        const int ls = base + lane / DG;
+        const bool act = ls < S;
+        const int lsc = act ? ls : S - 1;
+        const int row = lsc / L, l = lsc - row * L;
+        const float* rp = sR + row * ldr + 2 * l * M;
+        const float* xp = sX + row * ldr + 2 * l * M;
+        const float* tp = sT + row * ldr + 2 * l * M;
+        auto ld = [&](int m, float2& xv, float2& xt, float2& xe) {
+            xv = *reinterpret_cast<const float2*>(rp + 2 * m);
+            xe = *reinterpret_cast<const float2*>(xp + 2 * m);
+            xt = *reinterpret_cast<const float2*>(tp + 2 * m);
+        };
+        int bi, mm;
+        double se;
+        decide_section<KK, DG, true>(dc, M, g, ld, bi, mm, se);
+        if (act && g == 0) {
+            const long long s = (long long)(row0 + row) * L + l;
+            mism[lsc] = (unsigned char)mm;
+            count_section(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
+        }
+    }
+    __syncthreads();
+    // channel uses (Na sections each) and trials with any mismatch (loss.py:133-136, 150)
+    long long ver = 0, verf = 0, verm = 0, verL = 0, fer = 0;
+    for (int row = tid; row < nrows; row += PWG) {
+        int trial = 0;
+        for (int lin = 0; lin < P.Lin; ++lin) {
+            int cu = 0;
+            for (int a = 0; a < P.Na; ++a) cu |= mism[row * L + lin * P.Na + a];
+            ver += cu;
+            if (lin == 0) verf += cu;
+            if (lin == P.Lin / 2) verm += cu;
+            if (lin == P.Lin - 1) verL += cu;
+            trial |= cu;
+        }
+        fer += trial;
+    }
+    q.ier = group_sum(q.ier, 64); q.ser = group_sum(q.ser, 64); q.iber = group_sum(q.iber, 64);
+    q.sber = group_sum(q.sber, 64);
+    q.mse = group_sum(q.mse, 64); q.msef = group_sum(q.msef, 64); q.msem = group_sum(q.msem, 64);
+    q.mseL = group_sum(q.mseL, 64);
+    ver = group_sum(ver, 64); verf = group_sum(verf, 64); verm = group_sum(verm, 64); verL = group_sum(verL, 64);
+    fer = group_sum(fer, 64);
+    DecWG* sw = reinterpret_cast<DecWG*>(scr);
+    if (lane == 0) {
+        DecWG w;
+        w.p = q; w.ver = ver; w.verf = verf; w.verm = verm; w.verL = verL; w.fer = fer;
+        w.pad[0] = w.pad[1] = w.pad[2] = 0;
+        sw[wave] = w;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        DecWG o = sw[0];
+        for (int v = 1; v < PWG / 64; ++v) {
+            decpart_add(o.p, sw[v].p);
+            o.ver += sw[v].ver; o.verf += sw[v].verf; o.verm += sw[v].verm; o.verL += sw[v].verL; o.fer += sw[v].fer;
+        }
+        P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
+                                 // an agent-scope release writes back the L2 and cost ~90 us)
+    }
+}
+
+__global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out) {
+    __shared__ DecWG s[16];
+    dec_fold_block(w, n, out, s);
+}
+
 template <int NT, int KK, int NWV>
-__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64) {
+__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64, DecConst dc) {
     constexpr int PWG = 64 * NWV;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
@@ -475,6 +593,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         if (aborted) s.nan_state = -1;
         *P.status = s;
     }
+    if (P.dec_on) {
+        __syncthreads();   // the V0/V1 region (vlast) becomes the label / mismatch scratch
+        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldr, row0, nrows, sA, lds + Y.offV0, scr);
+    }
 }
 
 static std::once_flag g_pers_once;
@@ -524,18 +646,29 @@ static bool persist_coop() {
 }
 
 template <int NT, int KK, int NWV>
-static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) {
+static int persist_launch_t(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
     const void* fn = (const void*)vamp_persist<NT, KK, NWV>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) {
-        set_error("vamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
-        return AMP_E_LAUNCH;
+    // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
+    // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
+    static size_t attr_lds = 0;
+    static int per_cu = 0;
+    hipError_t e = hipSuccess;
+    if (attr_lds != lds) {
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("vamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
+            return AMP_E_LAUNCH;
+        }
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * NWV, lds);
+        if (e != hipSuccess) per_cu = 0;
+        attr_lds = lds;
     }
     if (persist_coop()) {
         VampK Pc = P;
         Const64 cc = c64;
-        void* args[] = {(void*)&Pc, (void*)&cc};
+        DecConst dd = dc;
+        void* args[] = {(void*)&Pc, (void*)&cc, (void*)&dd};
         e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
         if (e != hipSuccess) {
             set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
@@ -546,14 +679,12 @@ static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) 
     }
     // plain launch: co-residency checked here (resident workgroups per CU x CUs >= grid), the
     // check hipLaunchCooperativeKernel would make; the bounded barrier spins stay as the backstop
-    int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * NWV, lds);
-    if (e != hipSuccess || per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
+    if (per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
         set_error("vamp_persist: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", P.nwg, per_cu,
                   device_cu_count());
         return AMP_E_LAUNCH;
     }
-    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, c64);
+    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, c64, dc);
     e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
@@ -563,32 +694,42 @@ static int persist_launch_t(const VampK& P, const Const64& c64, hipStream_t st) 
 }
 
 template <int NT, int NWV>
-static int persist_launch_nt(const VampK& P, const Const64& c64, hipStream_t st) {
+static int persist_launch_nt(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV>(P, c64, st);
-    case 2: return persist_launch_t<NT, 2, NWV>(P, c64, st);
-    case 4: return persist_launch_t<NT, 4, NWV>(P, c64, st);
-    case 8: return persist_launch_t<NT, 8, NWV>(P, c64, st);
-    default: return persist_launch_t<NT, 16, NWV>(P, c64, st);
+    case 1: return persist_launch_t<NT, 1, NWV>(P, c64, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV>(P, c64, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV>(P, c64, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV>(P, c64, dc, st);
+    default: return persist_launch_t<NT, 16, NWV>(P, c64, dc, st);
     }
 }
 
-int vamp_persist_launch(const VampK& P, const Const64& c64, hipStream_t st, int ncu) {
+static int persist_dispatch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st);
+
+int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu) {
     (void)ncu;
+    int rc = persist_dispatch(P, c64, dc, st);
+    if (rc || !P.dec_on) return rc;
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);
+    AMP_LAUNCH_CHECK("vamp_decide_fold");
+    return AMP_OK;
+}
+
+static int persist_dispatch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
     if (persist_waves() == 4) {
         switch (P.N) {
-        case 64: return persist_launch_nt<2, 4>(P, c64, st);
-        case 128: return persist_launch_nt<4, 4>(P, c64, st);
-        case 256: return persist_launch_nt<8, 4>(P, c64, st);
+        case 64: return persist_launch_nt<2, 4>(P, c64, dc, st);
+        case 128: return persist_launch_nt<4, 4>(P, c64, dc, st);
+        case 256: return persist_launch_nt<8, 4>(P, c64, dc, st);
         default: break;
         }
     } else {
         switch (P.N) {
-        case 64: return persist_launch_nt<1, 8>(P, c64, st);
-        case 128: return persist_launch_nt<2, 8>(P, c64, st);
-        case 256: return persist_launch_nt<4, 8>(P, c64, st);
+        case 64: return persist_launch_nt<1, 8>(P, c64, dc, st);
+        case 128: return persist_launch_nt<2, 8>(P, c64, dc, st);
+        case 256: return persist_launch_nt<4, 8>(P, c64, dc, st);
         default: break;
         }
     }

@@ -96,6 +96,26 @@ class Loss:
                                            nat.stream_ptr(dev)), 'amp_map_decide_count')
         return counts
 
+    def decide_args(self, x, symbols, indices, out: torch.Tensor) -> nat.AmpVampDecideArgs:
+        """amp_vamp_decide_args for a fused forward + decision (amp_vamp_detect_count): the
+        truth tensors on the device, kept alive on this Loss until the next call."""
+        if self.decision_mode != 'sparc':
+            raise NotImplementedError("native decision implements generator_mode='sparc' (loss.py:282-302)")
+        dev = out.device
+        B = self.B
+        xt = _flat_c64(x, B, 'x')
+        sym = _as_device_labels(symbols, dev)
+        idx = _as_device_labels(indices, dev)
+        S = B * self.config.L
+        if sym.numel() != S or idx.numel() != S:
+            raise ValueError(f'expected {S} labels/indices, got {sym.numel()}/{idx.numel()}')
+        self._keep = (xt, sym, idx)
+        a = nat.AmpVampDecideArgs()
+        a.x, a.sym, a.idx = nat.dptr(xt, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices')
+        a.ibits_trunc = self._ibits
+        a.counts = nat.dptr(out)
+        return a
+
     @staticmethod
     def read_counts(buf: torch.Tensor) -> nat.AmpCounts:
         raw = buf[:C.sizeof(nat.AmpCounts)].cpu().numpy().tobytes()

@@ -9,6 +9,7 @@ the host reads back one 128-byte record per forward.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -24,6 +25,9 @@ def _c64(t: torch.Tensor, shape) -> torch.Tensor:
     if t.dtype != torch.complex64:
         t = t.to(torch.complex64)
     return t.contiguous()
+
+
+_FUSED_DECIDE = os.environ.get('AMP_FUSED_DECIDE', '1') != '0'
 
 
 class _Buffers:
@@ -178,10 +182,21 @@ class VAMP(nn.Module):
 
     def forward(self, U: torch.Tensor, s: torch.Tensor, Vh: torch.Tensor, y: torch.Tensor, SNR: float,
                 x: torch.Tensor, symbols: np.ndarray, indices: np.ndarray) -> Loss:
-        T = self.detect(U, s, Vh, y, SNR)
         self.L.dump()                                                    # vamp.py:180
-        # decision on T.r (vamp.py:187); counters land next to the status record
-        self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=T.buf.res[64:])
+        T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
+        T.args.engine = self.engine
+        lib = nat.lib()
+        fused = (_FUSED_DECIDE and
+                 lib.amp_vamp_select_engine(C.byref(T.dims), T.k, self.engine) == nat.ENGINE_PERSISTENT)
+        if fused:
+            # forward + decision on T.r (vamp.py:187) + counters in one launch sequence
+            dec = self.L.decide_args(x, symbols, indices, out=T.buf.res[64:])
+            nat.check(lib.amp_vamp_detect_count(C.byref(T.dims), C.byref(T.const), C.byref(T.args), C.byref(dec),
+                                                 T.stream), 'amp_vamp_detect_count')
+        else:
+            nat.check(lib.amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream), 'amp_vamp_run')
+            # decision on T.r (vamp.py:187); counters land next to the status record
+            self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=T.buf.res[64:])
         status, counts = read_result(T.buf.res)                          # the forward's one host sync
         if status.nan_state < 0:
             raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')

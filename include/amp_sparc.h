@@ -101,7 +101,7 @@ typedef struct amp_vamp_args {
 
 /* Engines of amp_vamp_run (same results up to f32 summation order):
  *  LAUNCHES   three launches per iteration (the layer-level path below);
- *  PERSISTENT one cooperative launch for the whole loop: each workgroup keeps 16 trials'
+ *  PERSISTENT one launch for the whole loop (co-residency checked): each workgroup keeps 16 trials'
  *             state in LDS across iterations, one grid barrier per iteration carries the
  *             batch-global scalars (needs k == N, N % 32 == 0, N <= 256, M <= 64 and
  *             ceil(B/16) workgroups co-resident: B <= 16 x #CUs);
@@ -125,6 +125,22 @@ int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_a
 int amp_vamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
 int amp_vamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t t, void* stream);
 int amp_vamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
+/* VAMP.forward + Loss.error_rate in one call (vamp.py:159-187 then loss.py:67-179): the
+ * forward of amp_vamp_run and the MAP decision on its r (vamp.py:187) with every counter of
+ * amp_map_decide_count.  On the PERSISTENT engine the decision runs in the same launch, on
+ * the rows each workgroup still holds in LDS (the counters are identical to
+ * amp_map_decide_count's).  Returns AMP_E_ARG when the shape is not persistent-eligible (use
+ * amp_vamp_run + amp_map_decide_count). */
+typedef struct amp_vamp_decide_args {
+    const void* x;        /* c64 [B][N] transmitted vector */
+    const void* sym;      /* int64 [B*L] true gray labels (data.py:89) */
+    const void* idx;      /* int64 [B*L] true flat nonzero indices (data.py:90) */
+    int32_t ibits_trunc;  /* ceil(log2(Lin*B*Na)) (loss.py:20) */
+    int32_t pad;
+    void* counts;         /* out amp_counts (device) */
+} amp_vamp_decide_args;
+int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                          const amp_vamp_decide_args* dec, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
  * launches, in milliseconds.  LAUNCHES engine: ms_out[4] = mean GEMM1 / GEMM2+denoiser /
  * reduction kernel time per executed iteration and the whole forward.  PERSISTENT engine
