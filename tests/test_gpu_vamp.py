@@ -277,3 +277,29 @@ def _check_T(got, ref, max_iter, ver_ref=0.0):
         assert ref - 5 <= got <= max_iter, (got, ref)
     else:
         assert abs(got - ref) <= 5, (got, ref)
+
+
+@pytest.mark.parametrize('name,ebn0', [('cfg4_vamp_16qam', 8.0), ('cfg4_vamp_qpsk', 4.0), ('cfg2_vamp_16qam', 20.0),
+                                       ('cfg2_vamp_qpsk', 0.0)])
+def test_fused_decision_equals_standalone(device, name, ebn0):
+    """amp_vamp_detect_count (decision + counters inside the persistent launch, from LDS) gives
+    the same amp_counts as amp_vamp_run followed by amp_map_decide_count on the same forward:
+    integer counters exactly, the float64 squared-error sums to summation-order rounding."""
+    import ctypes as C
+    import amp_native as nat
+    from vamp import VAMP, read_result
+    ent = CURVES[name]
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    inp = _regen_inputs(cfg, 0, ebn0)
+    det = VAMP(cfg, engine=nat.ENGINE_PERSISTENT)
+    L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    _, fused = read_result(det.last.buf.res)
+    T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    buf = det.L.device_counts(T.buf.r, T.buf.xmmse, inp['x'], inp['sym'], inp['idx'])
+    sep = det.L.read_counts(buf)
+    for f in ('ier', 'ser', 'iber', 'sber', 'ver', 'verf', 'verm', 'verL', 'fer'):
+        assert getattr(fused, f) == getattr(sep, f), (f, getattr(fused, f), getattr(sep, f))
+    for f in ('mse', 'msef', 'msem', 'mseL'):
+        a, b = getattr(fused, f), getattr(sep, f)
+        assert (a == b) or abs(a - b) <= 1e-12 * max(abs(a), abs(b)) or (a != a and b != b), (f, a, b)
+    assert int(L.loss['T']) == int(T.status().T)
