@@ -48,6 +48,7 @@ class Loss:
         self.sbits = config.symbol_bits
         self.rate = config.code_rate
         self.shannon_limt_dB = config.shannon_limit_dB
+        self._pending = None
         self.loss = {'T': 0}
         self.keys = list(KEYS)
         self.dtype = torch.complex64 if config.is_complex else torch.float32
@@ -61,6 +62,25 @@ class Loss:
         self._dims = None
 
     # ------------------------------------------------------------------
+    # The metrics dict.  A detector may leave its last forward's counters in flight on the
+    # device (``_pending``: a callable that waits for them and records them here); the first
+    # access resolves them, so callers see the reference's eager semantics.
+    @property
+    def loss(self) -> dict:
+        if self._pending is not None:
+            self.resolve()
+        return self._loss
+
+    @loss.setter
+    def loss(self, value: dict) -> None:
+        self._loss = value
+
+    def resolve(self) -> None:
+        """Wait for and record the counters of the forward still in flight (if any)."""
+        p, self._pending = self._pending, None
+        if p is not None:
+            p()
+
     def _native(self):
         if self._const is None:
             self._const = self.config.constellation()

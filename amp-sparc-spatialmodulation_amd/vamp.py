@@ -104,7 +104,9 @@ class Tracker:
                                               self.stream), 'amp_vamp_finalize')
 
     def status(self) -> nat.AmpStatus:
-        return nat.AmpStatus.from_buffer_copy(self.buf.res[:C.sizeof(nat.AmpStatus)].cpu().numpy().tobytes())
+        res = getattr(self, 'res', None)
+        res = self.buf.res if res is None else res
+        return nat.AmpStatus.from_buffer_copy(res[:C.sizeof(nat.AmpStatus)].cpu().numpy().tobytes())
 
 
 class VAMPLayer(nn.Module):
@@ -170,6 +172,8 @@ class VAMP(nn.Module):
         self.layers = nn.ModuleList([VAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
         self._bufs = _Buffers()
+        self._ring = None
+        self._slot = 1
         self.last = None
 
     def detect(self, U, s, Vh, y, SNR: float) -> Tracker:
@@ -180,27 +184,52 @@ class VAMP(nn.Module):
                   'amp_vamp_run')
         return T
 
+    def _result_slot(self, device):
+        """One of two (device, pinned host) 256-byte result buffers, alternating per forward, so
+        a forward's status / counters stay readable while the next forward runs."""
+        if self._ring is None or self._ring[0][0].device != device:
+            self._ring = [(torch.zeros(256, dtype=torch.uint8, device=device),
+                           torch.zeros(256, dtype=torch.uint8, pin_memory=True)) for _ in range(2)]
+        self._slot ^= 1
+        return self._ring[self._slot]
+
     def forward(self, U: torch.Tensor, s: torch.Tensor, Vh: torch.Tensor, y: torch.Tensor, SNR: float,
                 x: torch.Tensor, symbols: np.ndarray, indices: np.ndarray) -> Loss:
-        self.L.dump()                                                    # vamp.py:180
+        """vamp.py:159-187.  Everything runs on the device; the returned Loss resolves its
+        counters on first access (the forward's one host synchronisation), so the launches of
+        the next forward can be queued before this one's results are read back."""
         T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
         T.args.engine = self.engine
+        res, host = self._result_slot(T.y.device)
+        T.res = res
+        T.args.status = nat.dptr(res)
         lib = nat.lib()
         fused = (_FUSED_DECIDE and
                  lib.amp_vamp_select_engine(C.byref(T.dims), T.k, self.engine) == nat.ENGINE_PERSISTENT)
         if fused:
             # forward + decision on T.r (vamp.py:187) + counters in one launch sequence
-            dec = self.L.decide_args(x, symbols, indices, out=T.buf.res[64:])
+            dec = self.L.decide_args(x, symbols, indices, out=res[64:])
             nat.check(lib.amp_vamp_detect_count(C.byref(T.dims), C.byref(T.const), C.byref(T.args), C.byref(dec),
                                                  T.stream), 'amp_vamp_detect_count')
         else:
             nat.check(lib.amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream), 'amp_vamp_run')
             # decision on T.r (vamp.py:187); counters land next to the status record
-            self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=T.buf.res[64:])
-        status, counts = read_result(T.buf.res)                          # the forward's one host sync
-        if status.nan_state < 0:
-            raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')
-        self.L.record(self.L.rates_from_counts(counts), int(status.T))
+            self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
+        host.copy_(res, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        self.L.resolve()                 # the previous forward's counters (it has finished by now)
+        self.L.dump()                                                    # vamp.py:180
+
+        def finish(L=self.L):
+            done.synchronize()
+            raw = host.numpy().tobytes()
+            status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
+            counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
+            if status.nan_state < 0:
+                raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')
+            L.record(L.rates_from_counts(counts), int(status.T))
+        self.L._pending = finish
         self.last = T
         return self.L
 

@@ -5,7 +5,8 @@
 A step = one Monte-Carlo epoch of the hot path on inputs already resident in HBM:
 VAMP.forward (all iterations, early exit, MAP decision and every error counter on the
 GPU) + the one 128-byte result read-back — exactly what Model.simulate calls per epoch
-(vamp_model.py:61).  Input generation and the SVD are outside the timed region
+(vamp_model.py:61).  The read-back of step k is waited for after step k+1's launches are
+queued (Loss resolves lazily), so the GPU does not idle on the host between steps.  Input generation and the SVD are outside the timed region
 (SURVEY.md §8(d)).  Each rank runs its own independent epoch (its own seed): Monte-Carlo
 epochs are independent, so the path shards with no data-path collective ("weak").
 
@@ -100,8 +101,10 @@ def traffic_from_profile(persistent):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    # the chip's clocks ramp over the first ~25 ms of back-to-back epochs (vamp_persist 1.22 ms
+    # -> 1.05 ms over 20 steps on the box, r01): the default warmup covers the ramp
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=30)
     ap.add_argument('--config', default='cfg4', choices=sorted(CONFIGS))
     ap.add_argument('--ebn0', type=float, default=8.0)
     ap.add_argument('--seed', type=int, default=0)
@@ -144,7 +147,8 @@ def main():
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        L = step()
+        L = step()       # a step's counters are read back while the next step's launches run
+    L.resolve()          # ... and the last step's inside the timed region too
     torch.cuda.synchronize(device)
     el = time.perf_counter() - t0
     if dist:

@@ -293,7 +293,8 @@ def test_fused_decision_equals_standalone(device, name, ebn0):
     inp = _regen_inputs(cfg, 0, ebn0)
     det = VAMP(cfg, engine=nat.ENGINE_PERSISTENT)
     L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
-    _, fused = read_result(det.last.buf.res)
+    L.resolve()
+    _, fused = read_result(det.last.res)
     T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     buf = det.L.device_counts(T.buf.r, T.buf.xmmse, inp['x'], inp['sym'], inp['idx'])
     sep = det.L.read_counts(buf)
