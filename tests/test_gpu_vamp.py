@@ -304,3 +304,49 @@ def test_fused_decision_equals_standalone(device, name, ebn0):
         a, b = getattr(fused, f), getattr(sep, f)
         assert (a == b) or abs(a - b) <= 1e-12 * max(abs(a), abs(b)) or (a != a and b != b), (f, a, b)
     assert int(L.loss['T']) == int(T.status().T)
+
+
+@pytest.mark.parametrize('B', [1, 17, 1000, 4097])
+def test_vamp_ragged_batches_engines_agree(device, B):
+    """Ragged batches: a last persistent workgroup with fewer than 16 trials (B = 17, 1000),
+    one trial (B = 1), and one trial past the persistent engine's 16 x #CUs limit (B = 4097:
+    AUTO falls back to the launch engine).  After 3 iterations r of both engines agrees to
+    float32 summation-order noise; over 20 iterations T and the counting metrics agree where the
+    early exit is well conditioned (B >= 17 here: the oracle's allclose ratio stays >= 50 at
+    every iteration; at B = 1 it touches 1.28, so T there is rounding noise, as in
+    _check_T)."""
+    import amp_native as nat
+    from vamp import VAMP
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    cfg3 = _config(64, 4, 128, B, 'QPSK', iterations=3)
+    inp = _regen_inputs(cfg3, 3, 6.0)
+    eng = nat.lib().amp_vamp_select_engine(cfg3.dims(), 64, nat.ENGINE_AUTO)
+    assert eng == (nat.ENGINE_LAUNCHES if B > 16 * ncu else nat.ENGINE_PERSISTENT)
+    rs = [VAMP(cfg3, engine=e).detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR']).r.clone()
+          for e in (nat.ENGINE_LAUNCHES, nat.ENGINE_AUTO)]
+    scale = float(rs[0].abs().max())
+    assert torch.allclose(rs[0], rs[1], rtol=0, atol=1e-4 * scale), float((rs[0] - rs[1]).abs().max())
+    if B == 1:
+        return
+    cfg = _config(64, 4, 128, B, 'QPSK', iterations=20)
+    outs = []
+    for e in (nat.ENGINE_LAUNCHES, nat.ENGINE_AUTO):
+        L = VAMP(cfg, engine=e)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        outs.append({k: float(np.asarray(v)) for k, v in L.loss.items()})
+    a, b = outs
+    assert a['T'] == b['T'], (a['T'], b['T'])
+    for k in ('ver', 'ser', 'fer', 'ier', 'iber', 'sber'):
+        assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
+
+
+def test_vamp_empty_batch_raises(device):
+    """B = 0 never reaches a launch: like the reference, Loss(config) raises OverflowError on
+    log2(Lin * B * Na) (loss.py:20); the C ABI itself rejects B <= 0 (AMP_E_ARG)."""
+    import amp_native as nat
+    from vamp import VAMP
+    cfg = _config(64, 4, 128, 1, 'QPSK', iterations=5)
+    inp = _regen_inputs(cfg, 0, 6.0)
+    cfg.B = 0
+    with pytest.raises((OverflowError, nat.AmpError, ValueError, RuntimeError)):
+        VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'][:0], inp['SNR'], inp['x'][:0], inp['sym'][:0],
+                  inp['idx'][:0]).loss
