@@ -134,102 +134,137 @@ __device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const
 // scalar form (each packed lane is the same IEEE operation).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <bool kVar, int KK, int U, int G, class P>
-__device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa) {
-    static_assert(KK % 2 == 0, "packed form needs an even constellation size");
-    constexpr int KH = KK / 2;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int gpw = 64 / G;
-    const int gid = lane / G, g = lane % G;
-    const int nw = blockDim.x >> 6;
-    f32x2 pre[KH], pim[KH], sym[KK];   // (re_k, re_k+1), (im_k, im_k+1); (re_k, im_k)
+// The constellation as packed operands, kept in VGPRs: (re_k, re_k+1), (im_k, im_k+1) and
+// (re_k, im_k).
+template <int KK>
+struct DenRegs {
+    f32x2 pre[KK / 2], pim[KK / 2], sym[KK];
+    __device__ __forceinline__ void load(const Const& c) {
 #pragma unroll
-    for (int h = 0; h < KH; ++h) {
-        pre[h] = f32x2{c.re[2 * h], c.re[2 * h + 1]};
-        pim[h] = f32x2{c.im[2 * h], c.im[2 * h + 1]};
-        asm volatile("" : "+v"(pre[h]), "+v"(pim[h]));
-    }
+        for (int h = 0; h < KK / 2; ++h) {
+            pre[h] = f32x2{c.re[2 * h], c.re[2 * h + 1]};
+            pim[h] = f32x2{c.im[2 * h], c.im[2 * h + 1]};
+            asm volatile("" : "+v"(pre[h]), "+v"(pim[h]));
+        }
 #pragma unroll
-    for (int k = 0; k < KK; ++k) {
-        sym[k] = f32x2{c.re[k], c.im[k]};
-        asm volatile("" : "+v"(sym[k]));
+        for (int k = 0; k < KK; ++k) {
+            sym[k] = f32x2{c.re[k], c.im[k]};
+            asm volatile("" : "+v"(sym[k]));
+        }
     }
+};
+
+// Per-lane section statistics, folded into the float64 PartAcc once at the end.
+struct DenStat {
     float st_abs = 0.f, st_min = INFINITY;
     bool st_bad = false;
-    for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {   // wave-uniform trip count
-        int sec[U];
-        bool act[U];
-        f32x2 xk[U][KH];
-        float smax[U], sabs[U], ur[U], ui[U];
+    __device__ __forceinline__ void fold(PartAcc& pa) const {
+        pa.maxabs = st_bad ? __longlong_as_double(0x7ff8000000000000LL) : nan_max(pa.maxabs, (double)st_abs);
+        pa.minsecmax = nan_min(pa.minsecmax, (double)st_min);
+    }
+};
+
+// One step of the packed denoiser: sections base + u * gpw + gid (u < U) of this wave.
+// FULL: every one of them exists (< nsec): no branches at all, so the step can be scheduled
+// into a surrounding MFMA stream (the section statistics are then stored by every lane of the
+// group — the same value).
+template <bool kVar, int KK, int U, int G, bool FULL, class P>
+__device__ __forceinline__ void denoise_step_gp(const P& pol, int base, int nsec, const DenRegs<KK>& R, PartAcc& pa,
+                                                DenStat& S) {
+    static_assert(KK % 2 == 0, "packed form needs an even constellation size");
+    constexpr int KH = KK / 2;
+    const int lane = threadIdx.x & 63;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    int sec[U];
+    bool act[U];
+    f32x2 xk[U][KH];
+    float smax[U], sabs[U], ur[U], ui[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            sec[u] = base + u * gpw + gid;
-            act[u] = sec[u] < nsec;
-            float rr, ri, it;
-            pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
-            ur[u] = rr * it; ui[u] = ri * it;   // c64 / f32 == multiply by the reciprocal
+    for (int u = 0; u < U; ++u) {
+        sec[u] = base + u * gpw + gid;
+        act[u] = FULL || sec[u] < nsec;
+        float rr, ri, it;
+        pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
+        ur[u] = rr * it; ui[u] = ri * it;   // c64 / f32 == multiply by the reciprocal
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool bad = !(fabsf(ur[u]) <= FLT_MAX && fabsf(ui[u]) <= FLT_MAX);
+        S.st_bad |= act[u] && bad;
+        const f32x2 u2 = f32x2{ur[u], ur[u]}, v2 = f32x2{ui[u], ui[u]};
+        float lmax = -FLT_MAX, lmin = FLT_MAX;
+#pragma unroll
+        for (int h = 0; h < KH; ++h) {
+            xk[u][h] = __builtin_elementwise_fma(u2, R.pre[h], v2 * R.pim[h]);
+            lmax = fmaxf(lmax, fmaxf(xk[u][h].x, xk[u][h].y));
+            lmin = fminf(lmin, fminf(xk[u][h].x, xk[u][h].y));
         }
+        smax[u] = lmax;
+        sabs[u] = fmaxf(lmax, -lmin);
+    }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (act[u]) st_bad |= !(fabsf(ur[u]) <= FLT_MAX && fabsf(ui[u]) <= FLT_MAX);
-            const f32x2 u2 = f32x2{ur[u], ur[u]}, v2 = f32x2{ui[u], ui[u]};
-            float lmax = -FLT_MAX, lmin = FLT_MAX;
+    for (int u = 0; u < U; ++u) { smax[u] = group_fmax_c<G>(smax[u]); sabs[u] = group_fmax_c<G>(sabs[u]); }
+    float zt[U], ze[U];
+    f32x2 s2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const f32x2 m2 = f32x2{smax[u], smax[u]};
+        const f32x2 l2 = f32x2{AMP_LOG2E, AMP_LOG2E};
+        f32x2 z2 = f32x2{0.f, 0.f}, a2 = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < KH; ++h) {
+            const f32x2 d = (xk[u][h] - m2) * l2;
+            const f32x2 e = f32x2{__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+            xk[u][h] = e;
+            z2 += e;
+            a2 = __builtin_elementwise_fma(R.sym[2 * h], f32x2{e.x, e.x}, a2);
+            a2 = __builtin_elementwise_fma(R.sym[2 * h + 1], f32x2{e.y, e.y}, a2);
+        }
+        zt[u] = z2.x + z2.y; ze[u] = 0.f; s2[u] = a2;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const float iz = __builtin_amdgcn_rcpf(zt[u]);
+        const f32x2 x2 = s2[u] * f32x2{iz, iz};
+        float var = 0.f;
+        if (kVar) {
+            f32x2 v2 = f32x2{0.f, 0.f};
 #pragma unroll
             for (int h = 0; h < KH; ++h) {
-                xk[u][h] = __builtin_elementwise_fma(u2, pre[h], v2 * pim[h]);
-                lmax = fmaxf(lmax, fmaxf(xk[u][h].x, xk[u][h].y));
-                lmin = fminf(lmin, fminf(xk[u][h].x, xk[u][h].y));
+                const f32x2 d0 = x2 - R.sym[2 * h], d1 = x2 - R.sym[2 * h + 1];
+                v2 = __builtin_elementwise_fma(d0 * d0, f32x2{xk[u][h].x, xk[u][h].x}, v2);
+                v2 = __builtin_elementwise_fma(d1 * d1, f32x2{xk[u][h].y, xk[u][h].y}, v2);
             }
-            smax[u] = lmax;
-            sabs[u] = fmaxf(lmax, -lmin);
+            var = (x2.x * x2.x + x2.y * x2.y) * (ze[u] * iz) + (v2.x + v2.y) * iz;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) { smax[u] = group_fmax_c<G>(smax[u]); sabs[u] = group_fmax_c<G>(sabs[u]); }
-        float zt[U], ze[U];
-        f32x2 s2[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const f32x2 m2 = f32x2{smax[u], smax[u]};
-            const f32x2 l2 = f32x2{AMP_LOG2E, AMP_LOG2E};
-            f32x2 z2 = f32x2{0.f, 0.f}, a2 = f32x2{0.f, 0.f};
-#pragma unroll
-            for (int h = 0; h < KH; ++h) {
-                const f32x2 d = (xk[u][h] - m2) * l2;
-                const f32x2 e = f32x2{__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-                xk[u][h] = e;
-                z2 += e;
-                a2 = __builtin_elementwise_fma(sym[2 * h], f32x2{e.x, e.x}, a2);
-                a2 = __builtin_elementwise_fma(sym[2 * h + 1], f32x2{e.y, e.y}, a2);
-            }
-            zt[u] = z2.x + z2.y; ze[u] = 0.f; s2[u] = a2;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float iz = __builtin_amdgcn_rcpf(zt[u]);
-            const f32x2 x2 = s2[u] * f32x2{iz, iz};
-            float var = 0.f;
-            if (kVar) {
-                f32x2 v2 = f32x2{0.f, 0.f};
-#pragma unroll
-                for (int h = 0; h < KH; ++h) {
-                    const f32x2 d0 = x2 - sym[2 * h], d1 = x2 - sym[2 * h + 1];
-                    v2 = __builtin_elementwise_fma(d0 * d0, f32x2{xk[u][h].x, xk[u][h].x}, v2);
-                    v2 = __builtin_elementwise_fma(d1 * d1, f32x2{xk[u][h].y, xk[u][h].y}, v2);
-                }
-                var = (x2.x * x2.x + x2.y * x2.y) * (ze[u] * iz) + (v2.x + v2.y) * iz;
-            }
-            if (act[u]) {
-                pol.store(sec[u], g, x2.x, x2.y, var, pa);
-                st_abs = nan_max(st_abs, sabs[u]);
-                st_min = nan_min(st_min, smax[u]);
-                if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
-            }
+        if (FULL) {
+            pol.store(sec[u], g, x2.x, x2.y, var, pa);
+            S.st_abs = nan_max(S.st_abs, sabs[u]);
+            S.st_min = nan_min(S.st_min, smax[u]);
+            pol.section(sec[u], smax[u], sabs[u]);
+        } else if (act[u]) {
+            pol.store(sec[u], g, x2.x, x2.y, var, pa);
+            S.st_abs = nan_max(S.st_abs, sabs[u]);
+            S.st_min = nan_min(S.st_min, smax[u]);
+            if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
         }
     }
-    pa.maxabs = st_bad ? __longlong_as_double(0x7ff8000000000000LL) : nan_max(pa.maxabs, (double)st_abs);
-    pa.minsecmax = nan_min(pa.minsecmax, (double)st_min);
+}
+
+template <bool kVar, int KK, int U, int G, class P>
+__device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    const int wave = threadIdx.x >> 6;
+    constexpr int gpw = 64 / G;
+    const int nw = blockDim.x >> 6;
+    DenRegs<KK> R;
+    R.load(c);
+    DenStat S;
+    for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U)   // wave-uniform trip count
+        denoise_step_gp<kVar, KK, U, G, false>(pol, base, nsec, R, pa, S);
+    S.fold(pa);
 }
 
 // Runtime M (a power of two <= 64) -> the compile-time group size; PK selects the packed form.
