@@ -163,6 +163,9 @@ def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
         raise TypeError(f'{name}: expected {dtype}, got {t.dtype}')
     if not t.is_contiguous():
         raise ValueError(f'{name}: must be contiguous')
+    if t.is_conj() or t.is_neg():
+        # a lazy conjugate / negation view: its memory does not hold its values
+        raise ValueError(f'{name}: lazy conj/neg view; call .resolve_conj().resolve_neg() first')
     return t.data_ptr()
 
 

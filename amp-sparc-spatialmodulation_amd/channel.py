@@ -51,6 +51,8 @@ class Channel:
 
     def generate_as_sparc(self):
         """(W float32 [Lout,Lin], A complex64 [Nr*Lout, Nt*Lin]) — channel.py:75-95."""
+        if self.rng == 'device':
+            return self._generate_as_sparc_device()
         W = self._base_matrix()
         hr = np.random.normal(size=(self.Nr, self.Nt, self.Lh))
         hj = np.random.normal(size=(self.Nr, self.Nt, self.Lh))
@@ -68,6 +70,26 @@ class Channel:
         Wt = torch.tensor(W, dtype=torch.float32, device=self.device)
         At = torch.tensor(A, dtype=self.dtype, device=self.device)
         return Wt, At
+
+    def _generate_as_sparc_device(self):
+        """Throughput mode: the same block structure and distribution as generate_as_sparc,
+        h ~ CN(0, 1/(Na Lin)) drawn by the device generator (a different random stream from the
+        reference's numpy one: statistical, not bitwise, parity)."""
+        W = self._base_matrix()
+        shape = (self.Nr, self.Nt, self.Lh)
+        hr = torch.randn(shape, device=self.device, dtype=torch.float32)
+        hj = torch.randn(shape, device=self.device, dtype=torch.float32)
+        h = torch.complex(hr, hj) * float(1.0 / np.sqrt(2 * self.Na * self.Lin))
+        sw = np.sqrt(W)
+        A = torch.zeros((self.Nr * self.Lout, self.Nt * self.Lin), dtype=torch.complex64, device=self.device)
+        for l in range(self.Lh):
+            for i in range(self.Lin):
+                o = i + l
+                if o >= self.Lout:
+                    continue
+                A[o * self.Nr:(o + 1) * self.Nr, i * self.Nt:(i + 1) * self.Nt] += float(sw[o, i]) * h[:, :, l]
+        Wt = torch.tensor(W, dtype=torch.float32, device=self.device)
+        return Wt, A.to(self.dtype)
 
     def generate_channel(self) -> torch.Tensor:
         """Block-Toeplitz MIMO-ISI channel with trunc/tail/cyclic edges (channel.py:40-73)."""

@@ -22,7 +22,8 @@ def _pow2(v: int) -> bool:
 
 
 class Data:
-    def __init__(self, config: Config) -> None:
+    def __init__(self, config: Config, rng: str = 'host') -> None:
+        self.rng = rng
         self.B = config.B
         self.Lin = config.Lin
         self.Nt = config.Nt
@@ -44,6 +45,8 @@ class Data:
 
     def generate_message(self):
         """(x [B, Nt*Lin, 1] on config.device, gray labels, flat nonzero indices) — data.py:45-53."""
+        if self.rng == 'device':
+            return self._segmented_device()
         x, z, i = self._generator()
         return torch.tensor(x, device=self.device, dtype=self.dtype), z, i
 
@@ -89,3 +92,19 @@ class Data:
         x = np.reshape(x, (self.B, -1, 1))
         index = x.ravel().nonzero()[0]
         return x, xgray.ravel()[index], index
+
+    def _segmented_device(self):
+        """Throughput mode of ``segmented``: positions and symbols drawn by the device generator
+        (uniform, as data.py:82-87), x scattered on the device; labels and indices returned as
+        int64 device tensors (the decision consumes them there)."""
+        if self._generator != self.segmented:
+            raise NotImplementedError("rng='device' implements the 'sparc' / 'segmented' generator")
+        S, M, K = self.B * self.L, self.M, self.cardinality
+        pos = torch.randint(0, M, (S,), device=self.device)
+        k = torch.randint(0, K, (S,), device=self.device)
+        sym = torch.as_tensor(np.asarray(self.symbols), dtype=torch.complex128, device=self.device).to(self.dtype)
+        gray = torch.as_tensor(np.asarray(self.gray), dtype=torch.int64, device=self.device)
+        x = torch.zeros((S, M), dtype=self.dtype, device=self.device)
+        x[torch.arange(S, device=self.device), pos] = sym[k]
+        index = torch.arange(S, device=self.device, dtype=torch.int64) * M + pos
+        return x.reshape(self.B, -1, 1), gray[k], index

@@ -33,7 +33,7 @@ def _flat_c64(t: torch.Tensor, B: int, name: str) -> torch.Tensor:
     t = t.reshape(B, -1)
     if t.dtype != torch.complex64:
         t = t.to(torch.complex64)
-    return t.contiguous()
+    return t.resolve_conj().resolve_neg().contiguous()
 
 
 class Loss:

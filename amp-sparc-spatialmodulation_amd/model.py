@@ -48,7 +48,10 @@ def _dist():
 
 class Model(nn.Module):
     def __init__(self, config: Config, detector: str = 'vamp', path: str | None = None, amp=None,
-                 seed: int | None = None) -> None:
+                 seed: int | None = None, rng: str = 'host') -> None:
+        """rng='host' (default): the reference's numpy / torch-CPU random streams, bit for bit
+        (parity mode).  rng='device': channel, messages and noise drawn on the GPU and the SVD
+        on the GPU (throughput mode: same distributions, different streams)."""
         super().__init__()
         self.config = config
         self.detector = detector
@@ -57,8 +60,9 @@ class Model(nn.Module):
         self.min_snr = self.shannon_limit
         self.amp = amp if amp is not None else _detector(detector, config)
         self.loss = Loss(config)
-        self.channel = Channel(config)
-        self.data = Data(config)
+        self.rng = rng
+        self.channel = Channel(config, rng=rng)
+        self.data = Data(config, rng=rng)
         self.path = path if path is not None else f'Simulations/{_DIRS[detector]}/{config.name}'
         self.rank, self.world = _dist()
         if seed is not None:
@@ -75,7 +79,11 @@ class Model(nn.Module):
             self._A = A
             self._W = W
             if self.detector == 'vamp':
-                self._svd = torch.linalg.svd(A, full_matrices=False)
+                if self.rng == 'device':
+                    self._svd = torch.linalg.svd(A, full_matrices=False)
+                else:   # LAPACK on the host, as the reference's CPU path (vamp_model.py:58)
+                    U, s, Vh = torch.linalg.svd(A.cpu(), full_matrices=False)
+                    self._svd = (U.to(A.device), s.to(A.device), Vh.to(A.device))
         x, sym, idx = self.data.generate_message()
         y = self._A @ x + self.channel.awgn(SNR)
         if self.detector == 'vamp':

@@ -60,7 +60,7 @@ class SCAMP(nn.Module):
         n, N = A.shape[-2], A.shape[-1]
         A = _c64(A, (n, N))
         y = _c64(y, (B, n))
-        W = W.reshape(cfg.Lout, cfg.Lin).to(device=y.device, dtype=torch.float32).contiguous()
+        W = W.reshape(cfg.Lout, cfg.Lin).to(device=y.device, dtype=torch.float32).resolve_neg().contiguous()
         d, c = cfg.dims(), cfg.constellation()
         lib = nat.lib()
         wsb = lib.amp_scamp_workspace_bytes(C.byref(d), cfg.N_Layers)

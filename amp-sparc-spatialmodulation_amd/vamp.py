@@ -21,10 +21,12 @@ from loss import Loss
 
 
 def _c64(t: torch.Tensor, shape) -> torch.Tensor:
+    """Contiguous complex64 view/copy with torch's lazy conjugate / negative bits materialised
+    (torch.linalg.svd on the GPU returns such views: the raw memory is NOT the value)."""
     t = t.reshape(shape)
     if t.dtype != torch.complex64:
         t = t.to(torch.complex64)
-    return t.contiguous()
+    return t.resolve_conj().resolve_neg().contiguous()
 
 
 _FUSED_DECIDE = os.environ.get('AMP_FUSED_DECIDE', '1') != '0'
@@ -58,7 +60,7 @@ class Tracker:
         n, k = U.shape[0], U.shape[1]
         N = Vh.shape[1]
         self.U = _c64(U, (n, k))
-        self.s = s.reshape(k).to(torch.float32).contiguous()
+        self.s = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
         self.Vh = _c64(Vh, (k, N))
         self.y = _c64(y, (B, n))
         self.noise_var = sigma2
@@ -146,7 +148,7 @@ def block_denoise(config: Config, s: torch.Tensor, tau, mode: int):
     if mode == 0:
         tau_s = float(tau.item() if isinstance(tau, torch.Tensor) else tau)
     else:
-        tv = tau.reshape(B, -1).to(torch.float32).contiguous()
+        tv = tau.reshape(B, -1).to(torch.float32).resolve_neg().contiguous()
         tau_p = nat.dptr(tv, torch.float32, 'tau')
     lib = nat.lib()
     wsb = lib.amp_block_denoise_workspace_bytes(C.byref(d))

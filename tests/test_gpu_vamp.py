@@ -350,3 +350,43 @@ def test_vamp_empty_batch_raises(device):
     with pytest.raises((OverflowError, nat.AmpError, ValueError, RuntimeError)):
         VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'][:0], inp['SNR'], inp['x'][:0], inp['sym'][:0],
                   inp['idx'][:0]).loss
+
+
+@pytest.mark.parametrize('ebn0', [2.0, 6.0])
+def test_model_device_rng_matches_host_statistically(device, ebn0, tmp_path):
+    """Throughput mode (Model(rng='device'): channel, messages, noise and SVD on the GPU) draws
+    different random streams from the reference's, so it is checked statistically: VER / SER of
+    4 epochs (4096 trials, 16384 sections) within 6 binomial sigma (+1e-3) of the parity mode."""
+    from model import Model
+    got = {}
+    for rng in ('host', 'device'):
+        cfg = _config(64, 4, 128, 1024, 'QPSK', iterations=20)
+        m = Model(cfg, 'vamp', path=str(tmp_path / rng), seed=11, rng=rng)
+        got[rng] = m.simulate(4, start=ebn0, final=ebn0)[-1]
+    for k, n in (('ser', 4 * 1024 * 4), ('ver', 4 * 1024)):
+        p = min(max(got['host'][k], 1e-3), 1 - 1e-3)
+        tol = 6 * np.sqrt(p * (1 - p) / n) + 1e-3
+        assert abs(got['device'][k] - got['host'][k]) <= tol, (k, got['device'][k], got['host'][k], tol)
+
+
+def test_vamp_accepts_lazy_conj_views(device):
+    """torch.linalg.svd on the GPU returns lazily conjugated / transposed views (the memory is not
+    the value).  The host mirror materialises them: the same results as with plain tensors; a raw
+    lazy view handed to amp_native.dptr raises instead of reading the wrong numbers."""
+    import amp_native as nat
+    from vamp import VAMP
+    cfg = _config(64, 4, 128, 256, 'QPSK', iterations=20)
+    inp = _regen_inputs(cfg, 2, 6.0)
+    V = inp['Vh'].mH.resolve_conj().contiguous()          # plain memory of V = Vh^H
+    Vh_lazy = V.mH                                         # a (possibly lazy) conjugate-transpose view
+    # a lazy view whenever torch makes one (ROCm builds may materialise); a transposed view always
+    assert Vh_lazy.is_conj() or not Vh_lazy.is_contiguous()
+    ref = VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    ref = {k: float(np.asarray(v)) for k, v in ref.loss.items()}
+    got = VAMP(cfg)(inp['U'], inp['s'], Vh_lazy, inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    got = {k: float(np.asarray(v)) for k, v in got.loss.items()}
+    assert got['T'] == ref['T'] and got['ser'] == ref['ser'] and got['ver'] == ref['ver'], (got, ref)
+    lazy = inp['Vh'].clone().conj()
+    if lazy.is_conj():
+        with pytest.raises(ValueError):
+            nat.dptr(lazy)
