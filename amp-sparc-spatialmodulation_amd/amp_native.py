@@ -92,6 +92,10 @@ SIGNATURES = {
     'amp_block_denoise_workspace_bytes': (C.c_size_t, [_D]),
     'amp_map_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
     'amp_map_decide_workspace_bytes': (C.c_size_t, [_D]),
+    'amp_shrink_bayes': (C.c_int, [_K, C.c_int64, _I, _P, C.c_float, _P, C.c_float, C.c_float, _P, _P]),
+    'amp_shrink_ook': (C.c_int, [C.c_int64, _I, _P, C.c_float, _P, C.c_float, _P, _P, _P, C.c_size_t, _P]),
+    'amp_shrink_ook_workspace_bytes': (C.c_size_t, [C.c_int64]),
+    'amp_shrink_sw_ook': (C.c_int, [C.c_int64, _I, _I, _P, C.c_float, _P, _P, _P, _P]),
     'amp_gemm_nt_f32': (C.c_int, [_P, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P]),
     'amp_build_cweight': (C.c_int, [_P, C.c_int64, C.c_int64, _I, _P, _I, _I, _P, _I, _I, _P]),
     'amp_last_error': (C.c_char_p, []),

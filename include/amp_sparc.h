@@ -210,6 +210,26 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
                          void* stream);
 size_t amp_map_decide_workspace_bytes(const amp_dims* d);
 
+/* ---- Element-wise shrinkage denoisers — replace Shrink (shrink.py:8-166).
+ * r: [count] complex64 (is_complex != 0) or float32; cov: cov_vec [count] float32, or
+ * cov_scalar when cov_vec is NULL (a 0-dim tensor in the reference).
+ * amp_shrink_bayes   Shrink.bayes (shrink.py:78-96): out [count], same dtype as r;
+ *                    P0, Ps = Config.P0 / Config.Ps as float32 (shrink.py:19).
+ * amp_shrink_ook     Shrink.shrinkOOK (shrink.py:139-157): exp_out [count] float32 and
+ *                    dxdr_out = one float32, der.mean() over all count elements;
+ *                    theta = float32 log(P0/Ps) (shrink.py:152).  count must be > 0.
+ * amp_shrink_sw_ook  Shrink.sw_shrinkOOK (shrink.py:58-76) over `sections` sections of M:
+ *                    exp_out [sections*M] complex64 (imaginary 0), var_out float32.
+ * Shrink.shrink / Shrink.lasso (shrink.py:98-137) raise for every input in the reference
+ * and have no entry point. */
+int amp_shrink_bayes(const amp_constellation* c, int64_t count, int32_t is_complex, const void* r, float cov_scalar,
+                     const void* cov_vec, float P0, float Ps, void* out, void* stream);
+int amp_shrink_ook(int64_t count, int32_t is_complex, const void* r, float cov_scalar, const void* cov_vec,
+                   float theta, void* exp_out, void* dxdr_out, void* ws, size_t ws_bytes, void* stream);
+size_t amp_shrink_ook_workspace_bytes(int64_t count);
+int amp_shrink_sw_ook(int64_t sections, int32_t M, int32_t is_complex, const void* r, float cov_scalar,
+                      const void* cov_vec, void* exp_out, void* var_out, void* stream);
+
 /* ---- Building blocks exposed for tests and tools ---- */
 /* C[rows][ldc] = A[rows][lda] . Wt[ncp][kap]^T on fp32 MFMA (first ka columns of A, first nc of C);
    Wt row-major, kap % 64 == 0, ncp % 128 == 0, lda % 4 == 0. */

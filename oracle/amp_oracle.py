@@ -413,6 +413,85 @@ def loss_dict(xmap, xmmse, x, symbols, indices, T: int, cfg: OracleConfig) -> di
     return out
 
 
+
+
+# ---------------------------------------------------------------------------
+# Shrink (shrink.py:8-166): element-wise prior-based denoisers.  float32 arithmetic in the
+# reference's op order; regularize_exp (shrink.py:163-166) compares against
+# float32(log(FLT_MAX)) and writes float32(log(FLT_MAX) - 1); regularize_zero (:159-161)
+# replaces exact zeros by float32(1e-9).
+SHR_REG_MAX = F32(np.log(np.finfo(np.float32).max))
+SHR_REG_SET = F32(np.log(np.finfo(np.float32).max) - 1)
+SHR_TOL = F32(1.0e-9)
+
+
+def _shr_reg_exp(a):
+    a = np.array(a, dtype=F32, copy=True)
+    a[a >= SHR_REG_MAX] = SHR_REG_SET
+    return a
+
+
+def _shr_abs(z):
+    """torch.abs: |z| of complex64 as float32 (correctly rounded hypot), |x| for float32."""
+    if np.iscomplexobj(z):
+        return np.hypot(z.real.astype(np.float64), z.imag.astype(np.float64)).astype(F32)
+    return np.abs(z).astype(F32)
+
+
+def shrink_bayes(r, cov, symbols, P0, Ps):
+    """Shrink.bayes (shrink.py:91-96) on r [..] (complex64 or float32), cov scalar or like r.
+    symbols: complex64 or float32 [K] (shrink.py:26); P0, Ps float32 (shrink.py:19)."""
+    r = np.asarray(r)
+    cov = np.asarray(cov, dtype=F32)
+    sym = np.asarray(symbols)
+    cplx = np.iscomplexobj(r) or np.iscomplexobj(sym)
+    if cplx:
+        r = r.astype(C64)
+        sym = sym.astype(C64)
+    else:
+        r = r.astype(F32)
+        sym = sym.astype(F32)
+    with np.errstate(all='ignore'):
+        covK = cov[..., None] if cov.ndim else cov
+        G0 = np.exp(-(_shr_abs(r) ** 2) / cov).astype(F32)
+        Gs = np.exp(-(_shr_abs(r[..., None] - sym) ** 2) / covK).astype(F32)   # [.., K]
+        norm = (F32(P0) * G0 + F32(Ps) * Gs.sum(axis=-1, dtype=F32)).astype(F32)
+        norm[norm == 0] = SHR_TOL
+        num = F32(Ps) * (sym * Gs).sum(axis=-1)
+        if cplx:
+            return (num.astype(C64) * (F32(1) / norm)).astype(C64)
+        return (num / norm).astype(F32)
+
+
+def shrink_ook(r, cov, theta):
+    """Shrink.shrinkOOK (shrink.py:152-157): (exp float32, dxdr float32 = der.mean())."""
+    rr = np.real(np.asarray(r)).astype(F32)
+    cov = np.asarray(cov, dtype=F32)
+    with np.errstate(all='ignore'):
+        eta = np.exp(_shr_reg_exp(F32(theta) + (F32(1) - F32(2) * rr) / cov)).astype(F32)
+        x = (F32(1) / ((F32(1) + eta) + SHR_TOL)).astype(F32)
+        der = ((F32(2) * eta) * (x * x) / cov).astype(F32)
+    der = np.nan_to_num(der, nan=0.0)
+    return x, F32(der.astype(np.float64).mean())
+
+
+def shrink_sw_ook(r, cov, B, L, M):
+    """Shrink.sw_shrinkOOK (shrink.py:68-76): leave-one-out OOK softmax per section of M.
+    Returns (exp complex64 [B, L*M], var float32 [B, L*M])."""
+    rr = np.real(np.asarray(r)).astype(F32)
+    cov = np.broadcast_to(np.asarray(cov, dtype=F32), rr.shape)
+    with np.errstate(all='ignore'):
+        Lr = _shr_reg_exp(((F32(2) * rr - F32(1)) / cov).reshape(B, L, M))   # in place in the reference
+        e = np.exp(Lr).astype(F32)
+        S = e.sum(axis=-1, keepdims=True, dtype=F32)
+        Le = (-np.log(S - e)).astype(F32)
+        eta = np.exp(_shr_reg_exp(Lr + Le)).astype(F32)
+        x = (eta / (F32(1) + eta)).astype(F32)
+        var = (x * (F32(1) - x)).astype(F32)
+    return x.reshape(B, L * M).astype(C64), var.reshape(B, L * M)
+
+
 __all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect',
            'bamp_detect', 'scamp_detect', 'map_decision', 'error_rates', 'loss_dict', 'allclose_f32',
-           'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX']
+           'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX',
+           'shrink_bayes', 'shrink_ook', 'shrink_sw_ook']

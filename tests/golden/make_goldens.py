@@ -17,6 +17,8 @@ Groups:
   g1  per-iteration traces at small shapes, inputs stored (VAMP, BAMP, SCAMP)
   g2  denoiser unit vectors (scalar tau, per-element tau, SCAMP mean-only, NaN onset)
   g3  MAP decision + all 14 metrics on crafted inputs (ties, 16QAM duplicate, NaN rows)
+  g5  Shrink element-wise denoisers (bayes, shrinkOOK, sw_shrinkOOK) on random inputs,
+      scalar and per-element cov, real and complex configs, overflow / NaN regimes
   g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
       by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
 
@@ -43,6 +45,7 @@ from loss import Loss        # noqa: E402
 import vamp as ref_vamp      # noqa: E402
 import bamp as ref_bamp      # noqa: E402
 import scamp as ref_scamp    # noqa: E402
+import shrink as ref_shrink  # noqa: E402
 
 torch.set_num_threads(int(os.environ.get('GOLDEN_THREADS', '8')))
 
@@ -269,6 +272,78 @@ def g3():
 
 
 # ---------------------------------------------------------------------------
+def g5():
+    """Shrink (shrink.py:8-166) outputs straight from the reference class."""
+    rng = np.random.default_rng(555)
+    flat = {}
+    n = 0
+    shapes = [(16, 2, 4), (64, 4, 8), (24, 2, 3), (256, 2, 2)]     # (Nt, Na, B): M = 8, 16, 12, 128
+    combos = [(a, True) for a in ['OOK', 'BPSK', '4ASK', 'QPSK', '8PSK', '16PSK', '16QAM']] + \
+             [(a, False) for a in ['OOK', 'BPSK', '4ASK']]
+    for alph, is_complex in combos:
+        for si, (Nt, Na, B) in enumerate(shapes):
+            cfg = Config(Nt, Na, 2 * Nt, 1, 1, batch=B, generator_mode='sparc', iterations=5, alphabet=alph,
+                         channel_profile='uniform', channel_truncation='tail', is_complex=is_complex, device='cpu')
+            covs = [1e-3, 0.05, 0.5, 3.0, 'vec'] if si < 2 else [0.2, 'vec']
+            for cv in covs:
+                # sparse truth (one active point per section) + noise
+                x = np.zeros((B, Nt), dtype=np.complex128)
+                M = Nt // Na
+                for b in range(B):
+                    for l in range(Na):
+                        x[b, l * M + rng.integers(M)] = cfg.symbols[rng.integers(cfg.K)]
+                sd = 0.3 if cv == 'vec' else float(np.sqrt(max(cv, 1e-2)))
+                noise = rng.standard_normal((B, Nt)) + (1j * rng.standard_normal((B, Nt)) if is_complex else 0)
+                r = (x + sd * noise)
+                r = r.astype(np.complex64) if is_complex else r.real.astype(np.float32)
+                if cv == 'vec':
+                    cov = ((np.abs(rng.standard_normal((B, Nt))) + 0.05) * 0.3).astype(np.float32)
+                    cov_t = torch.from_numpy(cov).view(B, Nt, 1)
+                else:
+                    cov = np.array(np.float32(cv))
+                    cov_t = torch.tensor(np.float32(cv))
+                rt = torch.from_numpy(r).view(B, Nt, 1)
+                S = ref_shrink.Shrink(cfg, 'bayes')
+                xb = S(rt.clone(), cov_t.clone())
+                So = ref_shrink.Shrink(cfg, 'shrinkOOK')
+                xo, do = So(rt.clone(), cov_t.clone())
+                xs, vs = So.sw_shrinkOOK(rt.clone(), cov_t.clone())
+                key = f'case{n}'
+                flat.update({f'{key}/alphabet': np.array(alph), f'{key}/is_complex': np.array(int(is_complex)),
+                             f'{key}/dims': np.array([Nt, Na, B]), f'{key}/r': r, f'{key}/cov': cov,
+                             f'{key}/bayes': c(xb), f'{key}/ook_x': c(xo), f'{key}/ook_dxdr': c(do),
+                             f'{key}/sw_x': c(xs), f'{key}/sw_var': c(vs)})
+                n += 1
+    # overflow regimes: logits at / above log(FLT_MAX) (regularize_exp), leave-one-out sums
+    # that overflow to inf (sw: inf - inf = NaN) and a section whose only large logit wins
+    for alph in ['OOK', 'QPSK']:
+        Nt, Na, B = 16, 2, 2
+        cfg = Config(Nt, Na, 2 * Nt, 1, 1, batch=B, generator_mode='sparc', iterations=5, alphabet=alph,
+                     channel_profile='uniform', channel_truncation='tail', device='cpu')
+        for cv in [1e-2, 5e-3, 1e-4]:
+            r = (0.5 + 0.1 * rng.standard_normal((B, Nt))).astype(np.complex64)
+            r[0, 2] = 1.0
+            r[0, 9] = 1.5
+            r[0, 10] = 1.5
+            r[1, :8] = 2.0
+            rt = torch.from_numpy(r).view(B, Nt, 1)
+            cov_t = torch.tensor(np.float32(cv))
+            xb = ref_shrink.Shrink(cfg, 'bayes')(rt.clone(), cov_t.clone())
+            So = ref_shrink.Shrink(cfg, 'shrinkOOK')
+            xo, do = So(rt.clone(), cov_t.clone())
+            xs, vs = So.sw_shrinkOOK(rt.clone(), cov_t.clone())
+            key = f'case{n}'
+            flat.update({f'{key}/alphabet': np.array(alph), f'{key}/is_complex': np.array(1),
+                         f'{key}/dims': np.array([Nt, Na, B]), f'{key}/r': r, f'{key}/cov': np.array(np.float32(cv)),
+                         f'{key}/bayes': c(xb), f'{key}/ook_x': c(xo), f'{key}/ook_dxdr': c(do),
+                         f'{key}/sw_x': c(xs), f'{key}/sw_var': c(vs), f'{key}/overflow': np.array(1)})
+            n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g5_shrink.npz'), **flat)
+    print('g5 cases', n)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
@@ -319,7 +394,7 @@ def g4(names=None):
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5']
     names = [w for w in which if w.startswith('cfg')]
     for w in which:
         if w == 'g1':
@@ -328,5 +403,7 @@ if __name__ == '__main__':
             g2()
         elif w == 'g3':
             g3()
+        elif w == 'g5':
+            g5()
         elif w == 'g4':
             g4(names or None)
