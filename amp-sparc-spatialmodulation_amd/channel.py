@@ -91,6 +91,27 @@ class Channel:
         Wt = torch.tensor(W, dtype=torch.float32, device=self.device)
         return Wt, A.to(self.dtype)
 
+    def generate_correlated(self, rho: float = 0.5) -> torch.Tensor:
+        """Kronecker exponentially-correlated Rayleigh channel A = L_r G L_t^T, [Nr, Nt] complex64.
+
+        Not in the reference (its 'random' profile has no pdp and crashes, channel.py:27-31, and
+        there is no correlated model); BASELINE cfg5 names it, so this build defines it:
+        G ~ CN(0, 1/Nr) i.i.d. (the reference's entry variance for Lin = Lh = 1, channel.py:85-91),
+        R_r[i,j] = R_t[i,j] = rho^|i-j|, and L the Cholesky factor of R, which for the exponential
+        model is the AR(1) filter x_0 = g_0, x_i = rho x_{i-1} + sqrt(1 - rho^2) g_i.  Applied as
+        elementwise recursions in float64 (no BLAS: bit-reproducible on every host).  Draws
+        np.random.normal twice (real, imaginary parts), like generate_as_sparc."""
+        assert self.Lin == 1 and self.Lh == 1, 'correlated channel: Lin = Lh = 1 only'
+        gr = np.random.normal(size=(self.Nr, self.Nt))
+        gi = np.random.normal(size=(self.Nr, self.Nt))
+        A = (gr + 1j * gi) / np.sqrt(2 * self.Nr)
+        c = np.sqrt(1.0 - rho * rho)
+        for i in range(1, self.Nr):                    # receive side: rows
+            A[i] = rho * A[i - 1] + c * A[i]
+        for j in range(1, self.Nt):                    # transmit side: columns
+            A[:, j] = rho * A[:, j - 1] + c * A[:, j]
+        return torch.tensor(A.astype(np.complex64), dtype=self.dtype, device=self.device)
+
     def generate_channel(self) -> torch.Tensor:
         """Block-Toeplitz MIMO-ISI channel with trunc/tail/cyclic edges (channel.py:40-73)."""
         hr = np.random.normal(size=(self.Nr, self.Nt, self.Lh))

@@ -19,6 +19,9 @@ Groups:
   g3  MAP decision + all 14 metrics on crafted inputs (ties, 16QAM duplicate, NaN rows)
   g5  Shrink element-wise denoisers (bayes, shrinkOOK, sw_shrinkOOK) on random inputs,
       scalar and per-element cov, real and complex configs, overflow / NaN regimes
+  g6  BASELINE cfg5 shape (BAMP Nt=512 Nr=1024 Na=16) on the build-defined Kronecker
+      exponentially-correlated channel (rho = 0.5, injected into the reference's BAMP, which
+      takes any H), 16-QAM and QPSK twins of cfg5's 64-QAM (which Config rejects), B = 1024
   g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
       by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
 
@@ -344,6 +347,58 @@ def g5():
 
 
 # ---------------------------------------------------------------------------
+def correlated_channel(Nr, Nt, rho):
+    """Same recursion as the build's Channel.generate_correlated (its SHA is checked by the
+    tests): G ~ CN(0, 1/Nr), AR(1) filter over rows then columns, float64, then complex64."""
+    gr = np.random.normal(size=(Nr, Nt))
+    gi = np.random.normal(size=(Nr, Nt))
+    A = (gr + 1j * gi) / np.sqrt(2 * Nr)
+    c = np.sqrt(1.0 - rho * rho)
+    for i in range(1, Nr):
+        A[i] = rho * A[i - 1] + c * A[i]
+    for j in range(1, Nt):
+        A[:, j] = rho * A[:, j - 1] + c * A[:, j]
+    return torch.tensor(A.astype(np.complex64))
+
+
+G6_CONFIGS = {
+    'cfg5_bamp_corr_16qam': (512, 16, 1024, 1024, '16QAM', 20, [6, 10, 14, 18], [0]),
+    'cfg5_bamp_corr_qpsk': (512, 16, 1024, 1024, 'QPSK', 20, [2, 6, 10, 14], [0]),
+}
+
+
+def g6():
+    path = os.path.join(HERE, 'g6_cfg5_corr.json')
+    db = {}
+    rho = 0.5
+    for name, (Nt, Na, Nr, B, alph, iters, grid, seeds) in G6_CONFIGS.items():
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = {'algo': 'bamp', 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': B, 'alphabet': alph, 'iterations': iters,
+               'rho': rho, 'points': {}}
+        for seed in seeds:
+            for EbN0 in grid:
+                t0 = time.time()
+                np.random.seed(seed)
+                torch.manual_seed(seed)
+                ch, da = Channel(cfg), Data(cfg)
+                A = correlated_channel(Nr, Nt, rho)
+                x, sym, idx = da.generate_message()
+                SNR = snr_of(cfg, float(EbN0))
+                y = A @ x + ch.awgn(SNR)
+                L = ref_bamp.BAMP(cfg)(A, y, SNR, x, sym, idx)
+                rec = loss_to_json(L.loss)
+                rec['sha_A'] = sha(A)
+                rec['sha_x'] = sha(x)
+                rec['y_abs2_sum'] = float(np.sum(np.abs(y.numpy().astype(np.complex128)) ** 2))
+                ent['points'][f'{seed}/{EbN0}'] = rec
+                print(name, seed, EbN0, 'T=', rec['T'], 'ver=', rec['ver'], 'ser=', rec['ser'],
+                      f'{time.time() - t0:.1f}s', flush=True)
+        db[name] = ent
+    with open(path, 'w') as f:
+        json.dump(db, f, indent=1, sort_keys=True)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
@@ -394,7 +449,7 @@ def g4(names=None):
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6']
     names = [w for w in which if w.startswith('cfg')]
     for w in which:
         if w == 'g1':
@@ -403,6 +458,8 @@ if __name__ == '__main__':
             g2()
         elif w == 'g3':
             g3()
+        elif w == 'g6':
+            g6()
         elif w == 'g5':
             g5()
         elif w == 'g4':
