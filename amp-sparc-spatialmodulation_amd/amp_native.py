@@ -91,6 +91,7 @@ SIGNATURES = {
     'amp_block_denoise': (C.c_int, [_D, _K, _P, _I, C.c_float, _P, _P, _P, _P, C.c_size_t, _P]),
     'amp_block_denoise_workspace_bytes': (C.c_size_t, [_D]),
     'amp_map_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
+    'amp_segmented_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
     'amp_map_decide_workspace_bytes': (C.c_size_t, [_D]),
     'amp_shrink_bayes': (C.c_int, [_K, C.c_int64, _I, _P, C.c_float, _P, C.c_float, C.c_float, _P, _P]),
     'amp_shrink_ook': (C.c_int, [C.c_int64, _I, _P, C.c_float, _P, C.c_float, _P, _P, _P, C.c_size_t, _P]),

@@ -64,6 +64,77 @@ __device__ __forceinline__ T dec_group_reduce(T v, OP op) {
     return v;
 }
 
+// The decided section's xhat (a_k at position m, 0 elsewhere; bi = m * K + k) against the truth:
+// mismatch flag (loss.py:133) and float64 sum |xmmse - x|^2 (loss.py:116), group-reduced.
+template <int KK, int G, class LD>
+__device__ __forceinline__ void section_tail(const DecConst& c, int M, int g, const LD& ld, int bi, int& bi_out,
+                                             int& mm_out, double& se_out) {
+    constexpr int K = KK;
+    const int mh = bi / K, kh = bi - mh * K;
+    float ar = 0.f, ai = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (k == kh) { ar = c.re32[k]; ai = c.im32[k]; }
+    int mm = 0;
+    double se = 0.0;
+    for (int m = g; m < M; m += G) {
+        float2 xv, xt, xe;
+        ld(m, xv, xt, xe);
+        const float hr = (m == mh) ? ar : 0.f, hi = (m == mh) ? ai : 0.f;
+        mm |= (hr - xt.x != 0.f || hi - xt.y != 0.f) ? 1 : 0;
+        const float dr = xe.x - xt.x, di = xe.y - xt.y;
+        se += (double)dr * dr + (double)di * di;
+    }
+    mm = dec_group_reduce<G>(mm, [](int a, int b) { return a | b; });
+    se = dec_group_reduce<G>(se, [](double a, double b) { return a + b; });
+    bi_out = bi;
+    mm_out = mm;
+    se_out = se;
+}
+
+// Segmented decision (Loss.segmented_decision, loss.py:222-250; generator_mode='segmented'):
+// per section, the position of the largest |x_m| (np.abs of complex64 = float32 hypot;
+// np.argsort()[-1]: NaN sorts last; among exactly equal magnitudes numpy's SIMD quicksort order
+// is implementation-defined, and this kernel takes the last such position),
+// then the nearest constellation point |x_m - a_k| in float64 (strict <: first minimum).  A
+// NaN x_m has no nearest point in the reference (its section stays empty and the counting
+// arrays no longer line up); here it decides k = 0.
+template <int KK, int G, class LD>
+__device__ __forceinline__ void decide_section_seg(const DecConst& c, int M, int g, const LD& ld, int& bi_out,
+                                                   int& mm_out, double& se_out) {
+    constexpr int K = KK;
+    float bv = -1.f;
+    int bm = -1;
+    bool bn = false;
+    for (int m = g; m < M; m += G) {
+        float2 xv, xt, xe;
+        ld(m, xv, xt, xe);
+        const float a = hypotf(xv.x, xv.y);
+        const bool an = a != a;
+        // (a, m) beats (bv, bm): NaN largest, then larger value, then larger index
+        const bool win = an ? (!bn || m > bm) : (!bn && (a > bv || (a == bv && m > bm)));
+        if (win) { bv = a; bm = m; bn = an; }
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int om = __shfl_xor(bm, o, 64);
+        const bool on = __shfl_xor((int)bn, o, 64) != 0;
+        const bool win = on ? (!bn || om > bm) : (!bn && (ov > bv || (ov == bv && om > bm)));
+        if (win) { bv = ov; bm = om; bn = on; }
+    }
+    float2 xs, xt, xe;
+    ld(bm, xs, xt, xe);
+    double d = INFINITY;
+    int kh = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double ds = hypot((double)xs.x - c.re[k], (double)xs.y - c.im[k]);
+        if (ds < d) { d = ds; kh = k; }
+    }
+    section_tail<KK, G>(c, M, g, ld, bm * K + kh, bi_out, mm_out, se_out);
+}
+
 // One section decided by a group of G lanes (g = lane in group; lane g owns positions
 // g, g + G, ...).  ld(m, xmap, x, xmmse) loads position m of the section.  Every lane of the
 // group returns the decision bi = m * K + k, the mismatch flag (xhat != x anywhere in the
@@ -144,26 +215,7 @@ __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, 
             if (dec_better(ov, oi, on, bv, bi, bn)) { bv = ov; bi = oi; bn = on; }
         }
     }
-    const int mh = bi / K, kh = bi - mh * K;
-    float ar = 0.f, ai = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (k == kh) { ar = c.re32[k]; ai = c.im32[k]; }
-    int mm = 0;
-    double se = 0.0;
-    for (int m = g; m < M; m += G) {
-        float2 xv, xt, xe;
-        ld(m, xv, xt, xe);
-        const float hr = (m == mh) ? ar : 0.f, hi = (m == mh) ? ai : 0.f;
-        mm |= (hr - xt.x != 0.f || hi - xt.y != 0.f) ? 1 : 0;
-        const float dr = xe.x - xt.x, di = xe.y - xt.y;
-        se += (double)dr * dr + (double)di * di;
-    }
-    mm = dec_group_reduce<G>(mm, [](int a, int b) { return a | b; });
-    se = dec_group_reduce<G>(se, [](double a, double b) { return a + b; });
-    bi_out = bi;
-    mm_out = mm;
-    se_out = se;
+    section_tail<KK, G>(c, M, g, ld, bi, bi_out, mm_out, se_out);
 }
 
 // Counter contributions of one decided section s (global section index b * L + l).

@@ -31,6 +31,7 @@ struct DecK {
     DecPart* parts;
     int nblk;
     amp_counts* out;
+    int rule;            // 0: MAP (sparc), 1: segmented
     DecConst c;
 };
 
@@ -53,7 +54,10 @@ __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
         };
         int bi, mm;
         double se;
-        decide_section<KK, G, false>(P.c, M, g, ld, bi, mm, se);
+        if (P.rule == 1)
+            decide_section_seg<KK, G>(P.c, M, g, ld, bi, mm, se);
+        else
+            decide_section<KK, G, false>(P.c, M, g, ld, bi, mm, se);
         if (act && g == 0) {
             P.mism[s] = (unsigned char)mm;
             if (P.dec) P.dec[s] = bi;
@@ -174,9 +178,9 @@ size_t amp_map_decide_workspace_bytes(const amp_dims* d) {
     return cv.off;
 }
 
-int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
-                         const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
-                         void* decisions, void* ws, size_t ws_bytes, void* stream) {
+static int decide_count(int rule, const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
+                        const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
+                        void* decisions, void* ws, size_t ws_bytes, void* stream) {
     int rc = check_dims(d, c, false);
     if (rc) return rc;
     AMP_REQUIRE(xmap && xmmse && x && sym && idx && counts && ws, "amp_map_decide_count: null pointer argument");
@@ -194,12 +198,25 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
     P.out = (amp_counts*)counts;
     P.dec = (int*)decisions;
     P.c = to_decconst(c);
+    P.rule = rule;
     hipStream_t st = (hipStream_t)stream;
     launch_decide(P, d->M, st);
     AMP_LAUNCH_CHECK("map_decide");
     hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(1024), 0, st, P);
     AMP_LAUNCH_CHECK("map_count");
     return AMP_OK;
+}
+
+int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
+                         const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
+                         void* decisions, void* ws, size_t ws_bytes, void* stream) {
+    return decide_count(0, d, c, xmap, xmmse, x, sym, idx, ibits_trunc, counts, decisions, ws, ws_bytes, stream);
+}
+
+int amp_segmented_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
+                               const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
+                               void* decisions, void* ws, size_t ws_bytes, void* stream) {
+    return decide_count(1, d, c, xmap, xmmse, x, sym, idx, ibits_trunc, counts, decisions, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

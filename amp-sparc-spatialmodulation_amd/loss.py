@@ -52,12 +52,9 @@ class Loss:
         self.loss = {'T': 0}
         self.keys = list(KEYS)
         self.dtype = torch.complex64 if config.is_complex else torch.float32
-        if config.mode != 'sparc':
-            # loss.py:232, 261 reshape without the batch dimension and only work for B = 1;
-            # the native decision implements the MAP rule of 'sparc' (SURVEY.md fact 4).
-            self.decision_mode = config.mode
-        else:
-            self.decision_mode = 'sparc'
+        # loss.py:38-43: 'sparc' -> MAP_decision, 'segmented' -> segmented_decision (both native);
+        # 'random' -> random_decision (not built: the reference's random-mode VAMP crashes).
+        self.decision_mode = config.mode
         self._const = None
         self._dims = None
 
@@ -88,20 +85,27 @@ class Loss:
         return self._dims, self._const
 
     def device_counts(self, xmap, xmmse, x, symbols, indices, decisions: torch.Tensor | None = None,
-                      out: torch.Tensor | None = None):
+                      out: torch.Tensor | None = None, rule: str | None = None):
         """Launch the decision/count kernels; returns the device amp_counts buffer (async).
         ``out``: optional uint8 device buffer (>= sizeof(amp_counts)) to write the counters to."""
-        if self.decision_mode != 'sparc':
-            raise NotImplementedError("native decision implements generator_mode='sparc' (loss.py:282-302)")
+        rule = rule or self.decision_mode
+        if rule not in ('sparc', 'segmented'):
+            raise NotImplementedError("native decisions implement generator_mode 'sparc' and 'segmented' "
+                                      "(loss.py:222-250, 282-302)")
         d, c = self._native()
         dev = xmap.device
         B = self.B
+        L = self.Na * self.Lin
+        M = self.Nt // self.Na
+        if rule == 'segmented' and B != 1:
+            # loss.py:232 reshapes the whole batch to (Na*Lin, M): numpy raises for B > 1
+            raise ValueError(f'cannot reshape array of size {B * L * M} into shape ({L},{M})')
         xmap = _flat_c64(xmap, B, 'xmap')
         xmmse = _flat_c64(xmmse, B, 'xmmse')
         x = _flat_c64(x, B, 'x')
         sym = _as_device_labels(symbols, dev)
         idx = _as_device_labels(indices, dev)
-        S = B * self.config.L
+        S = B * L
         if sym.numel() != S or idx.numel() != S:
             raise ValueError(f'expected {S} labels/indices, got {sym.numel()}/{idx.numel()}')
         lib = nat.lib()
@@ -109,11 +113,11 @@ class Loss:
         ws = nat.WORKSPACE.get(dev, 'decide', wsb)
         counts = out if out is not None else nat.WORKSPACE.get(dev, 'counts', C.sizeof(nat.AmpCounts))
         dec_ptr = nat.dptr(decisions, torch.int32, 'decisions') if decisions is not None else None
-        nat.check(lib.amp_map_decide_count(C.byref(d), C.byref(c), nat.dptr(xmap, name='xmap'),
-                                           nat.dptr(xmmse, name='xmmse'), nat.dptr(x, name='x'),
-                                           nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices'),
-                                           self._ibits, nat.dptr(counts), dec_ptr, nat.dptr(ws), wsb,
-                                           nat.stream_ptr(dev)), 'amp_map_decide_count')
+        fn = lib.amp_map_decide_count if rule == 'sparc' else lib.amp_segmented_decide_count
+        nat.check(fn(C.byref(d), C.byref(c), nat.dptr(xmap, name='xmap'), nat.dptr(xmmse, name='xmmse'),
+                     nat.dptr(x, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices'),
+                     self._ibits, nat.dptr(counts), dec_ptr, nat.dptr(ws), wsb, nat.stream_ptr(dev)),
+                  f'{rule} decide_count')
         return counts
 
     def decide_args(self, x, symbols, indices, out: torch.Tensor) -> nat.AmpVampDecideArgs:
@@ -184,16 +188,27 @@ class Loss:
 
     def MAP_decision(self, xamp: torch.Tensor):
         """(xhat, gray labels, flat indices) of loss.py:282-302, decided on the GPU."""
+        return self._decide(xamp, 'sparc')
+
+    def segmented_decision(self, xamp: torch.Tensor):
+        """(xhat, gray labels, flat indices) of loss.py:222-250, decided on the GPU (B = 1)."""
+        return self._decide(xamp, 'segmented')
+
+    def decision(self, xamp: torch.Tensor):
+        """The mode's decision (loss.py:38-43)."""
+        return self._decide(xamp, self.decision_mode)
+
+    def _decide(self, xamp: torch.Tensor, rule: str):
         d, c = self._native()
         B = self.B
         xamp = _flat_c64(xamp, B, 'xamp')
-        S = B * self.config.L
+        S = B * self.Na * self.Lin
         dec = torch.empty(S, dtype=torch.int32, device=xamp.device)
         zeros = torch.zeros(S, dtype=torch.int64, device=xamp.device)
-        self.device_counts(xamp, xamp, xamp, zeros, zeros, decisions=dec)
+        self.device_counts(xamp, xamp, xamp, zeros, zeros, decisions=dec, rule=rule)
         f = dec.cpu().numpy().astype(np.int64)
         m_hat, k_hat = np.divmod(f, self.config.K)
-        M = self.config.M
+        M = self.Nt // self.Na
         xhat = np.zeros((S, M), dtype=np.complex64)
         xhat[np.arange(S), m_hat] = np.asarray(self.symbols)[k_hat]
         index = np.arange(S) * M + m_hat

@@ -206,7 +206,7 @@ class VAMP(nn.Module):
         T.res = res
         T.args.status = nat.dptr(res)
         lib = nat.lib()
-        fused = (_FUSED_DECIDE and
+        fused = (_FUSED_DECIDE and self.L.decision_mode == 'sparc' and
                  lib.amp_vamp_select_engine(C.byref(T.dims), T.k, self.engine) == nat.ENGINE_PERSISTENT)
         if fused:
             # forward + decision on T.r (vamp.py:187) + counters in one launch sequence

@@ -209,6 +209,14 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
                          int32_t ibits_trunc, void* counts, void* decisions, void* ws, size_t ws_bytes,
                          void* stream);
 size_t amp_map_decide_workspace_bytes(const amp_dims* d);
+/* Same counters with Loss.segmented_decision (loss.py:222-250, generator_mode='segmented'):
+ * per section the largest |x_m| (last index on ties, NaN largest), then the nearest point
+ * |x_m - a_k| (first minimum).  The reference only runs it for B = 1 (its reshape drops the
+ * batch axis); this entry point takes any B.  Same arguments and workspace as above. */
+int amp_segmented_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap,
+                               const void* xmmse, const void* x, const void* sym, const void* idx,
+                               int32_t ibits_trunc, void* counts, void* decisions, void* ws,
+                               size_t ws_bytes, void* stream);
 
 /* ---- Element-wise shrinkage denoisers — replace Shrink (shrink.py:8-166).
  * r: [count] complex64 (is_complex != 0) or float32; cov: cov_vec [count] float32, or

@@ -359,6 +359,24 @@ def map_decision(xmap: np.ndarray, cfg: OracleConfig):
     return xhat.ravel(), gray, index
 
 
+def segmented_decision(xmap: np.ndarray, cfg: OracleConfig):
+    """Loss.segmented_decision (loss.py:222-250): per section of M, the position of the largest
+    |x| (np.argsort()[-1] on float32 magnitudes: NaN sorts last), then the nearest constellation point (float64 |x - a_k|, first minimum).
+    Returns (xhat c64 [S*M], gray labels, flat indices) like map_decision."""
+    xa = np.asarray(xmap).reshape(-1, cfg.M)
+    sym = cfg.symbols.astype(np.complex128)
+    S = xa.shape[0]
+    mag = np.abs(xa.astype(np.complex64))
+    # numpy's own argsort, as loss.py:236: among exactly equal magnitudes its (SIMD quicksort)
+    # order is implementation-defined, so the oracle defers to it rather than restating it
+    m_hat = np.array([row.argsort()[-1] for row in mag], dtype=np.int64)
+    xs = xa[np.arange(S), m_hat].astype(np.complex128)
+    k_hat = np.abs(xs[:, None] - sym[None, :]).argmin(axis=1)
+    xhat = np.zeros_like(xa)
+    xhat[np.arange(S), m_hat] = sym[k_hat]
+    return xhat.ravel(), np.asarray(cfg.gray)[k_hat], np.arange(S) * cfg.M + m_hat
+
+
 def _de2bi_count(v: np.ndarray, bits: int) -> int:
     """count_nonzero(de2bi(v, bits)) (loss.py:181-196): set bits among the low `bits` bits."""
     v = v.astype(np.int64) & ((1 << bits) - 1)
@@ -372,7 +390,8 @@ def error_rates(xmap, xmmse, x, symbols, indices, cfg: OracleConfig):
     xmap = np.asarray(xmap).reshape(-1, Lin, Nt)
     xmmse = np.asarray(xmmse).reshape(-1, Lin, Nt)
     x = np.asarray(x).reshape(-1, Lin, Nt)
-    xhat, shat, ihat = map_decision(xmap, cfg)
+    decide = segmented_decision if cfg.mode == 'segmented' else map_decision    # loss.py:38-43
+    xhat, shat, ihat = decide(xmap, cfg)
     xhat = xhat.reshape((-1, Lin, Nt))
     # loss.py:116-119
     nMSE = np.sum(np.abs(xmmse - x) ** 2) / cfg.Ns
@@ -494,4 +513,4 @@ def shrink_sw_ook(r, cov, B, L, M):
 __all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect',
            'bamp_detect', 'scamp_detect', 'map_decision', 'error_rates', 'loss_dict', 'allclose_f32',
            'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX',
-           'shrink_bayes', 'shrink_ook', 'shrink_sw_ook']
+           'shrink_bayes', 'shrink_ook', 'shrink_sw_ook', 'segmented_decision']

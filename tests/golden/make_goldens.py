@@ -22,6 +22,8 @@ Groups:
   g6  BASELINE cfg5 shape (BAMP Nt=512 Nr=1024 Na=16) on the build-defined Kronecker
       exponentially-correlated channel (rho = 0.5, injected into the reference's BAMP, which
       takes any H), 16-QAM and QPSK twins of cfg5's 64-QAM (which Config rejects), B = 1024
+  g7  generator_mode='segmented' (B = 1): Loss.segmented_decision on crafted inputs (ties,
+      zero rows, the 16-QAM duplicate point) and VAMP / BAMP Loss dicts along EbN0
   g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
       by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
 
@@ -399,6 +401,73 @@ def g6():
 
 
 # ---------------------------------------------------------------------------
+def g7():
+    """generator_mode='segmented' at B = 1 (the only batch its decision reshape accepts)."""
+    rng = np.random.default_rng(77)
+    flat = {}
+    n = 0
+    for alph in ['QPSK', '16QAM', 'BPSK', '8PSK', 'OOK']:
+        for (Nt, Na, Nr, Lin, Lh) in [(16, 2, 32, 1, 1), (64, 4, 32, 3, 2), (128, 2, 64, 1, 1)]:
+            cfg = Config(Nt, Na, Nr, Lin, Lh, batch=1, generator_mode='segmented', iterations=5, alphabet=alph,
+                         channel_profile='uniform', channel_truncation='tail', device='cpu')
+            np.random.seed(n)
+            x, sym, idx = Data(cfg).generate_message()
+            xv = c(x).reshape(1, -1)
+            for variant in ['noisy', 'ties', 'zeros', 'exact']:
+                if variant == 'noisy':
+                    xmap = xv + (rng.standard_normal(xv.shape) + 1j * rng.standard_normal(xv.shape)).astype(np.complex64) * 0.4
+                elif variant == 'ties':
+                    xmap = xv.copy()
+                    xmap[0, 1::3] = xmap[0, 1::3] + np.complex64(1.0)    # repeated magnitudes inside sections
+                    xmap[0, ::5] = np.complex64(1.0 + 0j)
+                elif variant == 'zeros':
+                    xmap = np.zeros_like(xv)                              # every |x| equal -> last position
+                    xmap[0, :Nt // Na] = xv[0, :Nt // Na]
+                else:
+                    xmap = xv.copy()
+                xmap = xmap.astype(np.complex64)
+                xmmse = (xv + rng.standard_normal(xv.shape).astype(np.float32) * 0.1).astype(np.complex64)
+                L = Loss(cfg)
+                L(torch.from_numpy(xmap).view(1, -1, 1), torch.from_numpy(xmmse).view(1, -1, 1), x, sym, idx, 3)
+                dec = L.decision(xmap.reshape(-1, cfg.Lin, cfg.Nt))
+                key = f'case{n}'
+                flat.update({f'{key}/alphabet': np.array(alph), f'{key}/dims': np.array([Nt, Na, Nr, 1, Lin, Lh]),
+                             f'{key}/xmap': xmap, f'{key}/xmmse': xmmse, f'{key}/x': xv,
+                             f'{key}/sym': sym, f'{key}/idx': idx,
+                             f'{key}/xhat': dec[0], f'{key}/shat': dec[1], f'{key}/ihat': dec[2],
+                             f'{key}/loss': np.array(json.dumps(loss_to_json(L.loss)))})
+                n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g7_segmented.npz'), **flat)
+    print('g7 decision cases', n)
+    # detectors end to end (B = 1, one epoch per seed, the reference's call order)
+    curves = {}
+    for algo in ['vamp', 'bamp']:
+        for alph in ['QPSK', '16QAM']:
+            Nt, Na, Nr = 32, 4, 64
+            cfg = Config(Nt, Na, Nr, 1, 1, batch=1, generator_mode='segmented', iterations=20, alphabet=alph,
+                         channel_profile='uniform', channel_truncation='tail', device='cpu')
+            pts = {}
+            for EbN0 in [0, 4, 8, 12, 16]:
+                for seed in range(6):
+                    inp = gen_inputs(cfg, seed, float(EbN0), svd=(algo == 'vamp'))
+                    if algo == 'vamp':
+                        L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'],
+                                               inp['sym'], inp['idx'])
+                    else:
+                        L = ref_bamp.BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                    rec = loss_to_json(L.loss)
+                    rec['sha_A'] = sha(inp['A'])
+                    rec['sha_x'] = sha(inp['x'])
+                    pts[f'{seed}/{EbN0}'] = rec
+            curves[f'seg_{algo}_{alph}'] = {'algo': algo, 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': 1, 'alphabet': alph,
+                                            'iterations': 20, 'points': pts}
+            print('g7', algo, alph, 'ver', [round(p['ver'], 2) for p in pts.values()][:10])
+    with open(os.path.join(HERE, 'g7_segmented_curves.json'), 'w') as f:
+        json.dump(curves, f, indent=1, sort_keys=True)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
@@ -449,7 +518,7 @@ def g4(names=None):
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7']
     names = [w for w in which if w.startswith('cfg')]
     for w in which:
         if w == 'g1':
@@ -458,6 +527,8 @@ if __name__ == '__main__':
             g2()
         elif w == 'g3':
             g3()
+        elif w == 'g7':
+            g7()
         elif w == 'g6':
             g6()
         elif w == 'g5':
