@@ -57,9 +57,10 @@ class AmpVampDecideArgs(C.Structure):
 
 
 class AmpBampArgs(C.Structure):
-    _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('pad', C.c_int32),
+    _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('denoiser', C.c_int32),
                 ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p),
-                ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
+                ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t),
+                ('P0', C.c_float), ('Ps', C.c_float)]
 
 
 class AmpScampArgs(C.Structure):
@@ -92,6 +93,7 @@ SIGNATURES = {
     'amp_block_denoise_workspace_bytes': (C.c_size_t, [_D]),
     'amp_map_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
     'amp_segmented_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
+    'amp_random_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
     'amp_map_decide_workspace_bytes': (C.c_size_t, [_D]),
     'amp_shrink_bayes': (C.c_int, [_K, C.c_int64, _I, _P, C.c_float, _P, C.c_float, C.c_float, _P, _P]),
     'amp_shrink_ook': (C.c_int, [C.c_int64, _I, _P, C.c_float, _P, C.c_float, _P, _P, _P, C.c_size_t, _P]),

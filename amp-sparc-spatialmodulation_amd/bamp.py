@@ -65,6 +65,9 @@ class BAMP(nn.Module):
         a.H, a.y = nat.dptr(H, name='H'), nat.dptr(y, name='y')
         a.max_iter = cfg.N_Layers
         a.noise_var = float(self.E / SNR)                                 # bamp.py:124
+        # bamp.py:38-41: 'random' mode denoises element-wise (random_denoiser, bamp.py:79-88)
+        a.denoiser = 1 if cfg.mode == 'random' else 0
+        a.P0, a.Ps = float(np.float32(cfg.P0)), float(np.float32(cfg.Ps))
         a.xmap, a.xmmse, a.var = nat.dptr(self.xmap), nat.dptr(self.xmmse), nat.dptr(self.var)
         a.status = nat.dptr(self.res)
         a.ws, a.ws_bytes = nat.dptr(self.ws), self.ws.numel()

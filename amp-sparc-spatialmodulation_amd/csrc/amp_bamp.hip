@@ -48,7 +48,38 @@ struct BampK {
     BampIter* iters;       // [max_iter + 1]
     amp_status* status;
     Const c;
+    int elementwise;                       // random_denoiser (bamp.py:79-88) instead of the block one
+    float P0, Ps;
+    double sre[AMP_MAX_K], sim[AMP_MAX_K]; // torch.tensor(config.symbols): complex128 (bamp.py:37)
 };
+
+// BAMPLayer.random_denoiser (bamp.py:79-88) for one entry, in the reference's dtypes: G(0) in
+// float32 (r - 0 stays complex64), G(a_k) in float64 (complex64 - complex128), norm / exp / var
+// in float64 (the float32 prior scalars promoted), complex128 / float64 as a reciprocal multiply.
+__device__ __forceinline__ void bamp_bayes_elem(const BampK& P, float rr, float ri, float cov, float& xr, float& xi,
+                                                float& var) {
+    const float a0 = hypotf(rr, ri);
+    const float g0 = expf(-(a0 * a0) / cov);
+    const double cd = (double)cov;
+    double gs = 0.0, sr = 0.0, si = 0.0, s2 = 0.0;
+    for (int k = 0; k < P.c.K; ++k) {
+        const double a = hypot((double)rr - P.sre[k], (double)ri - P.sim[k]);
+        const double g = exp(-(a * a) / cd);
+        const double ak = hypot(P.sre[k], P.sim[k]);
+        gs += g;
+        sr += P.sre[k] * g;
+        si += P.sim[k] * g;
+        s2 += (ak * ak) * g;
+    }
+    double norm = (double)(P.P0 * g0) + (double)P.Ps * gs;
+    if (norm == 0.0) norm = 1e-9;                                       // regularize_zero (bamp.py:90-92)
+    const double rn = 1.0 / norm;
+    const double er = ((double)P.Ps * sr) * rn, ei = ((double)P.Ps * si) * rn;
+    const double ae = hypot(er, ei);
+    xr = (float)er;
+    xi = (float)ei;
+    var = (float)(((double)P.Ps * s2) / norm - ae * ae);
+}
 
 struct BampWs {
     float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
@@ -206,7 +237,26 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
     pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2;
     pol.xm = P.xm; pol.var_new = bvar(P, t); pol.var_prev = bvar(P, t + 1); pol.secmax = P.secmax; pol.secabs = P.secabs;
     PartAcc pa;
-    denoise_sections<true, KK>(pol, nrows * pol.spr, P.M, P.c, pa);
+    if (P.elementwise) {
+        // no batch-global shift in random_denoiser: the section statistics stay neutral
+        float* vn = bvar(P, t);
+        const float* vp = bvar(P, t + 1);
+        for (int e = threadIdx.x; e < GBM * (BN / 2); e += AMP_WG) {
+            const int rho = e / (BN / 2), cc = e % (BN / 2);
+            if (rho < nrows && 2 * cc < ncols) {
+                const size_t o = (size_t)(row0 + rho) * P.N + col0 / 2 + cc;
+                const float2 v = *reinterpret_cast<const float2*>(lds + rho * C::LDC + 2 * cc);
+                float xr, xi, var;
+                bamp_bayes_elem(P, v.x, v.y, P.cov[o], xr, xi, var);
+                *reinterpret_cast<float2*>(P.xm + 2 * o) = make_float2(xr, xi);
+                vn[o] = var;
+                pa.sumvar += (double)var;
+                pa.notclose += torch_close(var, vp[o]) ? 0u : 1u;     // bamp.py:140
+            }
+        }
+    } else {
+        denoise_sections<true, KK>(pol, nrows * pol.spr, P.M, P.c, pa);
+    }
     part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
 }
 
@@ -377,6 +427,14 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.var0 = (float*)a->var; P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    AMP_REQUIRE(a->denoiser == 0 || a->denoiser == 1, "amp_bamp_run: denoiser %d", a->denoiser);
+    P.elementwise = a->denoiser;
+    P.P0 = a->P0;
+    P.Ps = a->Ps;
+    for (int k = 0; k < AMP_MAX_K; ++k) {
+        P.sre[k] = k < c->K ? c->re64[k] : 0.0;
+        P.sim[k] = k < c->K ? c->im64[k] : 0.0;
+    }
     const Const64 c64 = to_const64(c);
     hipStream_t st = (hipStream_t)stream;
     const float2* H = (const float2*)a->H;

@@ -18,6 +18,8 @@
 
 namespace amp {
 
+constexpr int AMP_DEC_MAX_NA = 64;
+
 struct DecK {
     int B, L, M, Na, Lin, S;
     int ibits;
@@ -31,7 +33,7 @@ struct DecK {
     DecPart* parts;
     int nblk;
     amp_counts* out;
-    int rule;            // 0: MAP (sparc), 1: segmented
+    int rule;            // 0: MAP (sparc), 1: segmented, 2: random
     DecConst c;
 };
 
@@ -78,6 +80,111 @@ __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
             o.ier += sp[w].ier; o.ser += sp[w].ser; o.iber += sp[w].iber; o.sber += sp[w].sber;
             o.mse += sp[w].mse; o.msef += sp[w].msef; o.msem += sp[w].msem; o.mseL += sp[w].mseL;
         }
+        P.parts[blockIdx.x] = o;
+    }
+}
+
+
+// Random decision (Loss.random_decision, loss.py:252-280; generator_mode='random'): per channel
+// use (row of Nt), the Na largest |x_m| (np.argsort()[-Na:]: NaN largest; exact ties in an
+// implementation-defined order in numpy, by larger index here), each decided to its nearest
+// point (float64, first minimum); the decided positions in ascending order are compared with
+// the true sorted indices / labels of that row (loss.py:165-178).  One thread per row: the
+// reference runs this only for B = 1 (its reshape drops the batch axis).
+__device__ __forceinline__ bool rnd_greater(bool n1, float v1, int m1, bool n2, float v2, int m2) {
+    if (n1 != n2) return n1;
+    if (n1) return m1 > m2;
+    if (v1 != v2) return v1 > v2;
+    return m1 > m2;
+}
+
+template <int KK>
+__global__ __launch_bounds__(AMP_WG) void random_decide_kernel(DecK P, int Nt, int R) {
+    constexpr int K = KK;
+    DecPart q = decpart_zero();
+    const long long ibmask = dec_ibmask(P.ibits);
+    const long long sbmask = (1LL << P.c.sbits) - 1;
+    for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < R; row += gridDim.x * blockDim.x) {
+        const float2* xm = P.xmap + (size_t)row * Nt;
+        const float2* xt = P.x + (size_t)row * Nt;
+        const float2* xe = P.xmmse + (size_t)row * Nt;
+        int pos[AMP_DEC_MAX_NA];
+        bool pn = true;
+        float pv = 0.f;
+        int pm = 0x7fffffff;
+        for (int a = 0; a < P.Na; ++a) {
+            bool bn = false;
+            float bv = -1.f;
+            int bm = -1;
+            for (int m = 0; m < Nt; ++m) {
+                const float v = hypotf(xm[m].x, xm[m].y);
+                const bool vn = v != v;
+                if (!rnd_greater(pn, pv, pm, vn, v, m)) continue;     // already chosen
+                if (bm < 0 || rnd_greater(vn, v, m, bn, bv, bm)) { bn = vn; bv = v; bm = m; }
+            }
+            pos[a] = bm;
+            pn = bn; pv = bv; pm = bm;
+        }
+        for (int a = 1; a < P.Na; ++a)                                   // ascending positions
+            for (int j = a; j > 0 && pos[j - 1] > pos[j]; --j) { const int t = pos[j]; pos[j] = pos[j - 1]; pos[j - 1] = t; }
+        const int lin = row % P.Lin;
+        int mism = 0;
+        double se = 0.0;
+        for (int j = 0; j < P.Na; ++j) {
+            const int m = pos[j];
+            const double xr = (double)xm[m].x, xi = (double)xm[m].y;
+            double d = INFINITY;
+            int kh = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double ds = hypot(xr - P.c.re[k], xi - P.c.im[k]);
+                if (ds < d) { d = ds; kh = k; }
+            }
+            pos[j] = m * K + kh;
+            const long long e = (long long)row * P.Na + j;
+            const long long ih = (long long)row * Nt + m;
+            long long sh = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k == kh) sh = P.c.gray[k];
+            q.ier += (ih != P.idx[e]);
+            q.ser += (sh != P.sym[e]);
+            q.iber += __popcll((unsigned long long)((ih ^ P.idx[e]) & ibmask));
+            q.sber += __popcll((unsigned long long)((sh ^ P.sym[e]) & sbmask));
+            if (P.dec) P.dec[e] = pos[j];
+        }
+        for (int m = 0; m < Nt; ++m) {
+            float hr = 0.f, hi = 0.f;
+            for (int j = 0; j < P.Na; ++j)
+                if (pos[j] / K == m) {
+                    const int kh = pos[j] - m * K;
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (k == kh) { hr = P.c.re32[k]; hi = P.c.im32[k]; }
+                }
+            mism |= (hr - xt[m].x != 0.f || hi - xt[m].y != 0.f) ? 1 : 0;
+            const float dr = xe[m].x - xt[m].x, di = xe[m].y - xt[m].y;
+            se += (double)dr * dr + (double)di * di;
+        }
+        // one mismatch flag per channel use, in the layout map_count_kernel folds
+        unsigned char* mrow = P.mism + (size_t)(row / P.Lin) * P.L + (size_t)lin * P.Na;
+        for (int a = 0; a < P.Na; ++a) mrow[a] = (a == 0) ? (unsigned char)mism : 0;
+        q.mse += se;
+        if (lin == 0) q.msef += se;
+        if (lin == P.Lin / 2) q.msem += se;
+        if (lin == P.Lin - 1) q.mseL += se;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    q.ier = group_sum(q.ier, 64); q.ser = group_sum(q.ser, 64); q.iber = group_sum(q.iber, 64);
+    q.sber = group_sum(q.sber, 64);
+    q.mse = group_sum(q.mse, 64); q.msef = group_sum(q.msef, 64); q.msem = group_sum(q.msem, 64);
+    q.mseL = group_sum(q.mseL, 64);
+    __shared__ DecPart sp[AMP_WG / 64];
+    if (lane == 0) sp[wave] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        DecPart o = sp[0];
+        for (int w = 1; w < AMP_WG / 64; ++w) decpart_add(o, sp[w]);
         P.parts[blockIdx.x] = o;
     }
 }
@@ -217,6 +324,44 @@ int amp_segmented_decide_count(const amp_dims* d, const amp_constellation* c, co
                                const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
                                void* decisions, void* ws, size_t ws_bytes, void* stream) {
     return decide_count(1, d, c, xmap, xmmse, x, sym, idx, ibits_trunc, counts, decisions, ws, ws_bytes, stream);
+}
+
+int amp_random_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
+                            const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
+                            void* decisions, void* ws, size_t ws_bytes, void* stream) {
+    AMP_REQUIRE(d && c && d->B > 0 && d->Nt > 0 && d->Lin > 0 && d->Na >= 1 && d->Na <= AMP_DEC_MAX_NA &&
+                    d->Na <= d->Nt && d->L == d->Na * d->Lin && c->K >= 1 && c->K <= AMP_MAX_K,
+                "amp_random_decide_count: bad dims (Na <= %d)", AMP_DEC_MAX_NA);
+    AMP_REQUIRE(xmap && xmmse && x && sym && idx && counts && ws, "amp_random_decide_count: null pointer argument");
+    AMP_REQUIRE(ws_bytes >= amp_map_decide_workspace_bytes(d), "amp_random_decide_count: workspace too small");
+    AMP_REQUIRE(ibits_trunc >= 0 && ibits_trunc < 64, "amp_random_decide_count: ibits_trunc out of range");
+    DecK P;
+    P.B = d->B; P.L = d->L; P.M = d->M; P.Na = d->Na; P.Lin = d->Lin; P.S = d->B * d->L;
+    P.ibits = ibits_trunc;
+    P.xmap = (const float2*)xmap; P.xmmse = (const float2*)xmmse; P.x = (const float2*)x;
+    P.sym = (const long long*)sym; P.idx = (const long long*)idx;
+    Carve cv(ws);
+    P.mism = cv.take<unsigned char>((size_t)P.S);
+    const int R = d->B * d->Lin;
+    P.nblk = std::max(1, std::min(cdiv(R, AMP_WG), decide_nblk(d)));
+    P.parts = cv.take<DecPart>((size_t)decide_nblk(d));
+    P.out = (amp_counts*)counts;
+    P.dec = (int*)decisions;
+    P.c = to_decconst(c);
+    P.rule = 2;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g(P.nblk), b(AMP_WG);
+    switch (P.c.K) {
+    case 1: hipLaunchKernelGGL(random_decide_kernel<1>, g, b, 0, st, P, d->Nt, R); break;
+    case 2: hipLaunchKernelGGL(random_decide_kernel<2>, g, b, 0, st, P, d->Nt, R); break;
+    case 4: hipLaunchKernelGGL(random_decide_kernel<4>, g, b, 0, st, P, d->Nt, R); break;
+    case 8: hipLaunchKernelGGL(random_decide_kernel<8>, g, b, 0, st, P, d->Nt, R); break;
+    default: hipLaunchKernelGGL(random_decide_kernel<16>, g, b, 0, st, P, d->Nt, R); break;
+    }
+    AMP_LAUNCH_CHECK("random_decide");
+    hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(1024), 0, st, P);
+    AMP_LAUNCH_CHECK("map_count");
+    return AMP_OK;
 }
 
 }  // extern "C"

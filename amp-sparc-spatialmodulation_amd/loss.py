@@ -52,8 +52,8 @@ class Loss:
         self.loss = {'T': 0}
         self.keys = list(KEYS)
         self.dtype = torch.complex64 if config.is_complex else torch.float32
-        # loss.py:38-43: 'sparc' -> MAP_decision, 'segmented' -> segmented_decision (both native);
-        # 'random' -> random_decision (not built: the reference's random-mode VAMP crashes).
+        # loss.py:38-43: 'sparc' -> MAP_decision, 'segmented' -> segmented_decision,
+        # 'random' -> random_decision (all three on the GPU)
         self.decision_mode = config.mode
         self._const = None
         self._dims = None
@@ -89,9 +89,8 @@ class Loss:
         """Launch the decision/count kernels; returns the device amp_counts buffer (async).
         ``out``: optional uint8 device buffer (>= sizeof(amp_counts)) to write the counters to."""
         rule = rule or self.decision_mode
-        if rule not in ('sparc', 'segmented'):
-            raise NotImplementedError("native decisions implement generator_mode 'sparc' and 'segmented' "
-                                      "(loss.py:222-250, 282-302)")
+        if rule not in ('sparc', 'segmented', 'random'):
+            raise ValueError(f'unknown decision rule {rule!r}')
         d, c = self._native()
         dev = xmap.device
         B = self.B
@@ -100,6 +99,9 @@ class Loss:
         if rule == 'segmented' and B != 1:
             # loss.py:232 reshapes the whole batch to (Na*Lin, M): numpy raises for B > 1
             raise ValueError(f'cannot reshape array of size {B * L * M} into shape ({L},{M})')
+        if rule == 'random' and B != 1:
+            # loss.py:262 reshapes the whole batch to (Lin, Nt)
+            raise ValueError(f'cannot reshape array of size {B * self.Lin * self.Nt} into shape ({self.Lin},{self.Nt})')
         xmap = _flat_c64(xmap, B, 'xmap')
         xmmse = _flat_c64(xmmse, B, 'xmmse')
         x = _flat_c64(x, B, 'x')
@@ -113,7 +115,8 @@ class Loss:
         ws = nat.WORKSPACE.get(dev, 'decide', wsb)
         counts = out if out is not None else nat.WORKSPACE.get(dev, 'counts', C.sizeof(nat.AmpCounts))
         dec_ptr = nat.dptr(decisions, torch.int32, 'decisions') if decisions is not None else None
-        fn = lib.amp_map_decide_count if rule == 'sparc' else lib.amp_segmented_decide_count
+        fn = {'sparc': lib.amp_map_decide_count, 'segmented': lib.amp_segmented_decide_count,
+              'random': lib.amp_random_decide_count}[rule]
         nat.check(fn(C.byref(d), C.byref(c), nat.dptr(xmap, name='xmap'), nat.dptr(xmmse, name='xmmse'),
                      nat.dptr(x, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices'),
                      self._ibits, nat.dptr(counts), dec_ptr, nat.dptr(ws), wsb, nat.stream_ptr(dev)),
@@ -194,6 +197,10 @@ class Loss:
         """(xhat, gray labels, flat indices) of loss.py:222-250, decided on the GPU (B = 1)."""
         return self._decide(xamp, 'segmented')
 
+    def random_decision(self, xamp: torch.Tensor):
+        """(xhat, gray labels, flat indices) of loss.py:252-280, decided on the GPU (B = 1)."""
+        return self._decide(xamp, 'random')
+
     def decision(self, xamp: torch.Tensor):
         """The mode's decision (loss.py:38-43)."""
         return self._decide(xamp, self.decision_mode)
@@ -208,6 +215,12 @@ class Loss:
         self.device_counts(xamp, xamp, xamp, zeros, zeros, decisions=dec, rule=rule)
         f = dec.cpu().numpy().astype(np.int64)
         m_hat, k_hat = np.divmod(f, self.config.K)
+        if rule == 'random':                      # Na decided positions per row of Nt
+            R = B * self.Lin
+            xhat = np.zeros((R, self.Nt), dtype=np.complex64)
+            rows = np.repeat(np.arange(R), self.Na)
+            xhat[rows, m_hat] = np.asarray(self.symbols)[k_hat]
+            return xhat.ravel(), np.asarray(self.gray)[k_hat], rows * self.Nt + m_hat
         M = self.Nt // self.Na
         xhat = np.zeros((S, M), dtype=np.complex64)
         xhat[np.arange(S), m_hat] = np.asarray(self.symbols)[k_hat]

@@ -200,6 +200,10 @@ class VAMP(nn.Module):
         """vamp.py:159-187.  Everything runs on the device; the returned Loss resolves its
         counters on first access (the forward's one host synchronisation), so the launches of
         the next forward can be queued before this one's results are read back."""
+        if self.config.mode == 'random':
+            # vamp.py:45-48 picks Shrink('bayes') for 'random', which returns one tensor; the
+            # layer's two-value unpacking then fails (recorded in tests/golden/g8_random_curves.json)
+            raise ValueError('not enough values to unpack (expected 2, got 1)')
         T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
         T.args.engine = self.engine
         res, host = self._result_slot(T.y.device)

@@ -154,7 +154,9 @@ typedef struct amp_bamp_args {
     const void* H;      /* c64 [n][N] */
     const void* y;      /* c64 [B][n] */
     int32_t max_iter;
-    int32_t pad;
+    int32_t denoiser;   /* 0: segmented block denoiser (bamp.py:66-77, modes 'sparc'/'segmented');
+                           1: element-wise Bayes random_denoiser (bamp.py:79-88, mode 'random'),
+                              float64 with the P0 / Ps prior below */
     double noise_var;   /* Na/Nr/SNR (bamp.py:124) */
     void* xmap;         /* out c64 [B][N]: decision input T.xmap (bamp.py:142) */
     void* xmmse;        /* out c64 [B][N] */
@@ -162,6 +164,7 @@ typedef struct amp_bamp_args {
     void* status;
     void* ws;
     size_t ws_bytes;
+    float P0, Ps;       /* Config.P0 / Config.Ps as float32 (bamp.py:36), denoiser 1 only */
 } amp_bamp_args;
 
 size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
@@ -209,6 +212,14 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
                          int32_t ibits_trunc, void* counts, void* decisions, void* ws, size_t ws_bytes,
                          void* stream);
 size_t amp_map_decide_workspace_bytes(const amp_dims* d);
+/* Same counters with Loss.random_decision (loss.py:252-280, generator_mode='random'): per
+ * channel use the Na largest |x_m| (NaN largest; exact ties by larger index), each decided to
+ * its nearest point, compared in ascending position order with the row's true sorted indices.
+ * decisions (optional): int32 [B*Lin*Na], position * K + k.  Na <= 64.  Same workspace. */
+int amp_random_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap,
+                            const void* xmmse, const void* x, const void* sym, const void* idx,
+                            int32_t ibits_trunc, void* counts, void* decisions, void* ws,
+                            size_t ws_bytes, void* stream);
 /* Same counters with Loss.segmented_decision (loss.py:222-250, generator_mode='segmented'):
  * per section the largest |x_m| (last index on ties, NaN largest), then the nearest point
  * |x_m - a_k| (first minimum).  The reference only runs it for B = 1 (its reshape drops the

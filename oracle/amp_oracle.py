@@ -263,6 +263,25 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
     return dict(r=r, xmmse=xm, var=var, T=t + 1)
 
 
+def bamp_random_denoise(r, cov, cfg: OracleConfig):
+    """BAMPLayer.random_denoiser (bamp.py:79-88): element-wise Bayes posterior under the P0/Ps
+    prior.  G(0) in float32 (r - 0 stays complex64); G(a_k) in float64 (complex64 - complex128:
+    torch.tensor(config.symbols) keeps numpy's complex128, bamp.py:37); float32 prior scalars
+    promoted to float64; complex128 / float64 as a reciprocal multiply."""
+    r = np.asarray(r, C64)
+    cov = np.asarray(cov, F32)
+    sym = cfg.symbols.astype(np.complex128)
+    P0, Ps = F32(cfg.P0), F32(cfg.Ps)
+    with np.errstate(all='ignore'):
+        G0 = np.exp(-(_torch_abs(r) ** 2) / cov).astype(F32)
+        Gs = np.exp(-(np.abs(r.astype(np.complex128)[..., None] - sym) ** 2) / cov[..., None].astype(np.float64))
+        norm = (P0 * G0).astype(np.float64) + np.float64(Ps) * Gs.sum(axis=-1)
+        norm[norm == 0.] = 1e-9
+        ex = (np.float64(Ps) * (sym * Gs).sum(axis=-1)) * (1.0 / norm)
+        var = np.float64(Ps) * ((np.abs(sym) ** 2) * Gs).sum(axis=-1) / norm - np.abs(ex) ** 2
+    return ex.astype(C64), var.astype(F32)
+
+
 def bamp_detect(H, y, SNR: float, cfg: OracleConfig, trace: list | None = None):
     """BAMP: Tracker (bamp.py:12-25), BAMPLayer.forward (bamp.py:48-64),
     denoiser with tau = cov/2 (bamp.py:66-77), BAMP.forward (bamp.py:116-143).
@@ -289,8 +308,11 @@ def bamp_detect(H, y, SNR: float, cfg: OracleConfig, trace: list | None = None):
         cov = _recip(((_recip(u)) @ abs2).astype(F32))            # bamp.py:62
         g = (_div_real((y - z).astype(C64), u) @ Hc).astype(C64)  # bamp.py:63
         xmap = (xm + cov * g).astype(C64)
-        tau = (cov / F32(2)).astype(F32)                          # bamp.py:68
-        xm, var = block_denoise(xmap, tau, cfg)                   # bamp.py:64
+        if cfg.mode == 'random':                                  # bamp.py:38-41
+            xm, var = bamp_random_denoise(xmap, cov, cfg)
+        else:
+            tau = (cov / F32(2)).astype(F32)                      # bamp.py:68
+            xm, var = block_denoise(xmap, tau, cfg)               # bamp.py:64
         if trace is not None:
             trace.append(dict(xmap=xmap.copy(), xmmse=xm.copy(), var=var.copy(), z=z.copy(), u=u.copy()))
         if allclose_f32(var, prev):                               # bamp.py:140
@@ -377,6 +399,24 @@ def segmented_decision(xmap: np.ndarray, cfg: OracleConfig):
     return xhat.ravel(), np.asarray(cfg.gray)[k_hat], np.arange(S) * cfg.M + m_hat
 
 
+def random_decision(xmap: np.ndarray, cfg: OracleConfig):
+    """Loss.random_decision (loss.py:252-280): per channel use (row of Nt) the Na largest |x|
+    (numpy's own argsort()[-Na:], as the reference), each decided to its nearest point (float64,
+    first minimum); returns (xhat c64 [R*Nt], gray labels and flat indices in ascending order)."""
+    xa = np.asarray(xmap).reshape(-1, cfg.Nt)
+    sym = cfg.symbols.astype(np.complex128)
+    xhat = np.zeros_like(xa)
+    xgray = np.zeros(xa.shape, dtype=int)
+    for j, x in enumerate(xa):
+        for k in np.abs(x).argsort()[-cfg.Na:]:
+            i = int(np.abs(x[k].astype(np.complex128) - sym).argmin())
+            xhat[j, k] = sym[i]
+            xgray[j, k] = cfg.gray[i]
+    xhat = xhat.ravel()
+    index = np.sort(xhat.nonzero()[0])
+    return xhat, xgray.ravel()[index], index
+
+
 def _de2bi_count(v: np.ndarray, bits: int) -> int:
     """count_nonzero(de2bi(v, bits)) (loss.py:181-196): set bits among the low `bits` bits."""
     v = v.astype(np.int64) & ((1 << bits) - 1)
@@ -390,7 +430,7 @@ def error_rates(xmap, xmmse, x, symbols, indices, cfg: OracleConfig):
     xmap = np.asarray(xmap).reshape(-1, Lin, Nt)
     xmmse = np.asarray(xmmse).reshape(-1, Lin, Nt)
     x = np.asarray(x).reshape(-1, Lin, Nt)
-    decide = segmented_decision if cfg.mode == 'segmented' else map_decision    # loss.py:38-43
+    decide = {'segmented': segmented_decision, 'random': random_decision}.get(cfg.mode, map_decision)   # loss.py:38-43
     xhat, shat, ihat = decide(xmap, cfg)
     xhat = xhat.reshape((-1, Lin, Nt))
     # loss.py:116-119
@@ -513,4 +553,5 @@ def shrink_sw_ook(r, cov, B, L, M):
 __all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect',
            'bamp_detect', 'scamp_detect', 'map_decision', 'error_rates', 'loss_dict', 'allclose_f32',
            'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX',
-           'shrink_bayes', 'shrink_ook', 'shrink_sw_ook', 'segmented_decision']
+           'shrink_bayes', 'shrink_ook', 'shrink_sw_ook', 'segmented_decision',
+           'random_decision', 'bamp_random_denoise']

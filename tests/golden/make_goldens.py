@@ -24,6 +24,8 @@ Groups:
       takes any H), 16-QAM and QPSK twins of cfg5's 64-QAM (which Config rejects), B = 1024
   g7  generator_mode='segmented' (B = 1): Loss.segmented_decision on crafted inputs (ties,
       zero rows, the 16-QAM duplicate point) and VAMP / BAMP Loss dicts along EbN0
+  g8  generator_mode='random' (B = 1): Loss.random_decision on crafted inputs and BAMP Loss
+      dicts along EbN0 (the reference's random-mode VAMP raises; recorded)
   g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
       by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
 
@@ -468,6 +470,70 @@ def g7():
 
 
 # ---------------------------------------------------------------------------
+def g8():
+    """generator_mode='random' at B = 1."""
+    rng = np.random.default_rng(88)
+    flat = {}
+    n = 0
+    for alph in ['QPSK', '16QAM', 'BPSK', '8PSK']:
+        for (Nt, Na, Nr, Lin, Lh) in [(16, 2, 32, 1, 1), (24, 3, 32, 3, 2), (64, 8, 64, 2, 1)]:
+            cfg = Config(Nt, Na, Nr, Lin, Lh, batch=1, generator_mode='random', iterations=5, alphabet=alph,
+                         channel_profile='uniform', channel_truncation='tail', device='cpu')
+            np.random.seed(n)
+            x, sym, idx = Data(cfg).generate_message()
+            xv = c(x).reshape(1, -1)
+            for variant in ['noisy', 'weak', 'exact']:
+                if variant == 'noisy':
+                    xmap = xv + (rng.standard_normal(xv.shape) + 1j * rng.standard_normal(xv.shape)).astype(np.complex64) * 0.4
+                elif variant == 'weak':
+                    xmap = 0.3 * xv + (rng.standard_normal(xv.shape) + 1j * rng.standard_normal(xv.shape)).astype(np.complex64) * 0.3
+                else:
+                    xmap = xv.copy()
+                xmap = xmap.astype(np.complex64)
+                xmmse = (xv + rng.standard_normal(xv.shape).astype(np.float32) * 0.1).astype(np.complex64)
+                L = Loss(cfg)
+                L(torch.from_numpy(xmap).view(1, -1, 1), torch.from_numpy(xmmse).view(1, -1, 1), x, sym, idx, 3)
+                dec = L.decision(xmap.reshape(-1, cfg.Lin, cfg.Nt))
+                key = f'case{n}'
+                flat.update({f'{key}/alphabet': np.array(alph), f'{key}/dims': np.array([Nt, Na, Nr, 1, Lin, Lh]),
+                             f'{key}/xmap': xmap, f'{key}/xmmse': xmmse, f'{key}/x': xv,
+                             f'{key}/sym': sym, f'{key}/idx': idx,
+                             f'{key}/xhat': dec[0], f'{key}/shat': dec[1], f'{key}/ihat': dec[2],
+                             f'{key}/loss': np.array(json.dumps(loss_to_json(L.loss)))})
+                n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g8_random.npz'), **flat)
+    print('g8 decision cases', n)
+    curves = {}
+    for alph in ['QPSK', '16QAM']:
+        Nt, Na, Nr = 32, 4, 64
+        cfg = Config(Nt, Na, Nr, 1, 1, batch=1, generator_mode='random', iterations=20, alphabet=alph,
+                     channel_profile='uniform', channel_truncation='tail', device='cpu')
+        pts = {}
+        for EbN0 in [0, 4, 8, 12, 16]:
+            for seed in range(6):
+                inp = gen_inputs(cfg, seed, float(EbN0), svd=False)
+                L = ref_bamp.BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                rec = loss_to_json(L.loss)
+                rec['sha_A'] = sha(inp['A'])
+                rec['sha_x'] = sha(inp['x'])
+                pts[f'{seed}/{EbN0}'] = rec
+        curves[f'rand_bamp_{alph}'] = {'algo': 'bamp', 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': 1, 'alphabet': alph,
+                                       'iterations': 20, 'points': pts}
+        print('g8 bamp', alph, 'ver', [round(p['ver'], 2) for p in pts.values()][:10])
+    cfg = Config(32, 4, 64, 1, 1, batch=1, generator_mode='random', iterations=20, alphabet='QPSK',
+                 channel_profile='uniform', channel_truncation='tail', device='cpu')
+    inp = gen_inputs(cfg, 0, 8.0, svd=True)
+    try:
+        ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        curves['vamp_random_error'] = None
+    except Exception as e:  # noqa: BLE001  (recorded, not raised)
+        curves['vamp_random_error'] = [type(e).__name__, str(e)]
+    with open(os.path.join(HERE, 'g8_random_curves.json'), 'w') as f:
+        json.dump(curves, f, indent=1, sort_keys=True)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
@@ -518,7 +584,7 @@ def g4(names=None):
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
     names = [w for w in which if w.startswith('cfg')]
     for w in which:
         if w == 'g1':
@@ -527,6 +593,8 @@ if __name__ == '__main__':
             g2()
         elif w == 'g3':
             g3()
+        elif w == 'g8':
+            g8()
         elif w == 'g7':
             g7()
         elif w == 'g6':
