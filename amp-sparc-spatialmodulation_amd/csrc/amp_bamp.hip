@@ -128,7 +128,8 @@ __device__ __forceinline__ float* bvar(const BampK& P, int t) { return (t & 1) ?
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds);
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
 __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds);
     using C = GemmCfg<128>;
@@ -169,7 +171,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
 __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds);
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
@@ -217,7 +220,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     using C = GemmCfg<BN>;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);

@@ -65,6 +65,25 @@ __host__ __device__ __forceinline__ size_t wpack16_index(int n, int k, int kap) 
     return (((size_t)ct * (kap >> 4) + g) * 64 + lane) * 4 + (w & 3);
 }
 
+// XCD-aware tile order.  Workgroups are dispatched in linear order (x fastest) round-robin over
+// the 8 XCDs, each with its own 4 MB L2.  The row-block-fastest grid would make every XCD sweep
+// ALL column blocks, i.e. the whole packed weight (8 MB for BAMP's H at cfg5) through each L2.
+// Remapped, XCD x walks a contiguous run of tiles in column-block-major order: ~1/8 of the
+// column blocks over all row blocks, so its share of the weight stays resident in its L2.
+// A bijection of [0, gridDim.x * gridDim.y): every tile is computed exactly once.
+struct GemmTile {
+    int rb, cb;      // row block (trials), column block
+};
+__device__ __forceinline__ GemmTile xcd_tile() {
+    constexpr int NXCD = 8;
+    const int nr = gridDim.x, total = gridDim.x * gridDim.y;
+    const int id = blockIdx.y * nr + blockIdx.x;
+    const int x = id % NXCD, q = id / NXCD;
+    const int base = total / NXCD, rem = total % NXCD;
+    const int pos = x * base + min(x, rem) + q;
+    return GemmTile{pos % nr, pos / nr};
+}
+
 // Plain A operand: rows of `lda` floats, `ka` valid columns (zero beyond, and for rows >= rows).
 struct ALoadPlain {
     const float* __restrict__ a;

@@ -103,7 +103,8 @@ __device__ __forceinline__ float scamp_gamma(const ScampK& P, const float* psi_r
 __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds);
     using C = GemmCfg<128>;
@@ -163,7 +164,8 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     using C = GemmCfg<BN>;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
             for (int lo = 0; lo < P.Lout; ++lo)
                 acc += P.W[lo * P.Lin + lc] * (1.0f / phi[(size_t)(row0 + rho) * P.Lout + lo]);
             tv = ((1.0f / acc) * (float)P.L) / (float)P.Nr;          // L / x = recip(x) * L ; / Mr
-            if (blockIdx.y == 0) P.tau[(size_t)(row0 + rho) * P.Lin + lc] = tv;
+            if (tile.cb == 0) P.tau[(size_t)(row0 + rho) * P.Lin + lc] = tv;
         }
         tau_t[rho * P.Lin + lc] = tv;
     }

@@ -50,7 +50,8 @@ __global__ __launch_bounds__(AMP_WG) void vamp_k1(VampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const VampIter it = P.iters[t];
     if (it.stopped) return;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * 128;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twok = 2 * P.k;
     gemm_tile<128>(ALoadRt{P.xm, P.r, twoN, P.B, twoN, it.dxdr_prev, it.ns_prev}, P.Wt1, P.kap1, row0, col0, lds);
     using C = GemmCfg<128>;
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(AMP_WG) void vamp_k2(VampK P, int t) {
     const VampIter it = P.iters[t];
     if (it.stopped) return;
     using C = GemmCfg<BN>;
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twok = 2 * P.k;
     gemm_tile<BN>(ALoadPlain{P.w, twok, P.B, twok}, P.Wt2, P.kap2, row0, col0, lds);
     // x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)

@@ -185,7 +185,8 @@ __global__ __launch_bounds__(AMP_WG) void gemm_store_kernel(const float* __restr
                                                             const float* __restrict__ wt, int kap,
                                                             float* __restrict__ c, int ldc, int nc) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int row0 = blockIdx.x * GBM, col0 = blockIdx.y * BN;
+    const GemmTile tile = xcd_tile();
+    const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     gemm_tile<BN>(ALoadPlain{a, lda, rows, ka}, wt, kap, row0, col0, lds);
     using C = GemmCfg<BN>;
     for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
