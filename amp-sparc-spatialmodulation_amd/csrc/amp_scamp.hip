@@ -23,6 +23,12 @@ constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in register
 
 struct alignas(16) ScampIter {
     int32_t stopped, T, fixed, fixed_all;
+    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done by scamp_fix_*,
+    // settled by scamp_fin): the exact batch max |xi| G, the float32 estimate's slack, and the
+    // allclose count before the fix-up
+    double G, slack;
+    uint32_t notclose;
+    int32_t active, pad[2];
 };
 
 struct ScampK {
@@ -227,10 +233,31 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds);
 }
 
-// reduction, exact float64 fix-up of out-of-range sections (+ their psi), allclose(psi)
+// Rare path (float64 fix-up) spread over the grid.  scamp_r reduces the partials and, when some
+// section may leave the float64 range, settles the exact batch max |xi| G (one workgroup: few
+// candidate sections); scamp_fix_sec recomputes the out-of-range sections with the reference's
+// exact arithmetic, scamp_fix_psi their coupling blocks' psi (and the allclose delta), each a
+// grid kernel; scamp_fin adds the per-block counts and decides the early exit.  Without a
+// pending fix-up the three later kernels return at once.  (Before: one workgroup recomputed
+// every such section, 267 us per iteration at cfg3's NaN onset.)
+__device__ __forceinline__ void scamp_finish(const ScampK& P, int t, uint32_t notclose, int fixed, int fixed_all) {
+    ScampIter nx;
+    nx.stopped = notclose == 0 ? 1 : 0;
+    nx.T = t + 1;
+    nx.fixed = fixed;
+    nx.fixed_all = fixed_all;
+    nx.G = 0.0; nx.slack = 0.0; nx.notclose = notclose; nx.active = 0; nx.pad[0] = nx.pad[1] = 0;
+    P.iters[t + 1] = nx;
+    if (nx.stopped || t + 1 == P.max_iter) {
+        amp_status s;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+        *P.status = s;
+    }
+}
+
 __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
-    __shared__ unsigned s_nc[SRWG / 64];
     __shared__ double s_d[SRWG / 64];
     const ScampIter cur = P.iters[t];
     if (cur.stopped) {
@@ -238,77 +265,126 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, Const64 c64, int t) {
         return;
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
-    int fixed = 0;
     if (part_allnan(pa)) {
         if (!cur.fixed_all) {
             nan_fill(P.xm, nullptr, (size_t)P.B * P.N);
             float* psi_new = spsi(P, t);
             for (int e = threadIdx.x; e < P.B * P.Lin; e += blockDim.x) psi_new[e] = __int_as_float(0x7fc00000);
         }
-        pa.notclose = 1;
-        fixed = -1;
+        if (threadIdx.x == 0) scamp_finish(P, t, 1u, -1, 1);
     } else if (part_danger(pa)) {
-        // sections, then every coupling block that holds a recomputed section
+        // exact float64 batch max |xi| over the candidate sections (those within the float32
+        // estimate's slack of the float32 batch max)
         const double slack = logit_slack(pa.maxabs);
         const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
-        float2* x2 = reinterpret_cast<float2*>(P.xm);
         const float* tau = P.tau;
         const int M = P.M, L = P.L, N = P.N, Nt = P.Nt, Lin = P.Lin;
-        int dnc = 0;
-        auto ldf = [=](int sct) {
+        double gm = 0.0;
+        for (int sct = threadIdx.x; sct < P.B * L; sct += blockDim.x) {
+            if ((double)P.secabs[sct] < pa.maxabs - slack) continue;
             const size_t o0 = (size_t)sct * M;
             const int b = sct / L, lc = (int)((o0 % (size_t)N) / Nt);
             const float tv = tau[(size_t)b * Lin + lc];
-            return [=](int m, float& rr, float& ri, float& it) {
+            auto ld = [=](int m, float& rr, float& ri, float& it) {
                 const float2 v = xp2[o0 + m];
                 rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
             };
-        };
-        auto stf = [=](int sct) {
-            const size_t o0 = (size_t)sct * M;
-            return [=](int m, float xr, float xi, float) { x2[o0 + m] = make_float2(xr, xi); };
-        };
-        double G;
-        fixed = fixup_sections<false>(P.B * L, M, P.secmax, P.secabs, pa.maxabs, c64, ldf, stf, &G, s_d);
-        __syncthreads();
-        const float* psi_prev = spsi(P, t + 1);
-        float* psi_new = spsi(P, t);
-        const int spb = P.Nt / P.M;   // sections per coupling block
-        for (int blk = threadIdx.x; blk < P.B * P.Lin; blk += blockDim.x) {
-            bool hit = false;
-            for (int j = 0; j < spb && !hit; ++j) hit = (double)P.secmax[(size_t)blk * spb + j] - G < AMP_DANGER + slack;
-            if (!hit) continue;
-            const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
-            double ssum = 0.0;
-            for (int m = 0; m < P.Nt; ++m) {
-                const float a = (float)sqrt((double)xr[m].x * xr[m].x + (double)xr[m].y * xr[m].y);
-                ssum += (double)(a * a);
-            }
-            const float ps = 1.0f - (float)ssum / (float)P.Na;
-            dnc += (torch_close(ps, psi_prev[blk]) ? 0 : 1) - (torch_close(psi_new[blk], psi_prev[blk]) ? 0 : 1);
-            psi_new[blk] = ps;
+            gm = fmax(gm, section_absmax_f64(ld, M, c64));
         }
-        dnc = group_sum(dnc, 64);
-        if ((threadIdx.x & 63) == 0) s_nc[threadIdx.x >> 6] = (unsigned)dnc;
+        gm = group_max(gm, 64);
+        if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = gm;
         __syncthreads();
-        unsigned nc = 0;
-        for (int w = 0; w < SRWG / 64; ++w) nc += s_nc[w];
-        pa.notclose += nc;
-    }
-    if (threadIdx.x == 0) {
-        ScampIter nx;
-        nx.stopped = pa.notclose == 0 ? 1 : 0;
-        nx.T = t + 1;
-        nx.fixed = fixed;
-        nx.fixed_all = (fixed < 0) ? 1 : 0;
-        P.iters[t + 1] = nx;
-        if (nx.stopped || t + 1 == P.max_iter) {
-            amp_status s;
-            s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
-            s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
-            *P.status = s;
+        if (threadIdx.x == 0) {
+            double G = 0.0;
+            for (int w = 0; w < SRWG / 64; ++w) G = fmax(G, s_d[w]);
+            ScampIter nx;
+            nx.stopped = 0; nx.T = t + 1; nx.fixed = 0; nx.fixed_all = 0;
+            nx.G = G; nx.slack = slack; nx.notclose = pa.notclose; nx.active = 1; nx.pad[0] = nx.pad[1] = 0;
+            P.iters[t + 1] = nx;
         }
+    } else if (threadIdx.x == 0) {
+        scamp_finish(P, t, pa.notclose, 0, 0);
     }
+}
+
+// per-block integer counts of the fix-up kernels, written over iteration t's partials (already
+// consumed by scamp_r): slot i = {sections fixed, allclose delta} of block i
+__device__ __forceinline__ int2* scamp_fix_counts(const ScampK& P, int t) {
+    return reinterpret_cast<int2*>(P.parts + (size_t)t * P.nblk);
+}
+
+__device__ __forceinline__ int block_sum_int(int v, int* s_i) {
+    v = group_sum(v, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_i[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_i[w];
+    return tot;
+}
+
+__global__ __launch_bounds__(AMP_WG) void scamp_fix_sec(ScampK P, Const64 c64, int t) {
+    __shared__ int s_i[AMP_WG / 64];
+    const ScampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+    float2* x2 = reinterpret_cast<float2*>(P.xm);
+    const int M = P.M, L = P.L, N = P.N, Nt = P.Nt, Lin = P.Lin;
+    int cnt = 0;
+    for (int sct = blockIdx.x * blockDim.x + threadIdx.x; sct < P.B * L; sct += gridDim.x * blockDim.x) {
+        if (!((double)P.secmax[sct] - pend.G < AMP_DANGER + pend.slack)) continue;
+        const size_t o0 = (size_t)sct * M;
+        const int b = sct / L, lc = (int)((o0 % (size_t)N) / Nt);
+        const float tv = P.tau[(size_t)b * Lin + lc];
+        auto ld = [=](int m, float& rr, float& ri, float& it) {
+            const float2 v = xp2[o0 + m];
+            rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
+        };
+        auto st = [=](int m, float xr, float xi, float) { x2[o0 + m] = make_float2(xr, xi); };
+        exact_section_f64<false>(ld, st, M, c64, pend.G);
+        ++cnt;
+    }
+    cnt = block_sum_int(cnt, s_i);
+    if (threadIdx.x == 0) scamp_fix_counts(P, t)[blockIdx.x].x = cnt;
+}
+
+__global__ __launch_bounds__(AMP_WG) void scamp_fix_psi(ScampK P, int t) {
+    __shared__ int s_i[AMP_WG / 64];
+    const ScampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    const float* psi_prev = spsi(P, t + 1);
+    float* psi_new = spsi(P, t);
+    const int spb = P.Nt / P.M;   // sections per coupling block
+    int dnc = 0;
+    for (int blk = blockIdx.x * blockDim.x + threadIdx.x; blk < P.B * P.Lin; blk += gridDim.x * blockDim.x) {
+        bool hit = false;
+        for (int j = 0; j < spb && !hit; ++j)
+            hit = (double)P.secmax[(size_t)blk * spb + j] - pend.G < AMP_DANGER + pend.slack;
+        if (!hit) continue;
+        const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
+        double ssum = 0.0;
+        for (int m = 0; m < P.Nt; ++m) {
+            const float a = (float)sqrt((double)xr[m].x * xr[m].x + (double)xr[m].y * xr[m].y);
+            ssum += (double)(a * a);
+        }
+        const float ps = 1.0f - (float)ssum / (float)P.Na;
+        dnc += (torch_close(ps, psi_prev[blk]) ? 0 : 1) - (torch_close(psi_new[blk], psi_prev[blk]) ? 0 : 1);
+        psi_new[blk] = ps;
+    }
+    dnc = block_sum_int(dnc, s_i);
+    if (threadIdx.x == 0) scamp_fix_counts(P, t)[blockIdx.x].y = dnc;
+}
+
+__global__ __launch_bounds__(AMP_WG) void scamp_fin(ScampK P, int t, int nfix) {
+    __shared__ int s_i[AMP_WG / 64];
+    const ScampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    const int2* c = scamp_fix_counts(P, t);
+    int fixed = 0, dnc = 0;
+    for (int i = threadIdx.x; i < nfix; i += blockDim.x) { fixed += c[i].x; dnc += c[i].y; }
+    fixed = block_sum_int(fixed, s_i);
+    dnc = block_sum_int(dnc, s_i);
+    if (threadIdx.x == 0) scamp_finish(P, t, (uint32_t)((int)pend.notclose + dnc), fixed, 0);
 }
 
 // Tracker (scamp.py:9-25): z = y, psi = 1, phi = inf, xmmse = 0
@@ -324,6 +400,7 @@ __global__ void scamp_init_kernel(ScampK P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ScampIter it;
         it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0;
+        it.G = 0.0; it.slack = 0.0; it.notclose = 0; it.active = 0; it.pad[0] = it.pad[1] = 0;
         P.iters[0] = it;
     }
 }
@@ -418,10 +495,15 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     AMP_LAUNCH_CHECK("scamp_init");
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
+    // fix-up grid: one slot per block in iteration t's partials (consumed by then)
+    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
     for (int t = 0; t < P.max_iter; ++t) {
         hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
         launch_kb(P, gr, ldsB, t, st);
         hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
+        hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+        hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
+        hipLaunchKernelGGL(scamp_fin, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
         AMP_LAUNCH_CHECK("scamp iteration");
     }
     hipLaunchKernelGGL(scamp_output_kernel, dim3(64), dim3(256), 0, st, P);

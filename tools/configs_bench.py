@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Throughput of every BASELINE config on one MI355X (bench.py measures only the headline cfg4).
+
+cfg1 BAMP Nt=4 Nr=8 Na=1 QPSK B=100 T<=10 (the reference's CPU-plumbing case: launch-bound)
+cfg2 VAMP Nt=64 Nr=128 Na=4 16-QAM B=1024 T<=20
+cfg3 SCAMP Nt=128 Nr=256 Na=8 16-QAM B=4096 T<=20
+cfg4 VAMP Nt=256 Nr=512 Na=8 16-QAM B=4096 T<=20 (bench.py's workload; repeated for reference)
+(cfg5: tools/cfg5_bench.py.)  Inputs: the reference's generators on the host replica, resident
+in HBM.  Each forward (detector + GPU decision + 256-byte readback) is timed over 50 epochs
+after 30 warm-up epochs; algorithmic flops per trial-iteration from SURVEY.md §8(d):
+VAMP 16 N k, SCAMP 16 n N, BAMP 20 n N.  Prints one JSON line per config."""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'amp-sparc-spatialmodulation_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import amp_native as nat  # noqa: E402
+from bamp import BAMP  # noqa: E402
+from channel import Channel  # noqa: E402
+from config import Config  # noqa: E402
+from data import Data  # noqa: E402
+from scamp import SCAMP  # noqa: E402
+from vamp import VAMP  # noqa: E402
+
+PEAK_TF = 157.3
+CFGS = {
+    'cfg1': ('bamp', 4, 1, 8, 100, 'QPSK', 10, 8.0),
+    'cfg2': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
+    'cfg3': ('scamp', 128, 8, 256, 4096, '16QAM', 20, 8.0),
+    'cfg4': ('vamp', 256, 8, 512, 4096, '16QAM', 20, 8.0),
+}
+
+
+def main(steps=50, warmup=30, only=None):
+    dev = torch.device('cuda:0')
+    for name, (algo, Nt, Na, Nr, B, alph, iters, ebn0) in CFGS.items():
+        if only and name not in only:
+            continue
+        cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
+                     channel_profile='uniform', channel_truncation='tail', device='cpu')
+        np.random.seed(0)
+        torch.manual_seed(0)
+        ch, da = Channel(cfg), Data(cfg)
+        W, A = ch.generate_as_sparc()
+        x, sym, idx = da.generate_message()
+        SNR = cfg.snr(ebn0)
+        y = A @ x + ch.awgn(SNR)
+        cfg.device = 'cuda'
+        mv = lambda t: t.to(dev).contiguous()  # noqa: E731
+        if algo == 'vamp':
+            U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+            det, args = VAMP(cfg), (mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
+            flop = 16.0 * Nt * min(Nt, Nr)
+        elif algo == 'scamp':
+            det, args = SCAMP(cfg), (mv(W), mv(A), mv(y), SNR, mv(x), sym, idx)
+            flop = 16.0 * Nr * Nt
+        else:
+            det, args = BAMP(cfg), (mv(A), mv(y), SNR, mv(x), sym, idx)
+            flop = 20.0 * Nr * Nt
+        for _ in range(warmup):
+            L = det(*args)
+        L.resolve()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            L = det(*args)
+        L.resolve()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        T = int(L.loss['T'])
+        tf = B * T * flop / (ms * 1e-3) / 1e12
+        print(json.dumps({'config': name, 'algo': algo, 'Nt': Nt, 'Nr': Nr, 'Na': Na, 'alphabet': alph, 'B': B,
+                          'EbN0': ebn0, 'T': T, 'ver': float(L.loss['ver']), 'ser': float(L.loss['ser']),
+                          'ms_per_epoch': round(ms, 4), 'symbol_vectors_per_s': B / (ms * 1e-3),
+                          'trial_iterations_per_s': B * T / (ms * 1e-3), 'achieved_TFLOPs': round(tf, 2),
+                          'mfma_frac_incl_decision': round(tf / PEAK_TF, 4)}), flush=True)
+    nat.unload()
+
+
+if __name__ == '__main__':
+    main(only=sys.argv[1:] or None)
