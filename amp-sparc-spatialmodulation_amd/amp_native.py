@@ -87,6 +87,7 @@ SIGNATURES = {
     'amp_vamp_detect_count': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
+    'amp_bamp_random_denoise': (C.c_int, [_K, C.c_int64, _P, _P, C.c_float, C.c_float, _P, _P, _P]),
     'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_scamp_run': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
     'amp_block_denoise': (C.c_int, [_D, _K, _P, _I, C.c_float, _P, _P, _P, _P, C.c_size_t, _P]),

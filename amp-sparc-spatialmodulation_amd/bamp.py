@@ -30,6 +30,25 @@ class BAMPLayer(nn.Module):
         """bamp.py:66-77: tau is cov, halved inside (tau = cov/2)."""
         return block_denoise(self.config, s, tau, mode=1)
 
+    def random_denoiser(self, r: torch.Tensor, cov: torch.Tensor):
+        """bamp.py:79-88 (generator_mode 'random'): element-wise float64 Bayes posterior under the
+        P0 / Ps prior; (xmmse complex64, var float32) shaped like r."""
+        cfg = self.config
+        rr = _c64(r, (-1,))
+        cv = cov.to(device=rr.device, dtype=torch.float32).expand(r.shape).reshape(-1).contiguous()
+        xm = torch.empty_like(rr)
+        var = torch.empty(rr.shape, dtype=torch.float32, device=rr.device)
+        nat.check(nat.lib().amp_bamp_random_denoise(
+            cfg.constellation(), rr.numel(), nat.dptr(rr, name='r'), nat.dptr(cv, name='cov'),
+            float(np.float32(cfg.P0)), float(np.float32(cfg.Ps)), nat.dptr(xm), nat.dptr(var),
+            nat.stream_ptr(rr.device)), 'amp_bamp_random_denoise')
+        return xm.view(r.shape), var.view(r.shape)
+
+    @property
+    def denoiser(self):
+        """The mode's denoiser (bamp.py:38-41)."""
+        return self.random_denoiser if self.config.mode == 'random' else self.segmented_denoiser
+
 
 class BAMP(nn.Module):
     def __init__(self, config: Config) -> None:

@@ -466,4 +466,37 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     return AMP_OK;
 }
 
+// BAMPLayer.random_denoiser (bamp.py:79-88) as a standalone element-wise op (layer-level API).
+__global__ __launch_bounds__(AMP_WG) void bamp_random_denoise_kernel(BampK P, long long count, const float2* r,
+                                                                     const float* cov, float2* xm, float* var) {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < count;
+         e += (long long)gridDim.x * blockDim.x) {
+        float xr, xi, v;
+        bamp_bayes_elem(P, r[e].x, r[e].y, cov[e], xr, xi, v);
+        xm[e] = make_float2(xr, xi);
+        var[e] = v;
+    }
+}
+
+int amp_bamp_random_denoise(const amp_constellation* c, int64_t count, const void* r, const void* cov, float P0,
+                            float Ps, void* xmmse, void* var, void* stream) {
+    AMP_REQUIRE(c && c->K >= 1 && c->K <= AMP_MAX_K, "amp_bamp_random_denoise: bad constellation");
+    AMP_REQUIRE(count >= 0, "amp_bamp_random_denoise: count < 0");
+    if (count == 0) return AMP_OK;
+    AMP_REQUIRE(r && cov && xmmse && var, "amp_bamp_random_denoise: null pointer argument");
+    BampK P{};
+    P.c = to_const(c);
+    P.P0 = P0;
+    P.Ps = Ps;
+    for (int k = 0; k < AMP_MAX_K; ++k) {
+        P.sre[k] = k < c->K ? c->re64[k] : 0.0;
+        P.sim[k] = k < c->K ? c->im64[k] : 0.0;
+    }
+    const int g = (int)std::max(1LL, std::min(((long long)count + AMP_WG - 1) / AMP_WG, 8192LL));
+    hipLaunchKernelGGL(bamp_random_denoise_kernel, dim3(g), dim3(AMP_WG), 0, (hipStream_t)stream, P, (long long)count,
+                       (const float2*)r, (const float*)cov, (float2*)xmmse, (float*)var);
+    AMP_LAUNCH_CHECK("bamp_random_denoise");
+    return AMP_OK;
+}
+
 }  // extern "C"

@@ -169,6 +169,10 @@ typedef struct amp_bamp_args {
 
 size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
 int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
+/* BAMPLayer.random_denoiser (bamp.py:79-88) alone (layer-level API): r c64 [count], cov f32
+ * [count] -> xmmse c64, var f32; the element-wise float64 Bayes posterior of denoiser 1. */
+int amp_bamp_random_denoise(const amp_constellation* c, int64_t count, const void* r, const void* cov, float P0,
+                            float Ps, void* xmmse, void* var, void* stream);
 
 /* ---- SCAMP — replaces SCAMP.forward (scamp.py:77-107) with SCAMPLayer.forward
  *      (scamp.py:43-59) and its mean-only denoiser (scamp.py:61-68). ---- */

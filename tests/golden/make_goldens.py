@@ -26,6 +26,7 @@ Groups:
       zero rows, the 16-QAM duplicate point) and VAMP / BAMP Loss dicts along EbN0
   g8  generator_mode='random' (B = 1): Loss.random_decision on crafted inputs and BAMP Loss
       dicts along EbN0 (the reference's random-mode VAMP raises; recorded)
+  g9  BAMPLayer.random_denoiser (bamp.py:79-88) unit vectors (per-element cov, underflow regimes)
   g4  Loss dicts along EbN0 for the BASELINE configs + QPSK twins (inputs regenerated
       by the build's RNG replica; SHA-256 of the first (A, x) pins the replica)
 
@@ -534,6 +535,29 @@ def g8():
 
 
 # ---------------------------------------------------------------------------
+def g9():
+    """BAMPLayer.random_denoiser straight from the reference layer ('random' mode)."""
+    rng = np.random.default_rng(99)
+    flat = {}
+    n = 0
+    for alph in ['QPSK', '16QAM', 'BPSK', '8PSK', 'OOK']:
+        cfg = Config(32, 4, 64, 1, 1, batch=4, generator_mode='random', iterations=5, alphabet=alph,
+                     channel_profile='uniform', channel_truncation='tail', device='cpu')
+        lay = ref_bamp.BAMPLayer(cfg)
+        for scale in [1e-4, 1e-2, 0.1, 1.0, 10.0]:
+            r = ((rng.standard_normal((4, 32)) + 1j * rng.standard_normal((4, 32))) * 0.7).astype(np.complex64)
+            cov = ((np.abs(rng.standard_normal((4, 32))) + 0.2) * scale).astype(np.float32)
+            xm, var = lay.random_denoiser(torch.from_numpy(r).view(4, 32, 1), torch.from_numpy(cov).view(4, 32, 1))
+            key = f'case{n}'
+            flat.update({f'{key}/alphabet': np.array(alph), f'{key}/r': r, f'{key}/cov': cov,
+                         f'{key}/xmmse': c(xm), f'{key}/var': c(var)})
+            n += 1
+    flat['ncases'] = np.array(n)
+    np.savez_compressed(os.path.join(HERE, 'g9_bamp_random_denoise.npz'), **flat)
+    print('g9 cases', n)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
@@ -584,7 +608,7 @@ def g4(names=None):
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9']
     names = [w for w in which if w.startswith('cfg')]
     for w in which:
         if w == 'g1':
@@ -593,6 +617,8 @@ if __name__ == '__main__':
             g2()
         elif w == 'g3':
             g3()
+        elif w == 'g9':
+            g9()
         elif w == 'g8':
             g8()
         elif w == 'g7':

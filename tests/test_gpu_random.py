@@ -51,3 +51,19 @@ def test_random_mode_bamp_b1(device, name):
         if float(L.loss['ver']) != ref['ver'] or float(L.loss['ser']) != ref['ser']:
             diff.append((key, float(L.loss['ver']), ref['ver'], float(L.loss['ser']), ref['ser']))
     assert len(diff) <= 1, diff
+
+
+@pytest.mark.parametrize('name', sorted(__import__('test_random_cpu').G9, key=lambda k: int(k[4:])))
+def test_bamp_random_denoiser_layer(device, name):
+    """BAMPLayer.random_denoiser on the GPU (amp_bamp_random_denoise) against the reference's
+    layer (g9): float64 arithmetic, float32/complex64 outputs within 1e-5 relative."""
+    from bamp import BAMPLayer
+    from test_random_cpu import G9
+    c = G9[name]
+    layer = BAMPLayer(_cfg(32, 4, 64, 1, 1, 4, str(c.alphabet)))
+    r = torch.from_numpy(c.r).to(device).view(4, 32, 1)
+    cov = torch.from_numpy(c.cov).to(device).view(4, 32, 1)
+    xm, var = layer.denoiser(r, cov)
+    assert xm.dtype == torch.complex64 and var.shape == (4, 32, 1)
+    np.testing.assert_allclose(xm.cpu().numpy()[..., 0], c.xmmse, rtol=1e-5, atol=1e-6, equal_nan=True)
+    np.testing.assert_allclose(var.cpu().numpy()[..., 0], c.var, rtol=1e-5, atol=1e-6, equal_nan=True)

@@ -85,3 +85,17 @@ def test_oracle_random_mode_bamp_curves(name):
         if float(got['ver']) != ref['ver'] or float(got['ser']) != ref['ser']:
             diff.append((key, float(got['ver']), ref['ver'], float(got['ser']), ref['ser']))
     assert len(diff) <= 1, diff
+
+
+G9 = gio._group(np.load(os.path.join(gio.GOLDEN, 'g9_bamp_random_denoise.npz')))
+
+
+@pytest.mark.parametrize('name', sorted(G9, key=lambda k: int(k[4:])))
+def test_oracle_bamp_random_denoiser(name):
+    """oracle.bamp_random_denoise against the reference's BAMPLayer.random_denoiser (g9)."""
+    from oracle import bamp_random_denoise
+    c = G9[name]
+    cfg = OracleConfig(32, 4, 64, B=4, alphabet=str(c.alphabet), mode='random')
+    xm, var = bamp_random_denoise(c.r, c.cov, cfg)
+    np.testing.assert_allclose(xm, c.xmmse, rtol=1e-5, atol=1e-6, equal_nan=True)
+    np.testing.assert_allclose(var, c.var, rtol=1e-5, atol=1e-6, equal_nan=True)
