@@ -52,6 +52,8 @@ struct ScampK {
     float* secabs;         // [B*L] per-section max |logit|
     Partial* parts;
     ScampIter* iters;
+    unsigned* psi_nc;      // [max_iter][psi_nblk] allclose counts of scamp_psi (split tiles only)
+    int psi_nblk, psi_split;
     amp_status* status;
     Const c;
 };
@@ -61,10 +63,15 @@ struct ScampWs {
     float *secmax, *secabs;
     Partial* parts;
     ScampIter* iters;
+    unsigned* psi_nc;
     size_t bytes;
 };
 
-static int scamp_bn(const amp_dims* d) { return (2 * d->Nt <= 128) ? 128 : 256; }
+// 128 columns whenever a section fits (2M <= 128): twice the workgroups of a whole-coupling-
+// block tile (cfg3: 256 instead of 128).  A tile that does not hold whole coupling blocks
+// (2 Nt > BN) leaves psi to scamp_psi.
+static int scamp_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
+static int scamp_psi_nblk(const amp_dims* d) { return std::max(1, std::min(cdiv(d->B * d->Lin, AMP_WG), 1024)); }
 
 static void scamp_geometry(const amp_dims* d, ScampK& P) {
     P.B = d->B; P.N = d->N; P.n = d->n; P.L = d->L; P.M = d->M;
@@ -91,6 +98,7 @@ static ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.secabs = cv.take<float>((size_t)d->B * d->L);
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
     w.iters = cv.take<ScampIter>((size_t)max_iter + 1);
+    w.psi_nc = cv.take<unsigned>((size_t)max_iter * scamp_psi_nblk(d));
     w.bytes = cv.off;
     return w;
 }
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     const float* psi_prev = spsi(P, t + 1);
     float* psi_new = spsi(P, t);
     unsigned nc = 0;
-    for (int e = threadIdx.x; e < GBM * nlc; e += AMP_WG) {
+    for (int e = threadIdx.x; e < (P.psi_split ? 0 : GBM * nlc); e += AMP_WG) {
         const int rho = e / nlc, b = e % nlc;
         if (rho >= nrows) continue;
         const int lc = lc0 + b;
@@ -231,6 +239,39 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     }
     pa.notclose += nc;
     part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds);
+}
+
+// psi (scamp.py:59) and its allclose count (scamp.py:105) when the A^H tile holds only part of
+// a coupling block: one thread per (trial, block), after every tile of the iteration is written.
+__device__ __forceinline__ unsigned block_sum_u32(unsigned v, unsigned* s_u) {
+    v = group_sum(v, 64);
+    if ((threadIdx.x & 63) == 0) s_u[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_u[w];
+    return tot;
+}
+
+__global__ __launch_bounds__(AMP_WG) void scamp_psi(ScampK P, int t) {
+    __shared__ unsigned s_u[AMP_WG / 64];
+    if (P.iters[t].stopped) return;
+    const float* psi_prev = spsi(P, t + 1);
+    float* psi_new = spsi(P, t);
+    unsigned nc = 0;
+    for (int blk = blockIdx.x * blockDim.x + threadIdx.x; blk < P.B * P.Lin; blk += gridDim.x * blockDim.x) {
+        const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
+        double ssum = 0.0;
+        for (int m = 0; m < P.Nt; ++m) {
+            const float2 v = xr[m];
+            const float a = (float)sqrt((double)v.x * v.x + (double)v.y * v.y);   // torch abs (hypot)
+            ssum += (double)(a * a);
+        }
+        const float ps = 1.0f - (float)ssum / (float)P.Na;
+        nc += torch_close(ps, psi_prev[blk]) ? 0u : 1u;
+        psi_new[blk] = ps;
+    }
+    nc = block_sum_u32(nc, s_u);
+    if (threadIdx.x == 0) P.psi_nc[(size_t)t * P.psi_nblk + blockIdx.x] = nc;
 }
 
 // Rare path (float64 fix-up) spread over the grid.  scamp_r reduces the partials and, when some
@@ -265,6 +306,12 @@ __global__ __launch_bounds__(SRWG) void scamp_r(ScampK P, Const64 c64, int t) {
         return;
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
+    if (P.psi_split) {
+        __shared__ unsigned s_u[SRWG / 64];
+        unsigned nc = 0;
+        for (int i = threadIdx.x; i < P.psi_nblk; i += blockDim.x) nc += P.psi_nc[(size_t)t * P.psi_nblk + i];
+        pa.notclose += block_sum_u32(nc, s_u);
+    }
     if (part_allnan(pa)) {
         if (!cur.fixed_all) {
             nan_fill(P.xm, nullptr, (size_t)P.B * P.N);
@@ -484,6 +531,7 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     P.y = (const float*)a->y; P.z = w.z; P.s = w.s; P.phi = w.phi; P.tau = w.tau;
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
+    P.psi_nc = w.psi_nc; P.psi_nblk = scamp_psi_nblk(d); P.psi_split = (P.bn / 2 < P.Nt) ? 1 : 0;
     P.c = to_const(c);
     const Const64 c64 = to_const64(c);
     hipStream_t st = (hipStream_t)stream;
@@ -500,6 +548,8 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     for (int t = 0; t < P.max_iter; ++t) {
         hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
         launch_kb(P, gr, ldsB, t, st);
+        if (P.psi_split)
+            hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
         hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
         hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
         hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
