@@ -71,7 +71,7 @@ struct ScampWs {
 // block tile (cfg3: 256 instead of 128).  A tile that does not hold whole coupling blocks
 // (2 Nt > BN) leaves psi to scamp_psi.
 static int scamp_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
-static int scamp_psi_nblk(const amp_dims* d) { return std::max(1, std::min(cdiv(d->B * d->Lin, AMP_WG), 1024)); }
+static int scamp_psi_nblk(const amp_dims* d) { return std::max(1, std::min(cdiv(d->B * d->Lin, AMP_WG / 64), 2048)); }
 
 static void scamp_geometry(const amp_dims* d, ScampK& P) {
     P.B = d->B; P.N = d->N; P.n = d->n; P.L = d->L; P.M = d->M;
@@ -253,22 +253,28 @@ __device__ __forceinline__ unsigned block_sum_u32(unsigned v, unsigned* s_u) {
 }
 
 __global__ __launch_bounds__(AMP_WG) void scamp_psi(ScampK P, int t) {
+    // one wavefront per (trial, coupling block): lanes stride the block's Nt entries
     __shared__ unsigned s_u[AMP_WG / 64];
     if (P.iters[t].stopped) return;
     const float* psi_prev = spsi(P, t + 1);
     float* psi_new = spsi(P, t);
+    const int lane = threadIdx.x & 63;
+    const int nwave = gridDim.x * (AMP_WG / 64);
     unsigned nc = 0;
-    for (int blk = blockIdx.x * blockDim.x + threadIdx.x; blk < P.B * P.Lin; blk += gridDim.x * blockDim.x) {
+    for (int blk = blockIdx.x * (AMP_WG / 64) + (threadIdx.x >> 6); blk < P.B * P.Lin; blk += nwave) {
         const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * P.Nt;
         double ssum = 0.0;
-        for (int m = 0; m < P.Nt; ++m) {
+        for (int m = lane; m < P.Nt; m += 64) {
             const float2 v = xr[m];
             const float a = (float)sqrt((double)v.x * v.x + (double)v.y * v.y);   // torch abs (hypot)
             ssum += (double)(a * a);
         }
-        const float ps = 1.0f - (float)ssum / (float)P.Na;
-        nc += torch_close(ps, psi_prev[blk]) ? 0u : 1u;
-        psi_new[blk] = ps;
+        ssum = group_sum(ssum, 64);
+        if (lane == 0) {
+            const float ps = 1.0f - (float)ssum / (float)P.Na;
+            nc += torch_close(ps, psi_prev[blk]) ? 0u : 1u;
+            psi_new[blk] = ps;
+        }
     }
     nc = block_sum_u32(nc, s_u);
     if (threadIdx.x == 0) P.psi_nc[(size_t)t * P.psi_nblk + blockIdx.x] = nc;
