@@ -75,9 +75,12 @@ class Shrink(nn.Module):
         return 0.0, v
 
     @staticmethod
-    def _real_part(r: torch.Tensor) -> torch.Tensor:
-        """Re(r) as contiguous float32 (r.real, shrink.py:68/:153)."""
-        return (r.real if r.is_complex() else r).to(torch.float32).contiguous()
+    def _real_part(r: torch.Tensor):
+        """(tensor, is_complex) whose real part the kernels read (r.real, shrink.py:68/:153):
+        complex64 r is handed over as it lies (the kernel reads the real lanes), no copy."""
+        if r.is_complex():
+            return r.to(torch.complex64).resolve_conj().resolve_neg().contiguous(), 1
+        return r.to(torch.float32).contiguous(), 0
 
     # -- denoisers ----------------------------------------------------------------------------
     def bayes(self, r: torch.Tensor, cov) -> torch.Tensor:
@@ -94,24 +97,24 @@ class Shrink(nn.Module):
 
     def shrinkOOK(self, r: torch.Tensor, cov) -> Tuple[torch.Tensor, torch.Tensor]:
         """shrink.py:139-157: (exp float32 shaped like r, dxdr = der.mean() 0-dim float32)."""
-        re = self._real_part(r)
+        re, cplx = self._real_part(r)
         if re.numel() == 0:
             raise RuntimeError('shrinkOOK: empty input (the reference returns a NaN mean)')
-        out = torch.empty_like(re)
+        out = torch.empty(re.shape, dtype=torch.float32, device=re.device)
         dxdr = torch.empty((), dtype=torch.float32, device=re.device)
         cs, cv = self._cov_args(cov, re.shape, re.device)
         L = nat.lib()
         wsb = L.amp_shrink_ook_workspace_bytes(re.numel())
         ws = nat.WORKSPACE.get(re.device, 'shrink_ook', wsb)
         nat.check(L.amp_shrink_ook(
-            re.numel(), 0, nat.dptr(re, name='r'), cs, None if cv is None else nat.dptr(cv, name='cov'),
+            re.numel(), cplx, nat.dptr(re, name='r'), cs, None if cv is None else nat.dptr(cv, name='cov'),
             self._theta, nat.dptr(out, name='exp'), nat.dptr(dxdr, name='dxdr'), nat.dptr(ws), wsb,
             nat.stream_ptr(re.device)), 'amp_shrink_ook')
         return out, dxdr
 
     def sw_shrinkOOK(self, r: torch.Tensor, cov) -> Tuple[torch.Tensor, torch.Tensor]:
         """shrink.py:58-76: sections of M along the flattened (B, L, M) view."""
-        re = self._real_part(r)
+        re, cplx = self._real_part(r)
         if re.numel() != self.B * self.L * self.M:
             raise RuntimeError(f"shape '[{self.B}, {self.L}, {self.M}]' is invalid for input of size {re.numel()}")
         S = self.B * self.L
@@ -119,7 +122,7 @@ class Shrink(nn.Module):
         var = torch.empty(self.B, self.L * self.M, 1, dtype=torch.float32, device=re.device)
         cs, cv = self._cov_args(cov, re.shape, re.device)
         nat.check(nat.lib().amp_shrink_sw_ook(
-            S, self.M, 0, nat.dptr(re, name='r'), cs, None if cv is None else nat.dptr(cv, name='cov'),
+            S, self.M, cplx, nat.dptr(re, name='r'), cs, None if cv is None else nat.dptr(cv, name='cov'),
             nat.dptr(x, name='exp'), nat.dptr(var, name='var'), nat.stream_ptr(re.device)), 'amp_shrink_sw_ook')
         return x, var
 
