@@ -19,6 +19,33 @@ import amp_native as nat
 from config import Config
 
 KEYS = ['fer', 'nMSE', 'nMSEf', 'nMSEm', 'nMSEL', 'ver', 'verf', 'verm', 'verL', 'ber', 'iber', 'sber', 'ier', 'ser']
+# amp_counts (include/amp_sparc.h) fields in struct order
+COUNT_FIELDS = ('ier', 'ser', 'iber', 'sber', 'ver', 'verf', 'verm', 'verL', 'fer', 'mse', 'msef', 'msem', 'mseL')
+
+
+def counts_to_vector(c) -> np.ndarray:
+    """amp_counts -> float64[13] (the integer counters are exact in float64 below 2^53), the
+    payload of the one all-reduce that merges trial-sharded epochs."""
+    return np.array([float(getattr(c, f)) for f in COUNT_FIELDS], dtype=np.float64)
+
+
+def vector_to_counts(v):
+    c = nat.AmpCounts()
+    for i, f in enumerate(COUNT_FIELDS):
+        setattr(c, f, int(round(float(v[i]))) if i < 9 else float(v[i]))
+    return c
+
+
+def allreduce_counts(vec: np.ndarray) -> np.ndarray:
+    """Sum the per-rank counter vectors with ONE all-reduce (RCCL on the rank's GPU for the
+    'nccl' backend, host memory for gloo); identity without torch.distributed."""
+    dist = torch.distributed
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return np.asarray(vec, dtype=np.float64)
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    t = torch.as_tensor(np.asarray(vec, dtype=np.float64)).to(dev)
+    dist.all_reduce(t)
+    return t.cpu().numpy()
 
 
 def _as_device_labels(a, device) -> torch.Tensor:
@@ -171,6 +198,12 @@ class Loss:
             sber, sber_ = 0., 0.
         ber = (iber_ + sber_) / (Na * self.sbits + self.ibits)
         return fer, nMSE, nMSEf, nMSEm, nMSEL, ver, verf, verm, verL, ber, iber, sber, ier, ser
+
+    def rates_from_vector(self, vec: np.ndarray, epochs: int = 1):
+        """The 14 metrics averaged over `epochs` epochs of B trials whose counters were summed
+        into `vec` (counts_to_vector): every metric is linear in the counters, so this is the
+        mean of the per-epoch metrics (Loss.accumulate + Loss.average, loss.py:325-346)."""
+        return tuple(np.float64(r) / epochs for r in self.rates_from_counts(vector_to_counts(vec)))
 
     def record(self, rates, iterations: int) -> None:
         """Loss.__call__'s bookkeeping (loss.py:60-65)."""

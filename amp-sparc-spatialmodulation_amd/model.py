@@ -46,6 +46,21 @@ def _dist():
     return 0, 1
 
 
+def _comm_device():
+    """Where a collective's tensor must live: the rank's GPU for RCCL ('nccl'), host for gloo."""
+    if torch.distributed.get_backend() == 'nccl':
+        return torch.device('cuda', torch.cuda.current_device())
+    return torch.device('cpu')
+
+
+def _broadcast_seed() -> int:
+    """A fresh base seed drawn on rank 0 (OS entropy) and broadcast to every rank."""
+    base = torch.tensor([int(np.random.SeedSequence().entropy % (2 ** 31))], dtype=torch.int64)
+    base = base.to(_comm_device())
+    torch.distributed.broadcast(base, src=0)
+    return int(base.cpu().item())
+
+
 class Model(nn.Module):
     def __init__(self, config: Config, detector: str = 'vamp', path: str | None = None, amp=None,
                  seed: int | None = None, rng: str = 'host') -> None:
@@ -65,9 +80,15 @@ class Model(nn.Module):
         self.data = Data(config, rng=rng)
         self.path = path if path is not None else f'Simulations/{_DIRS[detector]}/{config.name}'
         self.rank, self.world = _dist()
+        if seed is None and self.world > 1:
+            # unseeded multi-rank sweep: every rank would start torch's and numpy's generators
+            # from the same default state and draw the same epochs; rank 0 draws a base seed
+            # and broadcasts it, so the ranks' streams are distinct
+            seed = _broadcast_seed()
+        self.seed = seed
         if seed is not None:
             # one independent stream per rank (rank 0 of a 1-process run = the plain seed)
-            np.random.seed(seed + 7919 * self.rank)
+            np.random.seed((seed + 7919 * self.rank) % 2 ** 32)
             torch.manual_seed(seed + 7919 * self.rank)
         if self.rank == 0:
             os.makedirs(self.path, exist_ok=True)
@@ -113,9 +134,7 @@ class Model(nn.Module):
             return
         keys = ['T'] + [k for k in self.loss.keys if k in self.loss.loss]
         vals = torch.tensor([float(np.asarray(self.loss.loss.get(k, 0.0), dtype=np.float64)) for k in keys],
-                            dtype=torch.float64)
-        if torch.distributed.get_backend() == 'nccl':
-            vals = vals.to(torch.device('cuda', torch.cuda.current_device()))
+                            dtype=torch.float64).to(_comm_device())
         torch.distributed.all_reduce(vals)
         vals = vals.cpu().numpy()
         self.loss.loss['T'] = float(vals[0])

@@ -75,6 +75,15 @@ class Shrink(nn.Module):
         return 0.0, v
 
     @staticmethod
+    def _single(r: torch.Tensor, what: str) -> None:
+        """The kernels compute in float32 / complex64 (the dtypes every reference caller hands
+        over).  For float64 / complex128 r the reference's outputs would be float64 / complex128;
+        rather than silently returning a downcast result, such inputs are refused."""
+        if r.dtype in (torch.float64, torch.complex128):
+            raise TypeError(f'Shrink.{what}: {r.dtype} input is not supported by the gfx950 kernels '
+                            '(float32 / complex64 only; no silent downcast)')
+
+    @staticmethod
     def _real_part(r: torch.Tensor):
         """(tensor, is_complex) whose real part the kernels read (r.real, shrink.py:68/:153):
         complex64 r is handed over as it lies (the kernel reads the real lanes), no copy."""
@@ -85,6 +94,7 @@ class Shrink(nn.Module):
     # -- denoisers ----------------------------------------------------------------------------
     def bayes(self, r: torch.Tensor, cov) -> torch.Tensor:
         """shrink.py:78-96.  Output dtype = promote(r, symbols) as in the reference."""
+        self._single(r, 'bayes')
         cplx = r.is_complex() or self.dtype == torch.complex64
         rr = r.to(torch.complex64 if cplx else torch.float32).resolve_conj().resolve_neg().contiguous()
         out = torch.empty_like(rr)
@@ -97,6 +107,7 @@ class Shrink(nn.Module):
 
     def shrinkOOK(self, r: torch.Tensor, cov) -> Tuple[torch.Tensor, torch.Tensor]:
         """shrink.py:139-157: (exp float32 shaped like r, dxdr = der.mean() 0-dim float32)."""
+        self._single(r, 'shrinkOOK')
         re, cplx = self._real_part(r)
         if re.numel() == 0:
             raise RuntimeError('shrinkOOK: empty input (the reference returns a NaN mean)')
@@ -114,6 +125,7 @@ class Shrink(nn.Module):
 
     def sw_shrinkOOK(self, r: torch.Tensor, cov) -> Tuple[torch.Tensor, torch.Tensor]:
         """shrink.py:58-76: sections of M along the flattened (B, L, M) view."""
+        self._single(r, 'sw_shrinkOOK')
         re, cplx = self._real_part(r)
         if re.numel() != self.B * self.L * self.M:
             raise RuntimeError(f"shape '[{self.B}, {self.L}, {self.M}]' is invalid for input of size {re.numel()}")

@@ -180,10 +180,11 @@ class VAMP(nn.Module):
 
     def detect(self, U, s, Vh, y, SNR: float) -> Tracker:
         """All iterations on the device, asynchronous (no host sync)."""
-        T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
-        T.args.engine = self.engine
-        nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
-                  'amp_vamp_run')
+        with torch.cuda.device(y.device):
+            T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
+            T.args.engine = self.engine
+            nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
+                      'amp_vamp_run')
         return T
 
     def _result_slot(self, device):
@@ -204,6 +205,10 @@ class VAMP(nn.Module):
             # vamp.py:45-48 picks Shrink('bayes') for 'random', which returns one tensor; the
             # layer's two-value unpacking then fails (recorded in tests/golden/g8_random_curves.json)
             raise ValueError('not enough values to unpack (expected 2, got 1)')
+        with torch.cuda.device(y.device):   # the C ABI sizes and launches on the current device
+            return self._forward(U, s, Vh, y, SNR, x, symbols, indices)
+
+    def _forward(self, U, s, Vh, y, SNR, x, symbols, indices) -> Loss:
         T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
         T.args.engine = self.engine
         res, host = self._result_slot(T.y.device)
@@ -223,7 +228,7 @@ class VAMP(nn.Module):
             self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
         host.copy_(res, non_blocking=True)
         done = torch.cuda.Event()
-        done.record()
+        done.record(torch.cuda.current_stream(T.y.device))   # the stream the launches and the copy ran on
         self.L.resolve()                 # the previous forward's counters (it has finished by now)
         self.L.dump()                                                    # vamp.py:180
 
@@ -234,6 +239,7 @@ class VAMP(nn.Module):
             counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
             if status.nan_state < 0:
                 raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')
+            L.last_counts = counts
             L.record(L.rates_from_counts(counts), int(status.T))
         self.L._pending = finish
         self.last = T

@@ -27,6 +27,10 @@ import torch        # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
 HBM_PEAK_GBS = 8000.0
+# time(oracle) / time(reference) on the same 8 cores of the build container, same cfg4 workload
+# (tools/cpu_ratio.py; the reference cannot travel to the GPU box): the port's CPU speed relative
+# to the reference's CPU path.  None until measured.
+PORT_OVER_REFERENCE = None
 
 CONFIGS = {
     # name: (Nt, Na, Nr, B, alphabet, iterations)
@@ -58,9 +62,10 @@ def make_inputs(cfg, seed, EbN0, device):
                          sym=sym, idx=idx))
 
 
-def cpu_baseline(cfgname, EbN0, seed, sample_trials):
+def cpu_baseline(cfgname, EbN0, seed, sample_trials, repeats=3):
     """The oracle (numpy restatement of the reference path, oracle/) timed on this host's
-    cores on a bounded sample of the same workload: `sample_trials` trials of the config."""
+    cores on a bounded sample of the same workload: `sample_trials` trials of the config, one
+    warm-up run, then the median of `repeats` timed runs."""
     from threadpoolctl import threadpool_limits
     from oracle import OracleConfig, vamp_detect, loss_dict
     from config import Config
@@ -70,14 +75,20 @@ def cpu_baseline(cfgname, EbN0, seed, sample_trials):
                  channel_profile='uniform', channel_truncation='tail', device='cpu')
     inp = make_inputs(cfg, seed, EbN0, 'cpu')['cpu']
     ocfg = OracleConfig(Nt, Na, Nr, B=sample_trials, alphabet=alph, iterations=iters)
+    times = []
     with threadpool_limits(limits=cores):
-        t0 = time.perf_counter()
-        out = vamp_detect(inp['U'], inp['s'], inp['Vh'], inp['y'], cfg.snr(EbN0), ocfg)
-        loss_dict(out['r'], out['xmmse'], inp['x'], inp['sym'], inp['idx'], out['T'], ocfg)
-        dt = time.perf_counter() - t0
+        for rep in range(repeats + 1):
+            t0 = time.perf_counter()
+            out = vamp_detect(inp['U'], inp['s'], inp['Vh'], inp['y'], cfg.snr(EbN0), ocfg)
+            loss_dict(out['r'], out['xmmse'], inp['x'], inp['sym'], inp['idx'], out['T'], ocfg)
+            if rep > 0:                       # run 0 is the warm-up
+                times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     return dict(value=sample_trials / dt, unit='symbol-vectors/s', cores=cores, kind='port',
                 sample=f'{sample_trials} trials of {cfgname} (Nt={Nt} Nr={Nr} Na={Na} {alph}), EbN0={EbN0} dB, '
-                       f'T={out["T"]}, numpy oracle incl. decision+metrics, {dt:.1f} s')
+                       f'T={out["T"]}, numpy oracle incl. decision+metrics, median of {repeats} runs '
+                       f'({", ".join(f"{t:.1f}" for t in times)} s) after one warm-up',
+                port_over_reference_time=PORT_OVER_REFERENCE)
 
 
 def traffic_from_profile(persistent):
@@ -98,6 +109,27 @@ def traffic_from_profile(persistent):
     return None
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: start N fresh child processes, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), wait for
+    all of them and return the worst exit status.  The parent makes no GPU call (it never
+    initialises HIP, and never re-execs itself)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -113,9 +145,13 @@ def main():
     ap.add_argument('--engine', default='auto', choices=['auto', 'launches', 'persistent'])
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
     dist = world > 1
     if dist:
         import torch.distributed as tdist
@@ -126,6 +162,7 @@ def main():
 
     from config import Config
     from vamp import VAMP
+    from loss import allreduce_counts, counts_to_vector
     import ctypes as C
     import amp_native as nat
     nat.lib()
@@ -133,6 +170,8 @@ def main():
     Nt, Na, Nr, B, alph, iters = CONFIGS[args.config]
     cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cuda')
+    # every rank detects its own independent Monte-Carlo epoch (its own channel, messages and
+    # noise: seed + rank), as the trial-sharded sweep does
     inp = make_inputs(cfg, args.seed + rank, args.ebn0, device)
     engine = {'auto': nat.ENGINE_AUTO, 'launches': nat.ENGINE_LAUNCHES, 'persistent': nat.ENGINE_PERSISTENT}[args.engine]
     det = VAMP(cfg, engine=engine)
@@ -142,13 +181,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    det.L.resolve()
     if dist:
         tdist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    acc = np.zeros(13)
+    L = None
     for _ in range(args.steps):
+        prev = L
         L = step()       # a step's counters are read back while the next step's launches run
+        if prev is not None:
+            acc += counts_to_vector(det.L.last_counts)   # resolved by step(): the previous forward's
     L.resolve()          # ... and the last step's inside the timed region too
+    acc += counts_to_vector(L.last_counts)
+    merged = allreduce_counts(acc)   # ONE all-reduce (RCCL) of the error counters of every rank
     torch.cuda.synchronize(device)
     el = time.perf_counter() - t0
     if dist:
@@ -157,7 +204,8 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         el = t.item()
     T = int(L.loss['T'])
-    ver, ser = float(L.loss['ver']), float(L.loss['ser'])
+    rates = dict(zip(L.keys, L.rates_from_vector(merged, epochs=world * args.steps)))
+    ver, ser = float(rates['ver']), float(rates['ser'])
 
     # dominant kernel timed with HIP events on the stream it runs on: the persistent engine's
     # single vamp_persist launch (T iterations: 2 complex mat-vecs per trial-iteration), or the
@@ -191,8 +239,10 @@ def main():
         'data': 'synthetic (reference generators replayed: sparc channel, segmented 16-QAM messages, AWGN)',
         'config': {'workload': f'{args.config}: VAMP Nt={Nt} Nr={Nr} Na={Na} {alph} batch={B} iterations<={iters} '
                                f'EbN0={args.ebn0} dB, one channel per batch',
-                   'global_batch': world * B, 'parallelism': f'trial-shard x{world} (independent epochs)'},
-        'detail': {'T': T, 'ver': ver, 'ser': ser, 'trial_iterations_per_s': world * B * T / (el / args.steps),
+                   'global_batch': world * B, 'parallelism': f'trial-shard x{world} (independent epochs, '
+                                                             'one all-reduce of the error counters)'},
+        'detail': {'T': T, 'ver': ver, 'ser': ser, 'epochs': world * args.steps,
+                   'trial_iterations_per_s': world * B * T / (el / args.steps),
                    'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),

@@ -560,13 +560,14 @@ def g9():
 # ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
+    # (round 2: seeds {0, 1, 2} over EbN0 0-20 step 1 for cfg2-cfg4)
     'cfg1_bamp_qpsk': ('bamp', 4, 1, 8, 100, 'QPSK', 10, list(range(0, 21, 2)), [0, 1]),
-    'cfg2_vamp_16qam': ('vamp', 64, 4, 128, 1024, '16QAM', 20, list(range(0, 21)), [0]),
-    'cfg2_vamp_qpsk': ('vamp', 64, 4, 128, 1024, 'QPSK', 20, list(range(0, 21)), [0, 1]),
-    'cfg3_scamp_16qam': ('scamp', 128, 8, 256, 4096, '16QAM', 20, list(range(0, 21, 2)), [0]),
-    'cfg3_scamp_qpsk': ('scamp', 128, 8, 256, 4096, 'QPSK', 20, list(range(0, 21, 2)), [0]),
-    'cfg4_vamp_16qam': ('vamp', 256, 8, 512, 4096, '16QAM', 20, list(range(0, 21)), [0]),
-    'cfg4_vamp_qpsk': ('vamp', 256, 8, 512, 4096, 'QPSK', 20, list(range(0, 21, 2)), [0]),
+    'cfg2_vamp_16qam': ('vamp', 64, 4, 128, 1024, '16QAM', 20, list(range(0, 21)), [0, 1, 2]),
+    'cfg2_vamp_qpsk': ('vamp', 64, 4, 128, 1024, 'QPSK', 20, list(range(0, 21)), [0, 1, 2]),
+    'cfg3_scamp_16qam': ('scamp', 128, 8, 256, 4096, '16QAM', 20, list(range(0, 21)), [0, 1, 2]),
+    'cfg3_scamp_qpsk': ('scamp', 128, 8, 256, 4096, 'QPSK', 20, list(range(0, 21)), [0, 1, 2]),
+    'cfg4_vamp_16qam': ('vamp', 256, 8, 512, 4096, '16QAM', 20, list(range(0, 21)), [0, 1, 2]),
+    'cfg4_vamp_qpsk': ('vamp', 256, 8, 512, 4096, 'QPSK', 20, list(range(0, 21)), [0, 1, 2]),
 }
 
 

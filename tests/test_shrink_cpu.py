@@ -57,3 +57,17 @@ def test_host_class_surface_and_errors():
     # compute calls need a ROCm tensor: no CPU fallback
     with pytest.raises(ValueError, match='no CPU fallback'):
         S(r, torch.tensor(0.1))
+
+
+@pytest.mark.parametrize('fn', ['bayes', 'shrinkOOK', 'sw_shrinkOOK'])
+@pytest.mark.parametrize('dtype', [torch.float64, torch.complex128])
+def test_shrink_refuses_double_inputs(fn, dtype):
+    """The kernels compute in float32 / complex64; a float64 / complex128 r is refused instead of
+    being returned downcast (the reference would keep float64)."""
+    from config import Config
+    from shrink import Shrink
+    cfg = Config(16, 2, 32, 1, 1, batch=2, generator_mode='sparc', alphabet='QPSK', device='cpu')
+    S = Shrink(cfg, 'shrinkOOK')
+    r = torch.zeros(2, 16, 1, dtype=dtype)
+    with pytest.raises(TypeError):
+        getattr(S, fn)(r, 0.5)
