@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 LIB_PATH = os.path.join(HERE, 'lib', 'libampsparc.so')
 
-AMP_MAX_K = 16
+AMP_MAX_K = 64      # include/amp_sparc.h (K in {1, 2, 4, 8, 16, 64})
 
 
 class AmpConstellation(C.Structure):
@@ -87,9 +87,15 @@ SIGNATURES = {
     'amp_vamp_detect_count': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
+    'amp_bamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
+    'amp_bamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _I, _P]),
+    'amp_bamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_bamp_random_denoise': (C.c_int, [_K, C.c_int64, _P, _P, C.c_float, C.c_float, _P, _P, _P]),
     'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_scamp_run': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
+    'amp_scamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
+    'amp_scamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _I, _P]),
+    'amp_scamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
     'amp_block_denoise': (C.c_int, [_D, _K, _P, _I, C.c_float, _P, _P, _P, _P, C.c_size_t, _P]),
     'amp_block_denoise_workspace_bytes': (C.c_size_t, [_D]),
     'amp_map_decide_count': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, _P, _P, _P, C.c_size_t, _P]),
@@ -107,6 +113,22 @@ SIGNATURES = {
 }
 
 _lib = None
+OPS_PATH = os.path.join(HERE, 'lib', 'libamp_torch_ops.so')
+_ops_loaded = False
+
+
+def torch_ops():
+    """torch.ops.amp — the C ABI registered as PyTorch-ROCm custom ops (csrc/amp_torch_ops.cpp,
+    TORCH_LIBRARY(amp)): vamp_run, bamp_run, scamp_run, block_denoise, map_decide_count.  Only
+    a ROCm device kernel is registered: CPU tensors raise (no CPU fallback)."""
+    global _ops_loaded
+    if not _ops_loaded:
+        if not os.path.exists(OPS_PATH):
+            raise RuntimeError(f'{OPS_PATH} not found: run __graft_entry__.build()')
+        lib()                          # libampsparc.so first (the op library links against it)
+        torch.ops.load_library(OPS_PATH)
+        _ops_loaded = True
+    return torch.ops.amp
 
 
 class AmpError(RuntimeError):

@@ -1,5 +1,13 @@
-"""BAMP detector — drop-in for the reference's ``BAMP`` / ``BAMPLayer`` (bamp.py:12-143),
-running on the gfx950 kernels of libampsparc.so (amp_bamp_run)."""
+"""BAMP detector — drop-in for the reference's ``BAMP`` / ``BAMPLayer`` / ``Tracker``
+(bamp.py:12-143), running on the gfx950 kernels of libampsparc.so.
+
+``BAMP.forward(H, y, SNR, x, symbols, indices) -> Loss`` keeps the reference's signature and
+returns its own reused ``Loss`` (bamp.py:116-143): the iteration loop (amp_bamp_run), the
+allclose early exit and the decision / counters run on the device; the Loss resolves its
+counters lazily, so consecutive epochs queue without a host stall.  The layer-level surface of
+the reference is kept too: ``Tracker(H, y, sigma2, config)`` + ``BAMPLayer.forward(T)``
+(amp_bamp_prepare / amp_bamp_iterate / amp_bamp_finalize).
+"""
 from __future__ import annotations
 
 import ctypes as C
@@ -11,20 +19,102 @@ from torch import nn
 import amp_native as nat
 from config import Config
 from loss import Loss
-from vamp import _c64, block_denoise, read_result
+from vamp import LazyResult, _c64, block_denoise
+
+
+class _Buffers:
+    """Per-shape device buffers reused across forwards (no allocation in steady state)."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, device, B, N, ws_bytes):
+        key = (str(device), B, N, ws_bytes)
+        if key != self.key:
+            self.xmap = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.xmmse = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.var = torch.empty(B, N, dtype=torch.float32, device=device)
+            self.res = torch.zeros(256, dtype=torch.uint8, device=device)     # amp_status @0, amp_counts @64
+            self.ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=device)
+            self.key = key
+        return self
+
+
+class Tracker:
+    """Device state of one BAMP forward (bamp.py:12-25): xmap, xmmse, var and the workspace holding
+    the H, H^H, |H|^2, |H|^2^T operators and z, u, cov of the running iteration."""
+
+    def __init__(self, H, y, sigma2: float, config: Config, bufs: _Buffers | None = None):
+        self.config = config
+        B = config.B
+        n, N = H.shape[-2], H.shape[-1]
+        self.H = _c64(H, (n, N))
+        self.y = _c64(y, (B, n))
+        self.noise_var = sigma2
+        self.dims = config.dims()
+        self.const = config.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_bamp_workspace_bytes(C.byref(self.dims), config.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_bamp_workspace_bytes: invalid dimensions')
+        self.buf = (bufs or _Buffers()).get(self.y.device, B, N, wsb)
+        a = nat.AmpBampArgs()
+        a.H, a.y = nat.dptr(self.H, name='H'), nat.dptr(self.y, name='y')
+        a.max_iter = config.N_Layers
+        a.noise_var = float(sigma2)                                       # bamp.py:124
+        # bamp.py:38-41: 'random' mode denoises element-wise (random_denoiser, bamp.py:79-88)
+        a.denoiser = 1 if config.mode == 'random' else 0
+        a.P0, a.Ps = float(np.float32(config.P0)), float(np.float32(config.Ps))
+        a.xmap, a.xmmse, a.var = nat.dptr(self.buf.xmap), nat.dptr(self.buf.xmmse), nat.dptr(self.buf.var)
+        a.status = nat.dptr(self.buf.res)
+        a.ws, a.ws_bytes = nat.dptr(self.buf.ws), self.buf.ws.numel()
+        self.args = a
+        self.stream = nat.stream_ptr(self.y.device)
+
+    @property
+    def xmap(self):
+        return self.buf.xmap.view(self.config.B, -1, 1)
+
+    @property
+    def xmmse(self):
+        return self.buf.xmmse.view(self.config.B, -1, 1)
+
+    @property
+    def var(self):
+        return self.buf.var.view(self.config.B, -1, 1)
+
+    def _call(self, fn, *extra):
+        nat.check(getattr(nat.lib(), fn)(C.byref(self.dims), C.byref(self.const), C.byref(self.args), *extra,
+                                         self.stream), fn)
+
+    def prepare(self):
+        self._call('amp_bamp_prepare')
+
+    def finalize(self):
+        self._call('amp_bamp_finalize')
+
+    def status(self) -> nat.AmpStatus:
+        res = getattr(self, 'res', None)
+        res = self.buf.res if res is None else res
+        return nat.AmpStatus.from_buffer_copy(res[:C.sizeof(nat.AmpStatus)].cpu().numpy().tobytes())
 
 
 class BAMPLayer(nn.Module):
-    """BAMPLayer (bamp.py:27-64); its denoiser is the per-element-tau block denoiser."""
+    """BAMPLayer (bamp.py:27-64): forward(T) is one iteration on the device (a no-op once the
+    early exit of bamp.py:140 has fired); its denoiser is the per-element-tau block denoiser."""
 
-    def __init__(self, config: Config) -> None:
+    def __init__(self, config: Config, index: int = 0) -> None:
         super().__init__()
         self.config = config
+        self.index = index
         self.Nt, self.Na, self.Lin, self.B = config.Nt, config.Na, config.Lin, config.B
         self.K = config.K
         self.M = self.Nt // self.Na
         self.L = self.Na * self.Lin
         self.LM = self.L * self.M
+
+    def forward(self, T: Tracker) -> None:
+        T._call('amp_bamp_iterate', self.index)
 
     def segmented_denoiser(self, s: torch.Tensor, tau: torch.Tensor):
         """bamp.py:66-77: tau is cov, halved inside (tau = cov/2)."""
@@ -50,54 +140,48 @@ class BAMPLayer(nn.Module):
         return self.random_denoiser if self.config.mode == 'random' else self.segmented_denoiser
 
 
-class BAMP(nn.Module):
+class BAMP(LazyResult, nn.Module):
     def __init__(self, config: Config) -> None:
         super().__init__()
         self.config = config
         self.E = config.Na / config.Nr                                    # bamp.py:102
-        self.layers = nn.ModuleList([BAMPLayer(config) for _ in range(config.N_Layers)])
+        self.layers = nn.ModuleList([BAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
-        self._key = None
+        self._bufs = _Buffers()
         self.last = None
 
-    def _ensure_buffers(self, dev, B, N, wsb):
-        key = (str(dev), B, N, wsb)
-        if key != self._key:
-            self.xmap = torch.empty(B, N, dtype=torch.complex64, device=dev)
-            self.xmmse = torch.empty(B, N, dtype=torch.complex64, device=dev)
-            self.var = torch.empty(B, N, dtype=torch.float32, device=dev)
-            self.res = torch.zeros(256, dtype=torch.uint8, device=dev)
-            self.ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
-            self._key = key
+    # buffers of the last forward (the Tracker's), for callers that read them directly
+    @property
+    def xmap(self):
+        return self._bufs.xmap
 
-    def detect(self, H: torch.Tensor, y: torch.Tensor, SNR: float):
-        cfg = self.config
-        B = cfg.B
-        n, N = H.shape[-2], H.shape[-1]
-        H = _c64(H, (n, N))
-        y = _c64(y, (B, n))
-        d, c = cfg.dims(), cfg.constellation()
-        lib = nat.lib()
-        wsb = lib.amp_bamp_workspace_bytes(C.byref(d), cfg.N_Layers)
-        self._ensure_buffers(y.device, B, N, wsb)
-        a = nat.AmpBampArgs()
-        a.H, a.y = nat.dptr(H, name='H'), nat.dptr(y, name='y')
-        a.max_iter = cfg.N_Layers
-        a.noise_var = float(self.E / SNR)                                 # bamp.py:124
-        # bamp.py:38-41: 'random' mode denoises element-wise (random_denoiser, bamp.py:79-88)
-        a.denoiser = 1 if cfg.mode == 'random' else 0
-        a.P0, a.Ps = float(np.float32(cfg.P0)), float(np.float32(cfg.Ps))
-        a.xmap, a.xmmse, a.var = nat.dptr(self.xmap), nat.dptr(self.xmmse), nat.dptr(self.var)
-        a.status = nat.dptr(self.res)
-        a.ws, a.ws_bytes = nat.dptr(self.ws), self.ws.numel()
-        self._keep = (H, y)
-        nat.check(lib.amp_bamp_run(C.byref(d), C.byref(c), C.byref(a), nat.stream_ptr(y.device)), 'amp_bamp_run')
+    @property
+    def xmmse(self):
+        return self._bufs.xmmse
+
+    @property
+    def var(self):
+        return self._bufs.var
+
+    def detect(self, H: torch.Tensor, y: torch.Tensor, SNR: float) -> Tracker:
+        """All iterations on the device, asynchronous (no host sync)."""
+        with torch.cuda.device(y.device):
+            T = Tracker(H, y, self.E / SNR, self.config, self._bufs)
+            T._call('amp_bamp_run')
+        self._keep = T
+        return T
 
     def forward(self, H: torch.Tensor, y: torch.Tensor, SNR: float, x: torch.Tensor, symbols, indices) -> Loss:
-        self.detect(H, y, SNR)
-        self.L.dump()                                                     # bamp.py:125
-        self.L.device_counts(self.xmap, self.xmmse, x, symbols, indices, out=self.res[64:])   # bamp.py:142
-        status, counts = read_result(self.res)
-        self.L.record(self.L.rates_from_counts(counts), int(status.T))
-        self.last = status
+        """bamp.py:116-143; the counters resolve lazily (see LazyResult)."""
+        with torch.cuda.device(y.device):
+            T = Tracker(H, y, self.E / SNR, self.config, self._bufs)
+            res, host = self._result_slot(T.y.device)
+            T.res = res
+            T.args.status = nat.dptr(res)
+            T._call('amp_bamp_run')
+            # decision on T.xmap (bamp.py:142); counters next to the status record
+            self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbols, indices, out=res[64:])
+            self._arm(self.L, res, host, 'amp_bamp_run')                  # + L.dump(), bamp.py:125
+        self._keep = T
+        self.last = T
         return self.L

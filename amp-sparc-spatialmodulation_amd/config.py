@@ -130,6 +130,41 @@ class Config:
             self._const_memo = memo
         return memo[1]
 
+    def inject_square_qam(self, K: int = 64) -> 'Config':
+        """Square K-QAM (unit mean power, per-axis binary-reflected gray code) in place of the
+        constructed alphabet — BASELINE cfg5's 64-QAM, which the reference's Config rejects
+        (config.py:44).  Same injection as tests/golden/make_goldens.py applies to the reference's
+        Config: every attribute the constellation feeds is re-derived as
+        config.py:117-157 would.  Call it before building Data / Loss / detectors."""
+        m = int(round(np.sqrt(K)))
+        if m * m != K or m & (m - 1):
+            raise ValueError(f'square QAM needs K = 4^j, got {K}')
+        b = int(np.log2(m))
+        levels = np.arange(-(m - 1), m, 2)
+        g1 = [i ^ (i >> 1) for i in range(m)]
+        pts = [complex(levels[i], levels[q]) for i in range(m) for q in range(m)]
+        self.symbols = np.array(pts) / np.sqrt(np.mean(np.abs(pts) ** 2))
+        self.gray = [(g1[i] << b) | g1[q] for i in range(m) for q in range(m)]
+        self.alphabet = f'{K}QAM'
+        self.K = K
+        self.symbol_bits = int(np.log2(K))
+        self.Ps = self.sparsity / K
+        self.is_complex = True
+        if self.mode == 'sparc':
+            self.inner_code_rate = self.Na * np.log2(self.M * self.K) / self.Mr
+            self.code_rate = self.Lc * self.inner_code_rate / self.Lr
+        else:
+            self.info_bits = self.symbol_bits + self.index_bits
+            self.code_rate = self.Lin * self.info_bits / self.Nr / self.Lout
+        with np.errstate(divide='ignore'):
+            self.min_amp_snr = 1 / (self.kappa * (1 / (np.exp(2 * self.code_rate) - 1) - 1 / self.Lh))
+        self.min_snr = 2 ** self.code_rate - 1
+        self.min_snr_dB = 10 * np.log10(self.min_snr)
+        self.shannon_limit_dB = self.min_snr_dB - 10 * np.log10(self.code_rate)
+        self.name = (f'{self.alphabet},{self.mode}/{self.profile},{self.trunc}/'
+                     f'Nt={self.Nt},Na={self.Na},Nr={self.Nr},Lh={self.Lh},Lin={self.Lin}')
+        return self
+
     def snr(self, EbN0dB: float) -> float:
         """Linear SNR of an EbN0 point as the drivers compute it (vamp_model.py:50-54)."""
         return 10 ** ((EbN0dB + 10 * np.log10(self.code_rate)) / 10)

@@ -50,25 +50,25 @@ struct BampK {
     Const c;
     int elementwise;                       // random_denoiser (bamp.py:79-88) instead of the block one
     float P0, Ps;
-    double sre[AMP_MAX_K], sim[AMP_MAX_K]; // torch.tensor(config.symbols): complex128 (bamp.py:37)
 };
 
 // BAMPLayer.random_denoiser (bamp.py:79-88) for one entry, in the reference's dtypes: G(0) in
 // float32 (r - 0 stays complex64), G(a_k) in float64 (complex64 - complex128), norm / exp / var
 // in float64 (the float32 prior scalars promoted), complex128 / float64 as a reciprocal multiply.
-__device__ __forceinline__ void bamp_bayes_elem(const BampK& P, float rr, float ri, float cov, float& xr, float& xi,
-                                                float& var) {
+// c64: torch.tensor(config.symbols), complex128 (bamp.py:37).
+__device__ __forceinline__ void bamp_bayes_elem(const BampK& P, const Const64& c64, float rr, float ri, float cov,
+                                                float& xr, float& xi, float& var) {
     const float a0 = hypotf(rr, ri);
     const float g0 = expf(-(a0 * a0) / cov);
     const double cd = (double)cov;
     double gs = 0.0, sr = 0.0, si = 0.0, s2 = 0.0;
-    for (int k = 0; k < P.c.K; ++k) {
-        const double a = hypot((double)rr - P.sre[k], (double)ri - P.sim[k]);
+    for (int k = 0; k < c64.K; ++k) {
+        const double a = hypot((double)rr - c64.re[k], (double)ri - c64.im[k]);
         const double g = exp(-(a * a) / cd);
-        const double ak = hypot(P.sre[k], P.sim[k]);
+        const double ak = hypot(c64.re[k], c64.im[k]);
         gs += g;
-        sr += P.sre[k] * g;
-        si += P.sim[k] * g;
+        sr += c64.re[k] * g;
+        si += c64.im[k] * g;
         s2 += (ak * ak) * g;
     }
     double norm = (double)(P.P0 * g0) + (double)P.Ps * gs;
@@ -216,7 +216,7 @@ struct BampDenoisePolicy {
 
 // xmap = xmmse + cov (H^H s) ; xmmse, var = denoiser(xmap, cov/2)   (bamp.py:63-64)
 template <int BN, int KK>
-__global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
+__global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     using C = GemmCfg<BN>;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, int t) {
                 const size_t o = (size_t)(row0 + rho) * P.N + col0 / 2 + cc;
                 const float2 v = *reinterpret_cast<const float2*>(lds + rho * C::LDC + 2 * cc);
                 float xr, xi, var;
-                bamp_bayes_elem(P, v.x, v.y, P.cov[o], xr, xi, var);
+                bamp_bayes_elem(P, c64, v.x, v.y, P.cov[o], xr, xi, var);
                 *reinterpret_cast<float2*>(P.xm + 2 * o) = make_float2(xr, xi);
                 vn[o] = var;
                 pa.sumvar += (double)var;
@@ -366,20 +366,23 @@ static int bamp_kb2_attrs() {
 }
 
 template <int KK>
-static void launch_kb2_kk(const BampK& P, int gr, int t, hipStream_t st) {
+static void launch_kb2_kk(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
     if (P.bn == 128)
-        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P,
+                           c64, t);
     else
-        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P, t);
+        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P,
+                           c64, t);
 }
 
-static void launch_kb2(const BampK& P, int gr, int t, hipStream_t st) {
+static void launch_kb2(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
     switch (P.c.K) {
-    case 1: launch_kb2_kk<1>(P, gr, t, st); break;
-    case 2: launch_kb2_kk<2>(P, gr, t, st); break;
-    case 4: launch_kb2_kk<4>(P, gr, t, st); break;
-    case 8: launch_kb2_kk<8>(P, gr, t, st); break;
-    default: launch_kb2_kk<16>(P, gr, t, st); break;
+    case 1: launch_kb2_kk<1>(P, c64, gr, t, st); break;
+    case 2: launch_kb2_kk<2>(P, c64, gr, t, st); break;
+    case 4: launch_kb2_kk<4>(P, c64, gr, t, st); break;
+    case 8: launch_kb2_kk<8>(P, c64, gr, t, st); break;
+    case 16: launch_kb2_kk<16>(P, c64, gr, t, st); break;
+    default: launch_kb2_kk<64>(P, c64, gr, t, st); break;
     }
 }
 
@@ -396,6 +399,7 @@ static int bamp_attrs() {
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<4>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<8>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<16>();
+        if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<64>();
     });
     return g_bamp_rc;
 }
@@ -411,7 +415,12 @@ size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter) {
     return bamp_carve(d, max_iter, nullptr).bytes;
 }
 
-int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
+}  // extern "C"
+
+namespace amp {
+
+// The parameter block of one BAMP forward from the C-ABI arguments (validated).
+static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, BampK& P, Const64& c64) {
     int rc = check_dims(d, c);
     if (rc) return rc;
     AMP_REQUIRE(a && a->H && a->y && a->xmap && a->xmmse && a->var && a->status && a->ws,
@@ -422,7 +431,6 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_bamp_run: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
     rc = bamp_attrs();
     if (rc) return rc;
-    BampK P;
     bamp_geometry(d, P);
     P.max_iter = a->max_iter;
     P.sigma2 = (float)a->noise_var;
@@ -435,12 +443,13 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     P.elementwise = a->denoiser;
     P.P0 = a->P0;
     P.Ps = a->Ps;
-    for (int k = 0; k < AMP_MAX_K; ++k) {
-        P.sre[k] = k < c->K ? c->re64[k] : 0.0;
-        P.sim[k] = k < c->K ? c->im64[k] : 0.0;
-    }
-    const Const64 c64 = to_const64(c);
-    hipStream_t st = (hipStream_t)stream;
+    c64 = to_const64(c);
+    return AMP_OK;
+}
+
+// Tracker (bamp.py:13-25): the four weights and the initial state.
+static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t st) {
+    int rc;
     const float2* H = (const float2*)a->H;
     // weights, once per forward (Tracker: adj, abs2, abs2T, bamp.py:17-19)
     if ((rc = build_abs2_weight(H, P.N, 1, P.n, P.N, (float*)P.Wabs2, P.kapA1, P.ncpA1, st))) return rc;
@@ -451,28 +460,76 @@ int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_a
     const int g = (int)std::min<size_t>((tot + 255) / 256, 2048);
     hipLaunchKernelGGL(bamp_init_kernel, dim3(g), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("bamp_init");
+    return AMP_OK;
+}
+
+// One BAMPLayer.forward (bamp.py:48-64) + the allclose test of bamp.py:140 (no-op once stopped).
+static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStream_t st) {
     const int gr = cdiv(P.B, GBM);
-    for (int t = 0; t < P.max_iter; ++t) {
-        hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        launch_kb2(P, gr, t, st);
-        hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
-        AMP_LAUNCH_CHECK("bamp iteration");
-    }
+    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_kb2(P, c64, gr, t, st);
+    hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("bamp iteration");
+    return AMP_OK;
+}
+
+// the caller's var holds the last executed iteration's (ping-pong buffers)
+static int bamp_finalize_impl(const BampK& P, hipStream_t st) {
     hipLaunchKernelGGL(bamp_output_kernel, dim3((int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048)),
                        dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("bamp_output");
     return AMP_OK;
 }
 
+}  // namespace amp
+
+extern "C" {
+
+int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
+    BampK P;
+    Const64 c64;
+    int rc = bamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = bamp_prepare_impl(P, a, st))) return rc;
+    for (int t = 0; t < P.max_iter; ++t)
+        if ((rc = bamp_iterate_impl(P, c64, t, st))) return rc;
+    return bamp_finalize_impl(P, st);
+}
+
+int amp_bamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
+    BampK P;
+    Const64 c64;
+    int rc = bamp_setup(d, c, a, P, c64);
+    return rc ? rc : bamp_prepare_impl(P, a, (hipStream_t)stream);
+}
+
+int amp_bamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, int32_t t, void* stream) {
+    BampK P;
+    Const64 c64;
+    int rc = bamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(t >= 0 && t < a->max_iter, "amp_bamp_iterate: t = %d outside [0, %d)", t, a->max_iter);
+    return bamp_iterate_impl(P, c64, t, (hipStream_t)stream);
+}
+
+int amp_bamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
+    BampK P;
+    Const64 c64;
+    int rc = bamp_setup(d, c, a, P, c64);
+    return rc ? rc : bamp_finalize_impl(P, (hipStream_t)stream);
+}
+
 // BAMPLayer.random_denoiser (bamp.py:79-88) as a standalone element-wise op (layer-level API).
-__global__ __launch_bounds__(AMP_WG) void bamp_random_denoise_kernel(BampK P, long long count, const float2* r,
-                                                                     const float* cov, float2* xm, float* var) {
+__global__ __launch_bounds__(AMP_WG) void bamp_random_denoise_kernel(BampK P, Const64 c64, long long count,
+                                                                     const float2* r, const float* cov, float2* xm,
+                                                                     float* var) {
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < count;
          e += (long long)gridDim.x * blockDim.x) {
         float xr, xi, v;
-        bamp_bayes_elem(P, r[e].x, r[e].y, cov[e], xr, xi, v);
+        bamp_bayes_elem(P, c64, r[e].x, r[e].y, cov[e], xr, xi, v);
         xm[e] = make_float2(xr, xi);
         var[e] = v;
     }
@@ -480,7 +537,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_random_denoise_kernel(BampK P, lo
 
 int amp_bamp_random_denoise(const amp_constellation* c, int64_t count, const void* r, const void* cov, float P0,
                             float Ps, void* xmmse, void* var, void* stream) {
-    AMP_REQUIRE(c && c->K >= 1 && c->K <= AMP_MAX_K, "amp_bamp_random_denoise: bad constellation");
+    AMP_REQUIRE(c && c->K >= 1 && c->K <= AMP_MAX_K, "amp_bamp_random_denoise: bad constellation size %d",
+                c ? c->K : 0);
     AMP_REQUIRE(count >= 0, "amp_bamp_random_denoise: count < 0");
     if (count == 0) return AMP_OK;
     AMP_REQUIRE(r && cov && xmmse && var, "amp_bamp_random_denoise: null pointer argument");
@@ -488,12 +546,9 @@ int amp_bamp_random_denoise(const amp_constellation* c, int64_t count, const voi
     P.c = to_const(c);
     P.P0 = P0;
     P.Ps = Ps;
-    for (int k = 0; k < AMP_MAX_K; ++k) {
-        P.sre[k] = k < c->K ? c->re64[k] : 0.0;
-        P.sim[k] = k < c->K ? c->im64[k] : 0.0;
-    }
+    const Const64 c64 = to_const64(c);
     const int g = (int)std::max(1LL, std::min(((long long)count + AMP_WG - 1) / AMP_WG, 8192LL));
-    hipLaunchKernelGGL(bamp_random_denoise_kernel, dim3(g), dim3(AMP_WG), 0, (hipStream_t)stream, P, (long long)count,
+    hipLaunchKernelGGL(bamp_random_denoise_kernel, dim3(g), dim3(AMP_WG), 0, (hipStream_t)stream, P, c64, (long long)count,
                        (const float2*)r, (const float*)cov, (float2*)xmmse, (float*)var);
     AMP_LAUNCH_CHECK("bamp_random_denoise");
     return AMP_OK;

@@ -17,12 +17,21 @@
 
 namespace amp {
 
-struct DecConst {
-    int K, sbits;
-    double re[AMP_MAX_K], im[AMP_MAX_K];
-    float re32[AMP_MAX_K], im32[AMP_MAX_K];   // complex64 casts of the points (xhat values)
-    int gray[AMP_MAX_K];
+// The decision's constellation: the float64 points (a Const64, shared with the exact rare path
+// of the fused kernels, so a kernel needs only this one table), their complex64 casts and the
+// gray labels.  Passed by value (kernel arguments, read through the scalar cache).
+struct DecConst : Const64 {
+    int sbits;
     float amax;                                // max_k max(|re_k|, |im_k|) (prefilter bound)
+    float re32[AMP_MAX_K], im32[AMP_MAX_K];   // complex64 casts of the points (xhat values)
+    unsigned char gray[AMP_MAX_K];            // gray label of point k (< 64)
+};
+
+// Unroll factor of the loops over the constellation: complete for K <= 16; chunks of 8 for
+// 64-QAM, whose 128 uniform operands would not fit the scalar register file at once.
+template <int KK>
+struct KUnroll {
+    static constexpr int value = KK > 16 ? 8 : KK;
 };
 
 struct alignas(16) DecPart {
@@ -72,7 +81,8 @@ __device__ __forceinline__ void section_tail(const DecConst& c, int M, int g, co
     constexpr int K = KK;
     const int mh = bi / K, kh = bi - mh * K;
     float ar = 0.f, ai = 0.f;
-#pragma unroll
+    constexpr int KU = KUnroll<KK>::value;
+#pragma unroll KU
     for (int k = 0; k < K; ++k)
         if (k == kh) { ar = c.re32[k]; ai = c.im32[k]; }
     int mm = 0;
@@ -127,7 +137,8 @@ __device__ __forceinline__ void decide_section_seg(const DecConst& c, int M, int
     ld(bm, xs, xt, xe);
     double d = INFINITY;
     int kh = 0;
-#pragma unroll
+    constexpr int KU = KUnroll<KK>::value;
+#pragma unroll KU
     for (int k = 0; k < K; ++k) {
         const double ds = hypot((double)xs.x - c.re[k], (double)xs.y - c.im[k]);
         if (ds < d) { d = ds; kh = k; }
@@ -154,6 +165,7 @@ template <int KK, int G, bool PF, class LD>
 __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, const LD& ld, int& bi_out, int& mm_out,
                                                double& se_out) {
     constexpr int K = KK;
+    constexpr int KU = KUnroll<KK>::value;
     bool full = true;
     float thr = 0.f;
     int ncand = 0, first = 0x7fffffff;
@@ -165,7 +177,7 @@ __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, 
             ld(m, xv, xt, xe);
             bad |= !(fabsf(xv.x) <= FLT_MAX && fabsf(xv.y) <= FLT_MAX);
             xs = fmaxf(xs, fabsf(xv.x) + fabsf(xv.y));
-#pragma unroll
+#pragma unroll KU
             for (int k = 0; k < K; ++k) vmax = fmaxf(vmax, fmaf(xv.x, c.re32[k], xv.y * c.im32[k]));
         }
         vmax = dec_group_reduce<G>(vmax, [](float a, float b) { return fmaxf(a, b); });
@@ -176,7 +188,7 @@ __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, 
             for (int m = g; m < M; m += G) {
                 float2 xv, xt, xe;
                 ld(m, xv, xt, xe);
-#pragma unroll
+#pragma unroll KU
                 for (int k = 0; k < K; ++k) {
                     const bool cand = fmaf(xv.x, c.re32[k], xv.y * c.im32[k]) >= thr;
                     first = (cand && first == 0x7fffffff) ? m * K + k : first;
@@ -197,7 +209,7 @@ __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, 
             float2 xv, xt, xe;
             ld(m, xv, xt, xe);
             const double xr = (double)xv.x, xi = (double)xv.y;
-#pragma unroll
+#pragma unroll KU
             for (int k = 0; k < K; ++k) {
                 if (!PF || full || fmaf(xv.x, c.re32[k], xv.y * c.im32[k]) >= thr) {
                     const double v = __fma_rn(xr, c.re[k], __dmul_rn(xi, c.im[k]));
@@ -219,16 +231,18 @@ __device__ __forceinline__ void decide_section(const DecConst& c, int M, int g, 
 }
 
 // Counter contributions of one decided section s (global section index b * L + l).
+template <int KK>
 __device__ __forceinline__ void count_section(const DecConst& c, long long s, int M, int L, int Na, int Lin, int bi,
                                               double se, long long sym, long long idx, long long ibmask,
                                               DecPart& q) {
-    const int K = c.K;
+    constexpr int K = KK;
+    constexpr int KU = KUnroll<KK>::value;
     const int mh = bi / K, kh = bi - mh * K;
     const long long sbmask = (1LL << c.sbits) - 1;
     const long long ih = s * M + mh;           // flat index of the chosen entry
     long long sh = 0;
-#pragma unroll
-    for (int k = 0; k < AMP_MAX_K; ++k)
+#pragma unroll KU
+    for (int k = 0; k < K; ++k)
         if (k == kh) sh = c.gray[k];
     q.ier += (ih != idx);
     q.ser += (sh != sym);
@@ -245,14 +259,16 @@ __device__ __forceinline__ void count_section(const DecConst& c, long long s, in
 __host__ inline DecConst to_decconst(const amp_constellation* c) {
     DecConst d;
     d.K = c->K;
+    d.real_alpha = 1;
     d.sbits = c->symbol_bits;
     for (int i = 0; i < AMP_MAX_K; ++i) {
         const bool v = i < c->K;
         d.re[i] = v ? c->re64[i] : 0.0;
         d.im[i] = v ? c->im64[i] : 0.0;
+        if (v && c->im64[i] != 0.0) d.real_alpha = 0;
         d.re32[i] = v ? (float)c->re64[i] : 0.f;
         d.im32[i] = v ? (float)c->im64[i] : 0.f;
-        d.gray[i] = v ? c->gray[i] : 0;
+        d.gray[i] = v ? (unsigned char)c->gray[i] : 0;
     }
     double am = 0.0;
     for (int i = 0; i < c->K; ++i) am = fmax(am, fmax(fabs(c->re64[i]), fabs(c->im64[i])));

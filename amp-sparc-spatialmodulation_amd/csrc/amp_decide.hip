@@ -63,7 +63,7 @@ __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
         if (act && g == 0) {
             P.mism[s] = (unsigned char)mm;
             if (P.dec) P.dec[s] = bi;
-            count_section(P.c, s, M, P.L, P.Na, P.Lin, bi, se, P.sym[s], P.idx[s], ibmask, q);
+            count_section<KK>(P.c, s, M, P.L, P.Na, P.Lin, bi, se, P.sym[s], P.idx[s], ibmask, q);
         }
     }
     long long ier = q.ier, ser = q.ser, iber = q.iber, sber = q.sber;
@@ -101,6 +101,7 @@ __device__ __forceinline__ bool rnd_greater(bool n1, float v1, int m1, bool n2, 
 template <int KK>
 __global__ __launch_bounds__(AMP_WG) void random_decide_kernel(DecK P, int Nt, int R) {
     constexpr int K = KK;
+    constexpr int KU = KUnroll<KK>::value;
     DecPart q = decpart_zero();
     const long long ibmask = dec_ibmask(P.ibits);
     const long long sbmask = (1LL << P.c.sbits) - 1;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(AMP_WG) void random_decide_kernel(DecK P, int Nt, i
             const double xr = (double)xm[m].x, xi = (double)xm[m].y;
             double d = INFINITY;
             int kh = 0;
-#pragma unroll
+#pragma unroll KU
             for (int k = 0; k < K; ++k) {
                 const double ds = hypot(xr - P.c.re[k], xi - P.c.im[k]);
                 if (ds < d) { d = ds; kh = k; }
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(AMP_WG) void random_decide_kernel(DecK P, int Nt, i
             const long long e = (long long)row * P.Na + j;
             const long long ih = (long long)row * Nt + m;
             long long sh = 0;
-#pragma unroll
+#pragma unroll KU
             for (int k = 0; k < K; ++k)
                 if (k == kh) sh = P.c.gray[k];
             q.ier += (ih != P.idx[e]);
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(AMP_WG) void random_decide_kernel(DecK P, int Nt, i
             for (int j = 0; j < P.Na; ++j)
                 if (pos[j] / K == m) {
                     const int kh = pos[j] - m * K;
-#pragma unroll
+#pragma unroll KU
                     for (int k = 0; k < K; ++k)
                         if (k == kh) { hr = P.c.re32[k]; hi = P.c.im32[k]; }
                 }
@@ -267,7 +268,8 @@ static void launch_decide(const DecK& P, int M, hipStream_t st) {
     case 2: launch_decide_k<2>(P, M, st); break;
     case 4: launch_decide_k<4>(P, M, st); break;
     case 8: launch_decide_k<8>(P, M, st); break;
-    default: launch_decide_k<16>(P, M, st); break;
+    case 16: launch_decide_k<16>(P, M, st); break;
+    default: launch_decide_k<64>(P, M, st); break;     // check_dims: K in {1, 2, 4, 8, 16, 64}
     }
 }
 
@@ -330,7 +332,8 @@ int amp_random_decide_count(const amp_dims* d, const amp_constellation* c, const
                             const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
                             void* decisions, void* ws, size_t ws_bytes, void* stream) {
     AMP_REQUIRE(d && c && d->B > 0 && d->Nt > 0 && d->Lin > 0 && d->Na >= 1 && d->Na <= AMP_DEC_MAX_NA &&
-                    d->Na <= d->Nt && d->L == d->Na * d->Lin && c->K >= 1 && c->K <= AMP_MAX_K,
+                    d->Na <= d->Nt && d->L == d->Na * d->Lin && c->K >= 1 && c->K <= AMP_MAX_K &&
+                    is_pow2(c->K) && c->K != 32,
                 "amp_random_decide_count: bad dims (Na <= %d)", AMP_DEC_MAX_NA);
     AMP_REQUIRE(xmap && xmmse && x && sym && idx && counts && ws, "amp_random_decide_count: null pointer argument");
     AMP_REQUIRE(ws_bytes >= amp_map_decide_workspace_bytes(d), "amp_random_decide_count: workspace too small");
@@ -356,7 +359,8 @@ int amp_random_decide_count(const amp_dims* d, const amp_constellation* c, const
     case 2: hipLaunchKernelGGL(random_decide_kernel<2>, g, b, 0, st, P, d->Nt, R); break;
     case 4: hipLaunchKernelGGL(random_decide_kernel<4>, g, b, 0, st, P, d->Nt, R); break;
     case 8: hipLaunchKernelGGL(random_decide_kernel<8>, g, b, 0, st, P, d->Nt, R); break;
-    default: hipLaunchKernelGGL(random_decide_kernel<16>, g, b, 0, st, P, d->Nt, R); break;
+    case 16: hipLaunchKernelGGL(random_decide_kernel<16>, g, b, 0, st, P, d->Nt, R); break;
+    default: hipLaunchKernelGGL(random_decide_kernel<64>, g, b, 0, st, P, d->Nt, R); break;
     }
     AMP_LAUNCH_CHECK("random_decide");
     hipLaunchKernelGGL(map_count_kernel, dim3(1), dim3(1024), 0, st, P);

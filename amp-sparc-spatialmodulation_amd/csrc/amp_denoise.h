@@ -30,11 +30,18 @@ namespace amp {
 
 #define AMP_LOG2E 1.44269504088896340736f
 
+// A uniform kernel-argument value taken through readfirstlane: the loads stay scalar loads of
+// the kernarg segment (left alone, memcpyopt merged consecutive constellation loads into a copy
+// of c.re into a private array, i.e. scratch memory, once Const held 64 points).
+__device__ __forceinline__ float kval(const float& x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
 // Policy interface (per lane; `sec` is the caller's local section id):
 //   void load(int sec, int m, float& rr, float& ri, float& inv_tau) const;
 //   void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const;
 //   void section(int sec, float secmax, float secabs) const;     // group lane 0
-// KK: the constellation size as a compile-time constant (1, 2, 4, 8 or 16).
+// KK: the constellation size as a compile-time constant (1, 2, 4, 8, 16 or 64).
 //
 // M <= 64 form (G = M lanes per section, compile-time): one position per lane, U sections
 // per lane group in flight (independent dependency chains for the scheduler).  Everything is
@@ -52,7 +59,7 @@ __device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const
     float cre[KK], cim[KK];
 #pragma unroll
     for (int k = 0; k < KK; ++k) {
-        cre[k] = c.re[k]; cim[k] = c.im[k];
+        cre[k] = kval(c.re[k]); cim[k] = kval(c.im[k]);
         asm volatile("" : "+v"(cre[k]), "+v"(cim[k]));
     }
     float st_abs = 0.f, st_min = INFINITY;
@@ -142,13 +149,13 @@ struct DenRegs {
     __device__ __forceinline__ void load(const Const& c) {
 #pragma unroll
         for (int h = 0; h < KK / 2; ++h) {
-            pre[h] = f32x2{c.re[2 * h], c.re[2 * h + 1]};
-            pim[h] = f32x2{c.im[2 * h], c.im[2 * h + 1]};
+            pre[h] = f32x2{kval(c.re[2 * h]), kval(c.re[2 * h + 1])};
+            pim[h] = f32x2{kval(c.im[2 * h]), kval(c.im[2 * h + 1])};
             asm volatile("" : "+v"(pre[h]), "+v"(pim[h]));
         }
 #pragma unroll
         for (int k = 0; k < KK; ++k) {
-            sym[k] = f32x2{c.re[k], c.im[k]};
+            sym[k] = f32x2{kval(c.re[k]), kval(c.im[k])};
             asm volatile("" : "+v"(sym[k]));
         }
     }
@@ -286,8 +293,101 @@ __device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M
     }
 }
 
+// 64-QAM form (KK > 16): the same arithmetic per element as denoise_sections_g, but the 64
+// points are streamed from the scalar cache in chunks of 8 (rolled loop: 128 uniform operands
+// do not fit the scalar register file) and nothing per point is kept in registers — the
+// logits are re-formed in each of the three passes (max, exp sums, variance) and the
+// variance pass recomputes exp(xi - max): the same bits as the first exp (2 x 64 v_exp_f32
+// per position instead of 64, against 5 GEMM launches per iteration at cfg5).
+// One position per lane (G = M <= 64 lanes per section).
+template <bool kVar, int KK, int G, class P>
+__device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    static_assert(KK % 8 == 0, "chunks of 8 points");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    const int nw = blockDim.x >> 6;
+    DenStat S;
+    for (int base = wave * gpw; base < nsec; base += nw * gpw) {   // wave-uniform trip count
+        const int sec = base + gid;
+        const bool act = sec < nsec;
+        float rr, ri, it;
+        pol.load(act ? sec : nsec - 1, g, rr, ri, it);
+        const float ur = rr * it, ui = ri * it;   // c64 / f32 == multiply by the reciprocal
+        if (act) S.st_bad |= !(fabsf(ur) <= FLT_MAX && fabsf(ui) <= FLT_MAX);
+        float lmax = -FLT_MAX, lmin = FLT_MAX;
+#pragma unroll 1
+        for (int k0 = 0; k0 < KK; k0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = fmaf(ur, c.re[k0 + j], ui * c.im[k0 + j]);
+                lmax = fmaxf(lmax, x);
+                lmin = fminf(lmin, x);
+            }
+        }
+        const float smax = group_fmax_c<G>(lmax), sabs = group_fmax_c<G>(fmaxf(lmax, -lmin));
+        float zm = 0.f, a = 0.f, b = 0.f;
+#pragma unroll 1
+        for (int k0 = 0; k0 < KK; k0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float cr = c.re[k0 + j], ci = c.im[k0 + j];
+                const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
+                zm += e;
+                a = fmaf(cr, e, a);
+                b = fmaf(ci, e, b);
+            }
+        }
+        float zt = zm, ze = 0.f;
+        group_sum_excl_c<G>(zt, ze);
+        const float iz = __builtin_amdgcn_rcpf(zt);
+        const float xr = a * iz, xi = b * iz;
+        float var = 0.f;
+        if (kVar) {
+            float vs = 0.f;
+#pragma unroll 1
+            for (int k0 = 0; k0 < KK; k0 += 8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float cr = c.re[k0 + j], ci = c.im[k0 + j];
+                    const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
+                    const float dr = xr - cr, di = xi - ci;
+                    vs = fmaf(fmaf(dr, dr, di * di), e, vs);
+                }
+            }
+            var = (xr * xr + xi * xi) * (ze * iz) + vs * iz;
+        }
+        if (act) {
+            pol.store(sec, g, xr, xi, var, pa);
+            S.st_abs = nan_max(S.st_abs, sabs);
+            S.st_min = nan_min(S.st_min, smax);
+            if (g == 0) pol.section(sec, smax, sabs);
+        }
+    }
+    S.fold(pa);
+}
+
+template <bool kVar, int KK, class P>
+__device__ __forceinline__ void denoise_sections_wide_m(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+    switch (M) {
+    case 64: denoise_sections_wide<kVar, KK, 64>(pol, nsec, c, pa); break;
+    case 32: denoise_sections_wide<kVar, KK, 32>(pol, nsec, c, pa); break;
+    case 16: denoise_sections_wide<kVar, KK, 16>(pol, nsec, c, pa); break;
+    case 8: denoise_sections_wide<kVar, KK, 8>(pol, nsec, c, pa); break;
+    case 4: denoise_sections_wide<kVar, KK, 4>(pol, nsec, c, pa); break;
+    case 2: denoise_sections_wide<kVar, KK, 2>(pol, nsec, c, pa); break;
+    default: denoise_sections_wide<kVar, KK, 1>(pol, nsec, c, pa); break;
+    }
+}
+
 template <bool kVar, int KK, class P>
 __device__ __forceinline__ void denoise_sections(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+    if constexpr (KK > 16) {
+        // 64-QAM: M <= 64 (check_dims); the generic M > 64 form below is not instantiated (its
+        // registers would set the whole kernel's occupancy)
+        denoise_sections_wide_m<kVar, KK>(pol, nsec, M, c, pa);
+        return;
+    } else {
     if (M <= 64) {
         denoise_sections_u<kVar, KK, 1>(pol, nsec, M, c, pa);
         return;
@@ -375,6 +475,7 @@ __device__ __forceinline__ void denoise_sections(const P& pol, int nsec, int M, 
             }
         }
     }
+    }
 }
 
 // max |xi| of one section in float64, exactly as the reference forms the logits.
@@ -417,17 +518,12 @@ __device__ void exact_section_f64(const LD& ld, const ST& st, int M, const Const
         float rr, ri, it;
         ld(m, rr, ri, it);
         const double ur = (double)(rr * it), ui = (double)(ri * it);
-        double eta[AMP_MAX_K];
         double zm = 0.0, sr = 0.0, si = 0.0;
-#pragma unroll
-        for (int k = 0; k < AMP_MAX_K; ++k) {
-            if (k < K) {
-                const double e = exp((ur * c.re[k] + ui * c.im[k]) - G);
-                eta[k] = e;
-                zm += e;
-                sr += c.re[k] * e;
-                si += c.im[k] * e;
-            }
+        for (int k = 0; k < K; ++k) {
+            const double e = exp((ur * c.re[k] + ui * c.im[k]) - G);
+            zm += e;
+            sr += c.re[k] * e;
+            si += c.im[k] * e;
         }
         double xr, xi;
         if (c.real_alpha) { xr = sr / Z; xi = 0.0; }
@@ -437,13 +533,12 @@ __device__ void exact_section_f64(const LD& ld, const ST& st, int M, const Const
             const double ax = c.real_alpha ? fabs(xr) : hypot(xr, xi);
             const double var0 = ax * ax * (1.0 - zm / Z);
             double vs = 0.0;
-#pragma unroll
-            for (int k = 0; k < AMP_MAX_K; ++k) {
-                if (k < K) {
-                    const double dr = xr - c.re[k], di = xi - c.im[k];
-                    const double h = c.real_alpha ? fabs(dr) : hypot(dr, di);
-                    vs += h * h * eta[k];
-                }
+            for (int k = 0; k < K; ++k) {
+                // eta recomputed (the same bits as above; no per-point array: 64-QAM)
+                const double e = exp((ur * c.re[k] + ui * c.im[k]) - G);
+                const double dr = xr - c.re[k], di = xi - c.im[k];
+                const double h = c.real_alpha ? fabs(dr) : hypot(dr, di);
+                vs += h * h * e;
             }
             var = (float)(var0 + vs / Z);
         }

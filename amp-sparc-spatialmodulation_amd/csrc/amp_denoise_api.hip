@@ -183,7 +183,8 @@ int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void*
     case 2: hipLaunchKernelGGL(denoise_kernel<2>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
     case 4: hipLaunchKernelGGL(denoise_kernel<4>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
     case 8: hipLaunchKernelGGL(denoise_kernel<8>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
-    default: hipLaunchKernelGGL(denoise_kernel<16>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    case 16: hipLaunchKernelGGL(denoise_kernel<16>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
+    default: hipLaunchKernelGGL(denoise_kernel<64>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
     }
     AMP_LAUNCH_CHECK("denoise");
     hipLaunchKernelGGL(denoise_reduce_kernel, dim3(1), dim3(DRWG), 0, st, P, c64);

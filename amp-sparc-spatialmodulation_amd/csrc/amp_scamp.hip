@@ -489,7 +489,8 @@ static void launch_kb(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t s
     case 2: launch_kb_kk<2>(P, gr, ldsB, t, st); break;
     case 4: launch_kb_kk<4>(P, gr, ldsB, t, st); break;
     case 8: launch_kb_kk<8>(P, gr, ldsB, t, st); break;
-    default: launch_kb_kk<16>(P, gr, ldsB, t, st); break;
+    case 16: launch_kb_kk<16>(P, gr, ldsB, t, st); break;
+    default: launch_kb_kk<64>(P, gr, ldsB, t, st); break;
     }
 }
 
@@ -501,6 +502,7 @@ static int scamp_attrs() {
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<4>();
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<8>();
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<16>();
+        if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<64>();
     });
     return g_scamp_rc;
 }
@@ -516,7 +518,12 @@ size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter) {
     return scamp_carve(d, max_iter, nullptr).bytes;
 }
 
-int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
+}  // extern "C"
+
+namespace amp {
+
+static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, ScampK& P,
+                       Const64& c64) {
     int rc = check_dims(d, c);
     if (rc) return rc;
     AMP_REQUIRE(a && a->W && a->A && a->y && a->xmap && a->xmmse && a->psi && a->status && a->ws,
@@ -528,7 +535,6 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_scamp_run: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
     rc = scamp_attrs();
     if (rc) return rc;
-    ScampK P;
     scamp_geometry(d, P);
     P.max_iter = a->max_iter;
     P.sigma2 = (float)a->noise_var;
@@ -539,32 +545,84 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.psi_nc = w.psi_nc; P.psi_nblk = scamp_psi_nblk(d); P.psi_split = (P.bn / 2 < P.Nt) ? 1 : 0;
     P.c = to_const(c);
-    const Const64 c64 = to_const64(c);
-    hipStream_t st = (hipStream_t)stream;
+    c64 = to_const64(c);
+    return AMP_OK;
+}
+
+// Tracker (scamp.py:9-25): the two weights and the initial state.
+static int scamp_prepare_impl(const ScampK& P, const amp_scamp_args* a, hipStream_t st) {
+    int rc;
     const float2* A = (const float2*)a->A;
     if ((rc = build_cweight(A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.kapA, P.ncpA, st))) return rc;
     if ((rc = build_cweight(A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WAH, P.kapB, P.ncpB, st))) return rc;
     const size_t tot = std::max(std::max((size_t)P.B * P.N, (size_t)P.B * P.n), (size_t)P.B * P.Lout);
     hipLaunchKernelGGL(scamp_init_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("scamp_init");
+    return AMP_OK;
+}
+
+// One SCAMPLayer.forward (scamp.py:43-59) + the allclose(psi) test of scamp.py:105.
+static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStream_t st) {
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     // fix-up grid: one slot per block in iteration t's partials (consumed by then)
     const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
-    for (int t = 0; t < P.max_iter; ++t) {
-        hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-        launch_kb(P, gr, ldsB, t, st);
-        if (P.psi_split)
-            hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
-        hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
-        hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
-        hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
-        hipLaunchKernelGGL(scamp_fin, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
-        AMP_LAUNCH_CHECK("scamp iteration");
-    }
+    hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_kb(P, gr, ldsB, t, st);
+    if (P.psi_split)
+        hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
+    hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
+    hipLaunchKernelGGL(scamp_fin, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
+    AMP_LAUNCH_CHECK("scamp iteration");
+    return AMP_OK;
+}
+
+static int scamp_finalize_impl(const ScampK& P, hipStream_t st) {
     hipLaunchKernelGGL(scamp_output_kernel, dim3(64), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("scamp_output");
     return AMP_OK;
+}
+
+}  // namespace amp
+
+extern "C" {
+
+int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = scamp_prepare_impl(P, a, st))) return rc;
+    for (int t = 0; t < P.max_iter; ++t)
+        if ((rc = scamp_iterate_impl(P, c64, t, st))) return rc;
+    return scamp_finalize_impl(P, st);
+}
+
+int amp_scamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    return rc ? rc : scamp_prepare_impl(P, a, (hipStream_t)stream);
+}
+
+int amp_scamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, int32_t t,
+                      void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(t >= 0 && t < a->max_iter, "amp_scamp_iterate: t = %d outside [0, %d)", t, a->max_iter);
+    return scamp_iterate_impl(P, c64, t, (hipStream_t)stream);
+}
+
+int amp_scamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    return rc ? rc : scamp_finalize_impl(P, (hipStream_t)stream);
 }
 
 }  // extern "C"

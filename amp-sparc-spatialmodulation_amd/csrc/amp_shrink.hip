@@ -75,7 +75,8 @@ __global__ __launch_bounds__(AMP_WG) void shrink_bayes_kernel(ShrinkK P, float* 
         float a0 = tabs(cplx, rr, ri);
         const float g0 = texpf(-(a0 * a0) / cov);
         float gs = 0.0f, xr = 0.0f, xi = 0.0f;
-#pragma unroll
+        constexpr int KU = KK > 16 ? 8 : KK;   // 64-QAM: chunks of 8 uniform operands
+#pragma unroll KU
         for (int k = 0; k < KK; ++k) {
             const float dr = rr - P.sre[k], di = ri - P.sim[k];
             const float a = tabs(cplx, dr, di);
@@ -221,7 +222,8 @@ int amp_shrink_bayes(const amp_constellation* c, int64_t count, int32_t is_compl
     ShrinkK P;
     int rc = fill_args(P, count, is_complex, r, cov_scalar, cov_vec);
     if (rc) return rc;
-    AMP_REQUIRE(c && c->K >= 1 && c->K <= AMP_MAX_K && is_pow2(c->K), "amp_shrink_bayes: bad constellation");
+    AMP_REQUIRE(c && c->K >= 1 && c->K <= AMP_MAX_K && is_pow2(c->K) && c->K != 32,
+                "amp_shrink_bayes: constellation size K = %d must be 1, 2, 4, 8, 16 or 64", c ? c->K : 0);
     AMP_REQUIRE(out || count == 0, "amp_shrink_bayes: null out");
     if (!is_complex)
         for (int k = 0; k < c->K; ++k)
@@ -242,7 +244,8 @@ int amp_shrink_bayes(const amp_constellation* c, int64_t count, int32_t is_compl
     case 2: hipLaunchKernelGGL(shrink_bayes_kernel<2>, g, b, 0, st, P, o); break;
     case 4: hipLaunchKernelGGL(shrink_bayes_kernel<4>, g, b, 0, st, P, o); break;
     case 8: hipLaunchKernelGGL(shrink_bayes_kernel<8>, g, b, 0, st, P, o); break;
-    default: hipLaunchKernelGGL(shrink_bayes_kernel<16>, g, b, 0, st, P, o); break;
+    case 16: hipLaunchKernelGGL(shrink_bayes_kernel<16>, g, b, 0, st, P, o); break;
+    default: hipLaunchKernelGGL(shrink_bayes_kernel<64>, g, b, 0, st, P, o); break;
     }
     AMP_LAUNCH_CHECK("shrink_bayes");
     return AMP_OK;

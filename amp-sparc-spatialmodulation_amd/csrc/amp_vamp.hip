@@ -282,6 +282,7 @@ static int vamp_attrs() {
         if (!rc) rc = vamp_k2_attrs<4>();
         if (!rc) rc = vamp_k2_attrs<8>();
         if (!rc) rc = vamp_k2_attrs<16>();
+        if (!rc) rc = vamp_k2_attrs<64>();
         g_vamp_attr_rc = rc;
     });
     return g_vamp_attr_rc;
@@ -303,7 +304,8 @@ static void launch_k2(const VampK& P, int t, hipStream_t st) {
     case 2: launch_k2_kk<2>(P, t, st); break;
     case 4: launch_k2_kk<4>(P, t, st); break;
     case 8: launch_k2_kk<8>(P, t, st); break;
-    default: launch_k2_kk<16>(P, t, st); break;
+    case 16: launch_k2_kk<16>(P, t, st); break;
+    default: launch_k2_kk<64>(P, t, st); break;
     }
 }
 

@@ -303,7 +303,7 @@ __device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float*
         if (act && g == 0) {
             const long long s = (long long)(row0 + row) * L + l;
             mism[lsc] = (unsigned char)mm;
-            count_section(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
+            count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
         }
     }
     __syncthreads();
@@ -352,9 +352,11 @@ __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, 
     dec_fold_block(w, n, out, s);
 }
 
+// dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
 template <int NT, int KK, int NWV>
-__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64, DecConst dc) {
+__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc) {
     constexpr int PWG = 64 * NWV;
+    const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
     __shared__ double s_d[PWG / 64][4];
@@ -485,7 +487,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, Const64 c64
         // 4. denoiser (vamp.py:84)
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         PartAcc pa;
-        denoise_sections_u<true, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
+        if constexpr (KK > 16)
+            denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
+        else
+            denoise_sections_u<true, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
         stamp(t, 5);
@@ -646,7 +651,7 @@ static bool persist_coop() {
 }
 
 template <int NT, int KK, int NWV>
-static int persist_launch_t(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
+static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
     const void* fn = (const void*)vamp_persist<NT, KK, NWV>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
@@ -666,9 +671,8 @@ static int persist_launch_t(const VampK& P, const Const64& c64, const DecConst& 
     }
     if (persist_coop()) {
         VampK Pc = P;
-        Const64 cc = c64;
         DecConst dd = dc;
-        void* args[] = {(void*)&Pc, (void*)&cc, (void*)&dd};
+        void* args[] = {(void*)&Pc, (void*)&dd};
         e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
         if (e != hipSuccess) {
             set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
@@ -684,7 +688,7 @@ static int persist_launch_t(const VampK& P, const Const64& c64, const DecConst& 
                   device_cu_count());
         return AMP_E_LAUNCH;
     }
-    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, c64, dc);
+    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, dc);
     e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
@@ -694,42 +698,47 @@ static int persist_launch_t(const VampK& P, const Const64& c64, const DecConst& 
 }
 
 template <int NT, int NWV>
-static int persist_launch_nt(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
+static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV>(P, c64, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV>(P, c64, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV>(P, c64, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV>(P, c64, dc, st);
-    default: return persist_launch_t<NT, 16, NWV>(P, c64, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV>(P, dc, st);
+    case 16: return persist_launch_t<NT, 16, NWV>(P, dc, st);
+    default: return persist_launch_t<NT, 64, NWV>(P, dc, st);
     }
 }
 
-static int persist_dispatch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st);
+static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
 
+// c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
+// launch: dc's Const64 base is overwritten with c64.
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu) {
     (void)ncu;
-    int rc = persist_dispatch(P, c64, dc, st);
+    DecConst d2 = dc;
+    static_cast<Const64&>(d2) = c64;
+    int rc = persist_dispatch(P, d2, st);
     if (rc || !P.dec_on) return rc;
     hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);
     AMP_LAUNCH_CHECK("vamp_decide_fold");
     return AMP_OK;
 }
 
-static int persist_dispatch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st) {
+static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) {
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
     if (persist_waves() == 4) {
         switch (P.N) {
-        case 64: return persist_launch_nt<2, 4>(P, c64, dc, st);
-        case 128: return persist_launch_nt<4, 4>(P, c64, dc, st);
-        case 256: return persist_launch_nt<8, 4>(P, c64, dc, st);
+        case 64: return persist_launch_nt<2, 4>(P, dc, st);
+        case 128: return persist_launch_nt<4, 4>(P, dc, st);
+        case 256: return persist_launch_nt<8, 4>(P, dc, st);
         default: break;
         }
     } else {
         switch (P.N) {
-        case 64: return persist_launch_nt<1, 8>(P, c64, dc, st);
-        case 128: return persist_launch_nt<2, 8>(P, c64, dc, st);
-        case 256: return persist_launch_nt<4, 8>(P, c64, dc, st);
+        case 64: return persist_launch_nt<1, 8>(P, dc, st);
+        case 128: return persist_launch_nt<2, 8>(P, dc, st);
+        case 256: return persist_launch_nt<4, 8>(P, dc, st);
         default: break;
         }
     }

@@ -24,7 +24,9 @@ int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled) {
     AMP_REQUIRE(d->M == d->Nt / d->Na && d->L == d->Na * d->Lin && d->N == d->Nt * d->Lin && d->n == d->Nr * d->Lout,
                 "inconsistent derived dimensions");
     AMP_REQUIRE(is_pow2(d->M), "section size M = Nt/Na = %d must be a power of two", d->M);
-    AMP_REQUIRE(c->K >= 1 && c->K <= AMP_MAX_K && is_pow2(c->K), "constellation size K = %d must be 1, 2, 4, 8 or 16", c->K);
+    AMP_REQUIRE(c->K >= 1 && c->K <= AMP_MAX_K && is_pow2(c->K) && c->K != 32,
+                "constellation size K = %d must be 1, 2, 4, 8, 16 or 64", c->K);
+    AMP_REQUIRE(c->K <= 16 || d->M <= 64, "64-point constellations need M = Nt/Na <= 64 (M = %d)", d->M);
     if (!tiled) return AMP_OK;   // the decision / standalone denoiser have no GEMM tiling
     AMP_REQUIRE(2 * d->M <= 256, "section size M = %d > 128 not supported by the fused detectors", d->M);
     AMP_REQUIRE(d->N % 2 == 0 && d->n % 2 == 0, "N (%d) and n (%d) must be even", d->N, d->n);

@@ -1,6 +1,12 @@
-"""SCAMP (spatially coupled SPARC AMP) — drop-in for the reference's ``SCAMP`` /
-``SCAMPLayer`` (scamp.py:8-108), running on the gfx950 kernels of libampsparc.so
-(amp_scamp_run)."""
+"""SCAMP (spatially coupled SPARC AMP) — drop-in for the reference's ``SCAMP`` / ``SCAMPLayer`` /
+``Tracker`` (scamp.py:8-108), running on the gfx950 kernels of libampsparc.so.
+
+``SCAMP.forward(W, A, y, SNR, x, symbol, index) -> Loss`` keeps the reference's signature and
+returns its own reused ``Loss`` (scamp.py:77-107); the loop (amp_scamp_run), the allclose(psi)
+early exit and the decision run on the device, and the counters resolve lazily.  Layer level:
+``Tracker(W, A, y, sigma2, config)`` + ``SCAMPLayer.forward(T)`` (amp_scamp_prepare /
+amp_scamp_iterate / amp_scamp_finalize).
+"""
 from __future__ import annotations
 
 import ctypes as C
@@ -11,15 +17,93 @@ from torch import nn
 import amp_native as nat
 from config import Config
 from loss import Loss
-from vamp import _c64, block_denoise, read_result
+from vamp import LazyResult, _c64, block_denoise
+
+
+class _Buffers:
+    """Per-shape device buffers reused across forwards (no allocation in steady state)."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, device, B, N, Lin, ws_bytes):
+        key = (str(device), B, N, Lin, ws_bytes)
+        if key != self.key:
+            self.xmap = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.xmmse = torch.empty(B, N, dtype=torch.complex64, device=device)
+            self.psi = torch.empty(B, Lin, dtype=torch.float32, device=device)
+            self.res = torch.zeros(256, dtype=torch.uint8, device=device)
+            self.ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=device)
+            self.key = key
+        return self
+
+
+class Tracker:
+    """Device state of one SCAMP forward (scamp.py:8-25): xmap, xmmse, psi and the workspace holding
+    the A / A^H operators and z, phi, tau of the running iteration."""
+
+    def __init__(self, W, A, y, sigma2: float, config: Config, bufs: _Buffers | None = None):
+        self.config = config
+        B = config.B
+        n, N = A.shape[-2], A.shape[-1]
+        self.A = _c64(A, (n, N))
+        self.y = _c64(y, (B, n))
+        self.W = W.reshape(config.Lout, config.Lin).to(device=self.y.device, dtype=torch.float32).resolve_neg()
+        self.W = self.W.contiguous()
+        self.noise_var = sigma2
+        self.dims = config.dims()
+        self.const = config.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_scamp_workspace_bytes(C.byref(self.dims), config.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_scamp_workspace_bytes: invalid dimensions')
+        self.buf = (bufs or _Buffers()).get(self.y.device, B, N, config.Lin, wsb)
+        a = nat.AmpScampArgs()
+        a.W, a.A, a.y = nat.dptr(self.W, torch.float32, 'W'), nat.dptr(self.A, name='A'), nat.dptr(self.y, name='y')
+        a.max_iter = config.N_Layers
+        a.noise_var = float(sigma2)                                       # scamp.py:98
+        a.xmap, a.xmmse, a.psi = nat.dptr(self.buf.xmap), nat.dptr(self.buf.xmmse), nat.dptr(self.buf.psi)
+        a.status = nat.dptr(self.buf.res)
+        a.ws, a.ws_bytes = nat.dptr(self.buf.ws), self.buf.ws.numel()
+        self.args = a
+        self.stream = nat.stream_ptr(self.y.device)
+
+    @property
+    def xmap(self):
+        return self.buf.xmap.view(self.config.B, -1, 1)
+
+    @property
+    def xmmse(self):
+        return self.buf.xmmse.view(self.config.B, -1, 1)
+
+    @property
+    def psi(self):
+        return self.buf.psi.view(self.config.B, -1, 1)
+
+    def _call(self, fn, *extra):
+        nat.check(getattr(nat.lib(), fn)(C.byref(self.dims), C.byref(self.const), C.byref(self.args), *extra,
+                                         self.stream), fn)
+
+    def prepare(self):
+        self._call('amp_scamp_prepare')
+
+    def finalize(self):
+        self._call('amp_scamp_finalize')
+
+    def status(self) -> nat.AmpStatus:
+        res = getattr(self, 'res', None)
+        res = self.buf.res if res is None else res
+        return nat.AmpStatus.from_buffer_copy(res[:C.sizeof(nat.AmpStatus)].cpu().numpy().tobytes())
 
 
 class SCAMPLayer(nn.Module):
-    """SCAMPLayer (scamp.py:27-68); its denoiser is the mean-only block denoiser."""
+    """SCAMPLayer (scamp.py:27-68): forward(T) is one iteration on the device (a no-op once the
+    early exit of scamp.py:105 has fired); its denoiser is the mean-only block denoiser."""
 
-    def __init__(self, config: Config) -> None:
+    def __init__(self, config: Config, index: int = 0) -> None:
         super().__init__()
         self.config = config
+        self.index = index
         self.B, self.Na = config.B, config.Na
         self.M = config.Nt // config.Na
         self.Mc, self.Mr = config.Nt, config.Nr
@@ -29,58 +113,56 @@ class SCAMPLayer(nn.Module):
         self.LM = self.Mc * self.Lc
         self.K = config.K
 
+    def forward(self, T: Tracker) -> None:
+        T._call('amp_scamp_iterate', self.index)
+
     def denoiser(self, s: torch.Tensor, tau: torch.Tensor) -> torch.Tensor:
         """scamp.py:61-68: tau is tau_use, halved inside."""
         return block_denoise(self.config, s, tau, mode=2)
 
 
-class SCAMP(nn.Module):
+class SCAMP(LazyResult, nn.Module):
     def __init__(self, config: Config) -> None:
         super().__init__()
         self.config = config
         self.E = config.Na / config.Nr                                    # scamp.py:72
-        self.layers = nn.ModuleList([SCAMPLayer(config) for _ in range(config.N_Layers)])
+        self.layers = nn.ModuleList([SCAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
-        self._key = None
+        self._bufs = _Buffers()
         self.last = None
 
-    def _ensure_buffers(self, dev, B, N, Lin, wsb):
-        key = (str(dev), B, N, Lin, wsb)
-        if key != self._key:
-            self.xmap = torch.empty(B, N, dtype=torch.complex64, device=dev)
-            self.xmmse = torch.empty(B, N, dtype=torch.complex64, device=dev)
-            self.psi = torch.empty(B, Lin, dtype=torch.float32, device=dev)
-            self.res = torch.zeros(256, dtype=torch.uint8, device=dev)
-            self.ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
-            self._key = key
+    @property
+    def xmap(self):
+        return self._bufs.xmap
 
-    def detect(self, W: torch.Tensor, A: torch.Tensor, y: torch.Tensor, SNR: float):
-        cfg = self.config
-        B = cfg.B
-        n, N = A.shape[-2], A.shape[-1]
-        A = _c64(A, (n, N))
-        y = _c64(y, (B, n))
-        W = W.reshape(cfg.Lout, cfg.Lin).to(device=y.device, dtype=torch.float32).resolve_neg().contiguous()
-        d, c = cfg.dims(), cfg.constellation()
-        lib = nat.lib()
-        wsb = lib.amp_scamp_workspace_bytes(C.byref(d), cfg.N_Layers)
-        self._ensure_buffers(y.device, B, N, cfg.Lin, wsb)
-        a = nat.AmpScampArgs()
-        a.W, a.A, a.y = nat.dptr(W, torch.float32, 'W'), nat.dptr(A, name='A'), nat.dptr(y, name='y')
-        a.max_iter = cfg.N_Layers
-        a.noise_var = float(self.E / SNR)                                 # scamp.py:98
-        a.xmap, a.xmmse, a.psi = nat.dptr(self.xmap), nat.dptr(self.xmmse), nat.dptr(self.psi)
-        a.status = nat.dptr(self.res)
-        a.ws, a.ws_bytes = nat.dptr(self.ws), self.ws.numel()
-        self._keep = (W, A, y)
-        nat.check(lib.amp_scamp_run(C.byref(d), C.byref(c), C.byref(a), nat.stream_ptr(y.device)), 'amp_scamp_run')
+    @property
+    def xmmse(self):
+        return self._bufs.xmmse
+
+    @property
+    def psi(self):
+        return self._bufs.psi
+
+    def detect(self, W: torch.Tensor, A: torch.Tensor, y: torch.Tensor, SNR: float) -> Tracker:
+        """All iterations on the device, asynchronous (no host sync)."""
+        with torch.cuda.device(y.device):
+            T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
+            T._call('amp_scamp_run')
+        self._keep = T
+        return T
 
     def forward(self, W: torch.Tensor, A: torch.Tensor, y: torch.Tensor, SNR: float, x: torch.Tensor, symbol,
                 index) -> Loss:
-        self.detect(W, A, y, SNR)
-        self.L.dump()                                                     # scamp.py:99
-        self.L.device_counts(self.xmap, self.xmmse, x, symbol, index, out=self.res[64:])   # scamp.py:107
-        status, counts = read_result(self.res)
-        self.L.record(self.L.rates_from_counts(counts), int(status.T))
-        self.last = status
+        """scamp.py:77-107; the counters resolve lazily (see LazyResult)."""
+        with torch.cuda.device(y.device):
+            T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
+            res, host = self._result_slot(T.y.device)
+            T.res = res
+            T.args.status = nat.dptr(res)
+            T._call('amp_scamp_run')
+            # decision on T.xmap (scamp.py:107); counters next to the status record
+            self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
+            self._arm(self.L, res, host, 'amp_scamp_run')                 # + L.dump(), scamp.py:99
+        self._keep = T
+        self.last = T
         return self.L

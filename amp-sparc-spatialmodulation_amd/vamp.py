@@ -161,7 +161,48 @@ def block_denoise(config: Config, s: torch.Tensor, tau, mode: int):
     return xm.view(B, -1, 1), var.view(B, -1, 1)
 
 
-class VAMP(nn.Module):
+class LazyResult:
+    """A detector's result read-back without a host stall: a forward leaves its status + counter
+    record in one of two (device, pinned host) 256-byte slots, copies it to the host
+    asynchronously and arms Loss._pending; the record is resolved (and the metrics recorded)
+    on the Loss's first access or at the next forward, so the launches of the next epoch are
+    queued before this one's results are waited for (Model.simulate's loop)."""
+
+    _ring = None
+    _slot = 1
+
+    def _result_slot(self, device):
+        """One of two (device, pinned host) 256-byte result buffers, alternating per forward, so
+        a forward's status / counters stay readable while the next forward runs."""
+        if self._ring is None or self._ring[0][0].device != device:
+            self._ring = [(torch.zeros(256, dtype=torch.uint8, device=device),
+                           torch.zeros(256, dtype=torch.uint8, pin_memory=True)) for _ in range(2)]
+        self._slot ^= 1
+        return self._ring[self._slot]
+
+    def _arm(self, L: Loss, res: torch.Tensor, host: torch.Tensor, what: str) -> None:
+        """Queue the copy of `res` to `host` on the device's current stream and make L resolve it
+        lazily; the previous forward's record is resolved first."""
+        host.copy_(res, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(res.device))   # the stream the launches and the copy ran on
+        L.resolve()                 # the previous forward's counters (it has finished by now)
+        L.dump()
+
+        def finish(L=L):
+            done.synchronize()
+            raw = host.numpy().tobytes()
+            status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
+            counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
+            if status.nan_state < 0:
+                raise RuntimeError(f'{what}: persistent engine grid barrier timed out (results invalid)')
+            L.last_counts = counts
+            L.last_status = status
+            L.record(L.rates_from_counts(counts), int(status.T))
+        L._pending = finish
+
+
+class VAMP(LazyResult, nn.Module):
     """``engine``: nat.ENGINE_AUTO (persistent single-launch engine when the shape allows it,
     else three launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h)."""
 
@@ -174,8 +215,6 @@ class VAMP(nn.Module):
         self.layers = nn.ModuleList([VAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
         self._bufs = _Buffers()
-        self._ring = None
-        self._slot = 1
         self.last = None
 
     def detect(self, U, s, Vh, y, SNR: float) -> Tracker:
@@ -186,15 +225,6 @@ class VAMP(nn.Module):
             nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
                       'amp_vamp_run')
         return T
-
-    def _result_slot(self, device):
-        """One of two (device, pinned host) 256-byte result buffers, alternating per forward, so
-        a forward's status / counters stay readable while the next forward runs."""
-        if self._ring is None or self._ring[0][0].device != device:
-            self._ring = [(torch.zeros(256, dtype=torch.uint8, device=device),
-                           torch.zeros(256, dtype=torch.uint8, pin_memory=True)) for _ in range(2)]
-        self._slot ^= 1
-        return self._ring[self._slot]
 
     def forward(self, U: torch.Tensor, s: torch.Tensor, Vh: torch.Tensor, y: torch.Tensor, SNR: float,
                 x: torch.Tensor, symbols: np.ndarray, indices: np.ndarray) -> Loss:
@@ -226,22 +256,7 @@ class VAMP(nn.Module):
             nat.check(lib.amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream), 'amp_vamp_run')
             # decision on T.r (vamp.py:187); counters land next to the status record
             self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
-        host.copy_(res, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(T.y.device))   # the stream the launches and the copy ran on
-        self.L.resolve()                 # the previous forward's counters (it has finished by now)
-        self.L.dump()                                                    # vamp.py:180
-
-        def finish(L=self.L):
-            done.synchronize()
-            raw = host.numpy().tobytes()
-            status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
-            counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
-            if status.nan_state < 0:
-                raise RuntimeError('amp_vamp_run: persistent engine grid barrier timed out (results invalid)')
-            L.last_counts = counts
-            L.record(L.rates_from_counts(counts), int(status.T))
-        self.L._pending = finish
+        self._arm(self.L, res, host, 'amp_vamp_run')                     # + L.dump(), vamp.py:180
         self.last = T
         return self.L
 

@@ -38,7 +38,8 @@ extern "C" {
 #define AMP_E_WORKSPACE (-2) /* workspace too small */
 #define AMP_E_LAUNCH (-3)    /* HIP launch failure */
 
-#define AMP_MAX_K 16         /* largest constellation of config.py:44 (16PSK / 16QAM) */
+#define AMP_MAX_K 64         /* 64-QAM (BASELINE cfg5; the reference's own Config stops at 16, config.py:44)
+                              * sizes: K in {1, 2, 4, 8, 16, 64} */
 
 /* Constellation of Config (config.py:78-118): unit-power points in float32 (for the
  * denoiser) and float64 (for the MAP decision, loss.py:295), plus gray labels. */
@@ -169,6 +170,14 @@ typedef struct amp_bamp_args {
 
 size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
 int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
+/* Layer-level pieces of amp_bamp_run (same arguments; amp_bamp_run = prepare, iterate(t) for
+ * t < max_iter, finalize): prepare = Tracker (bamp.py:13-25: the H / H^H / |H|^2 operators,
+ * xmmse = 0, var = 1, z = y, u = sigma2); iterate(t) = one BAMPLayer.forward (bamp.py:48-64) +
+ * the allclose(var) early exit of bamp.py:140 (a device-side no-op once it has fired);
+ * finalize = the executed iterations' var into a->var and the status record. */
+int amp_bamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
+int amp_bamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, int32_t t, void* stream);
+int amp_bamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
 /* BAMPLayer.random_denoiser (bamp.py:79-88) alone (layer-level API): r c64 [count], cov f32
  * [count] -> xmmse c64, var f32; the element-wise float64 Bayes posterior of denoiser 1. */
 int amp_bamp_random_denoise(const amp_constellation* c, int64_t count, const void* r, const void* cov, float P0,
@@ -193,6 +202,13 @@ typedef struct amp_scamp_args {
 
 size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+/* Layer-level pieces of amp_scamp_run, as for BAMP: prepare = Tracker (scamp.py:9-25), iterate(t)
+ * = one SCAMPLayer.forward (scamp.py:43-59) + the allclose(psi) early exit of scamp.py:105,
+ * finalize = the last psi into a->psi. */
+int amp_scamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+int amp_scamp_iterate(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, int32_t t,
+                      void* stream);
+int amp_scamp_finalize(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
 
 /* ---- Block-sparse denoiser — replaces VAMPLayer.segmented_denoiser
  *      (vamp.py:96-119), BAMPLayer.segmented_denoiser (bamp.py:66-77) and

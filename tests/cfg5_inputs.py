@@ -23,10 +23,20 @@ def g6_points():
 
 
 def cfg5_config(ent, device='cpu', B=None):
+    """The entry's Config; 64-QAM (BASELINE cfg5's alphabet, which Config rejects like the
+    reference) is injected after construction exactly as make_goldens.py injected it into the
+    reference's Config, and checked against the table the golden recorded."""
     from config import Config
-    return Config(ent['Nt'], ent['Na'], ent['Nr'], 1, 1, batch=B or ent['B'], generator_mode='sparc',
-                  iterations=ent['iterations'], alphabet=ent['alphabet'], channel_profile='uniform',
-                  channel_truncation='tail', device=device)
+    qam64 = ent['alphabet'] == '64QAM'
+    cfg = Config(ent['Nt'], ent['Na'], ent['Nr'], 1, 1, batch=B or ent['B'], generator_mode='sparc',
+                 iterations=ent['iterations'], alphabet='16QAM' if qam64 else ent['alphabet'],
+                 channel_profile='uniform', channel_truncation='tail', device=device)
+    if qam64:
+        cfg.inject_square_qam(64)
+        assert np.array_equal(np.real(cfg.symbols), np.array(ent['symbols_re']))
+        assert np.array_equal(np.imag(cfg.symbols), np.array(ent['symbols_im']))
+        assert list(cfg.gray) == list(ent['gray']) and cfg.code_rate == ent['code_rate']
+    return cfg
 
 
 def cfg5_inputs(ent, seed, EbN0):
@@ -42,3 +52,10 @@ def cfg5_inputs(ent, seed, EbN0):
     SNR = cfg.snr(EbN0)
     y = A @ x + ch.awgn(SNR)
     return dict(A=A, x=x, y=y, sym=sym, idx=idx, SNR=SNR)
+
+
+def cfg5_inputs_b(ent, seed, EbN0, B):
+    """cfg5_inputs with the batch taken from the caller (entries recorded at another B)."""
+    e = dict(ent)
+    e['B'] = B
+    return cfg5_inputs(e, seed, EbN0)

@@ -366,22 +366,65 @@ def correlated_channel(Nr, Nt, rho):
     return torch.tensor(A.astype(np.complex64))
 
 
+def inject_square_qam(cfg, K=64):
+    """Square K-QAM (unit mean power, per-axis binary-reflected gray code) injected into a
+    reference Config after construction, as SURVEY.md §8(c) verified the reference's BAMP takes
+    it: the reference's Config rejects 64QAM (config.py:44).  Every Config attribute the
+    constellation feeds is set the way config.py:117-157 would derive it."""
+    m = int(round(np.sqrt(K)))
+    b = int(np.log2(m))
+    levels = np.arange(-(m - 1), m, 2)
+    g1 = [i ^ (i >> 1) for i in range(m)]
+    pts = [complex(levels[i], levels[q]) for i in range(m) for q in range(m)]
+    cfg.symbols = np.array(pts) / np.sqrt(np.mean(np.abs(pts) ** 2))
+    cfg.gray = [(g1[i] << b) | g1[q] for i in range(m) for q in range(m)]
+    cfg.alphabet = f'{K}QAM'
+    cfg.K = K
+    cfg.symbol_bits = int(np.log2(K))
+    cfg.Ps = cfg.sparsity / K
+    cfg.is_complex = True
+    cfg.inner_code_rate = cfg.Na * np.log2(cfg.M * cfg.K) / cfg.Mr
+    cfg.code_rate = cfg.Lc * cfg.inner_code_rate / cfg.Lr
+    cfg.min_amp_snr = 1 / (cfg.kappa * (1 / (np.exp(2 * cfg.code_rate) - 1) - 1 / cfg.Lh))
+    cfg.min_snr = 2 ** cfg.code_rate - 1
+    cfg.min_snr_dB = 10 * np.log10(cfg.min_snr)
+    cfg.shannon_limit_dB = cfg.min_snr_dB - 10 * np.log10(cfg.code_rate)
+    cfg.name = (f'{cfg.alphabet},{cfg.mode}/{cfg.profile},{cfg.trunc}/'
+                f'Nt={cfg.Nt},Na={cfg.Na},Nr={cfg.Nr},Lh={cfg.Lh},Lin={cfg.Lin}')
+    return cfg
+
+
 G6_CONFIGS = {
     'cfg5_bamp_corr_16qam': (512, 16, 1024, 1024, '16QAM', 20, [6, 10, 14, 18], [0]),
     'cfg5_bamp_corr_qpsk': (512, 16, 1024, 1024, 'QPSK', 20, [2, 6, 10, 14], [0]),
+    # BASELINE cfg5's own alphabet (round 2): 64-QAM injected into the reference's Config
+    'cfg5_bamp_corr_64qam': (512, 16, 1024, 1024, '64QAM', 20, [0, 2, 4, 6, 7, 8, 9, 10, 14, 18, 22, 26], [0]),
+    'cfg5_bamp_corr_64qam_b8192': (512, 16, 1024, 8192, '64QAM', 20, [6], [0]),
 }
 
 
-def g6():
+def g6(names=None):
     path = os.path.join(HERE, 'g6_cfg5_corr.json')
-    db = {}
+    db = json.load(open(path)) if os.path.exists(path) else {}
     rho = 0.5
     for name, (Nt, Na, Nr, B, alph, iters, grid, seeds) in G6_CONFIGS.items():
-        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
-        ent = {'algo': 'bamp', 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': B, 'alphabet': alph, 'iterations': iters,
-               'rho': rho, 'points': {}}
+        if names and name not in names:
+            continue
+        if alph == '64QAM':
+            cfg = inject_square_qam(cfg_of(Nt, Na, Nr, B, '16QAM', iterations=iters), 64)
+        else:
+            cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = db.get(name, {'algo': 'bamp', 'Nt': Nt, 'Na': Na, 'Nr': Nr, 'B': B, 'alphabet': alph,
+                            'iterations': iters, 'rho': rho, 'points': {}})
+        if alph == '64QAM':
+            ent['symbols_re'] = [float(v) for v in np.real(cfg.symbols)]
+            ent['symbols_im'] = [float(v) for v in np.imag(cfg.symbols)]
+            ent['gray'] = [int(v) for v in cfg.gray]
+            ent['code_rate'] = float(cfg.code_rate)
         for seed in seeds:
             for EbN0 in grid:
+                if f'{seed}/{EbN0}' in ent['points']:
+                    continue
                 t0 = time.time()
                 np.random.seed(seed)
                 torch.manual_seed(seed)
@@ -395,12 +438,13 @@ def g6():
                 rec['sha_A'] = sha(A)
                 rec['sha_x'] = sha(x)
                 rec['y_abs2_sum'] = float(np.sum(np.abs(y.numpy().astype(np.complex128)) ** 2))
+                rec['SNR'] = float(SNR)
                 ent['points'][f'{seed}/{EbN0}'] = rec
                 print(name, seed, EbN0, 'T=', rec['T'], 'ver=', rec['ver'], 'ser=', rec['ser'],
                       f'{time.time() - t0:.1f}s', flush=True)
-        db[name] = ent
-    with open(path, 'w') as f:
-        json.dump(db, f, indent=1, sort_keys=True)
+                db[name] = ent
+                with open(path, 'w') as f:
+                    json.dump(db, f, indent=1, sort_keys=True)
 
 
 # ---------------------------------------------------------------------------
@@ -625,7 +669,7 @@ if __name__ == '__main__':
         elif w == 'g7':
             g7()
         elif w == 'g6':
-            g6()
+            g6(names or None)
         elif w == 'g5':
             g5()
         elif w == 'g4':

@@ -68,3 +68,15 @@ def loss_close(got: dict, ref: dict, count_tol=0.0, mse_rtol=1e-3):
         elif abs(g - r) > count_tol + 1e-12:
             bad[k] = (g, r)
     return bad
+
+
+def bits_equal(a, b) -> bool:
+    """Bitwise equality of two device tensors (NaN payloads included): the NaN-onset iterations
+    must agree too, which torch.equal (NaN != NaN) cannot check."""
+    import torch
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return False
+    if a.is_complex():
+        a, b = torch.view_as_real(a), torch.view_as_real(b)
+    w = torch.int64 if a.element_size() == 8 else torch.int32
+    return torch.equal(a.contiguous().view(w), b.contiguous().view(w))

@@ -69,3 +69,36 @@ def test_curve_point(device, name, key):
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
     _check_T(int(got['T']), int(ref['T']), ent['iterations'])
+
+
+@pytest.mark.parametrize('name', ['bamp_QPSK_0_0', 'bamp_QPSK_12_0', 'scamp_16QAM_8_0', 'scamp_QPSK_2_0'])
+def test_layer_level_equals_forward(device, name):
+    """Tracker + Layer.forward(T) per iteration (the reference's layer surface, bamp.py:12-64,
+    scamp.py:8-59) == the detector's whole-loop launch sequence, bit for bit, with the same T."""
+    import torch
+    c = G1[name]
+    cfg = _config(int(c.Nt), int(c.Na), int(c.Nr), int(c.B), c.alphabet, iterations=int(c.iters))
+    if name.startswith('bamp'):
+        from bamp import BAMP, Tracker
+        det = BAMP(cfg)
+        args = (_t(c.A, device), _t(c.y, device))
+        T1 = det.detect(*args, float(c.SNR))
+        ref = (T1.xmap.clone(), T1.var.clone(), T1.status().T)
+        T = Tracker(*args, det.E / float(c.SNR), cfg)
+        outs = lambda T: (T.xmap, T.var)  # noqa: E731
+    else:
+        from scamp import SCAMP, Tracker
+        det = SCAMP(cfg)
+        args = (_t(c.W, device), _t(c.A, device), _t(c.y, device))
+        T1 = det.detect(*args, float(c.SNR))
+        ref = (T1.xmap.clone(), T1.psi.clone(), T1.status().T)
+        T = Tracker(*args, det.E / float(c.SNR), cfg)
+        outs = lambda T: (T.xmap, T.psi)  # noqa: E731
+    T.prepare()
+    for layer in det.layers:
+        layer(T)
+    T.finalize()
+    a, b = outs(T)
+    assert T.status().T == ref[2] == int(c.T)
+    assert gio.bits_equal(a, ref[0]) and gio.bits_equal(b, ref[1])
+

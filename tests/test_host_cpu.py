@@ -36,7 +36,8 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     import ctypes as C
     import amp_native as nat
-    assert C.sizeof(nat.AmpConstellation) == 8 + 16 * 4 * 2 + 16 * 8 * 2 + 16 * 4
+    assert nat.AMP_MAX_K == 64
+    assert C.sizeof(nat.AmpConstellation) == 8 + 64 * 4 * 2 + 64 * 8 * 2 + 64 * 4
     assert C.sizeof(nat.AmpDims) == 40
     assert C.sizeof(nat.AmpStatus) == 32
     assert C.sizeof(nat.AmpCounts) == 13 * 8
@@ -132,3 +133,20 @@ def test_segmented_replica_matches_draw_loop():
             xl[s, p] = cfg.symbols[k]
         assert np.array_equal(x.numpy().ravel(), xl.ravel())
         assert np.array_equal(idx, xl.ravel().nonzero()[0])
+
+
+def test_detector_api_surface():
+    """The reference's class surface (vamp.py / bamp.py / scamp.py: Tracker, Layer.forward(T),
+    the detector's forward) and the lazy read-back every detector shares — checked on the CPU so
+    a broken host mirror is caught before a GPU run."""
+    import inspect
+    import vamp
+    import bamp
+    import scamp
+    for mod, det, layer in ((vamp, 'VAMP', 'VAMPLayer'), (bamp, 'BAMP', 'BAMPLayer'), (scamp, 'SCAMP', 'SCAMPLayer')):
+        D, Ly, T = getattr(mod, det), getattr(mod, layer), getattr(mod, 'Tracker')
+        for m in ('forward', 'detect', '_result_slot', '_arm'):
+            assert callable(getattr(D, m, None)), (det, m)
+        assert 'T' in inspect.signature(Ly.forward).parameters
+        for m in ('prepare', 'finalize', 'status'):
+            assert callable(getattr(T, m, None)), (det, m)
