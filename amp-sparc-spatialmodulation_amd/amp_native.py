@@ -65,7 +65,7 @@ class AmpBampArgs(C.Structure):
 
 class AmpScampArgs(C.Structure):
     _fields_ = [('W', C.c_void_p), ('A', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32),
-                ('pad', C.c_int32), ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p),
+                ('engine', C.c_int32), ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p),
                 ('psi', C.c_void_p), ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
 
@@ -92,6 +92,7 @@ SIGNATURES = {
     'amp_bamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_bamp_random_denoise': (C.c_int, [_K, C.c_int64, _P, _P, C.c_float, C.c_float, _P, _P, _P]),
     'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),
+    'amp_scamp_select_engine': (C.c_int, [_D, _I]),
     'amp_scamp_run': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
     'amp_scamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
     'amp_scamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _I, _P]),

@@ -73,6 +73,7 @@ inline Const64 to_const64(const amp_constellation* c) {
 }
 
 int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
+int device_cu_count();   // compute units of the current device (cached)
 
 // Column tile width of the section-fused GEMMs: a multiple of 2M so no section straddles
 // two workgroups.

@@ -1,0 +1,195 @@
+// amp_persist.h — device building blocks of the persistent engines (amp_vamp_persist.hip,
+// amp_scamp_persist.hip): one workgroup per CU keeps 16 trials' state in LDS across the whole
+// iteration loop.
+//  * gemm16: C[16 x 16 NT] += A[16 x 16 G] (LDS) . Wq^T on v_mfma_f32_16x16x4_f32, the weight
+//    streamed from L2 through a buffer-load ring in 16x16x4-packed order (wpack16_index);
+//  * the per-iteration batch-global exchange: each workgroup publishes its partial as two
+//    sc1 write-through granules tagged with (launch generation, iteration), every workgroup
+//    sweeps and reduces all of them in one fixed order (bit-identical scalars everywhere);
+//  * grid_sync: a bounded-spin grid barrier for the rare exact-float64 path.
+// Every spin is bounded (2 s) and raises an abort word that releases every other workgroup.
+#pragma once
+
+#include "amp_common.h"
+
+namespace amp {
+
+constexpr int PRING = 4;   // W groups in flight per wave
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// C[16 x 16*NT] (this wave's columns ct0*16 ...) += A[16 x 16*G] (LDS, row stride lda) . Wq^T,
+// Wq packed by wpack16_index.  Accumulator t, register r: row 4*(lane>>4) + r, column
+// 16*(ct0 + t) + (lane & 15).  Fully unrolled over the G reduction groups so every wait on the
+// weight ring is a counted `s_waitcnt vmcnt(n)` (a rolled loop drained it to vmcnt(0) at the
+// back edge: ~25 % of the GEMM time at cfg4, r01 trace); the A row of group g+1 is read from
+// LDS one group ahead.
+template <int NT, int G>
+__device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __restrict__ wq, int ct0,
+                                       f32x4 (&acc)[NT]) {
+    constexpr int R = G < PRING ? G : PRING;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one buffer resource per wave (base = this wave's first column tile); every load is
+    // lane * 16 + a compile-time byte offset (SGPR), so the unrolled ring holds no addresses
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);   // wave-uniform: SGPR resource, no waterfall
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(wq) + (size_t)ct0u * G * 256, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = lane * 16;
+    auto wload = [&](int t, int g) {
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, (t * G + g) * 1024, 0);
+        return make_float4(v.x, v.y, v.z, v.w);
+    };
+    float4 ring[R][NT];
+#pragma unroll
+    for (int d = 0; d < R; ++d)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ring[d][t] = wload(t, d);
+    const float* a_s = sA + (lane & 15) * lda + 4 * (lane >> 4);
+    float4 acur = *reinterpret_cast<const float4*>(a_s);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int d = g % R;
+        const float4 anext = *reinterpret_cast<const float4*>(a_s + 16 * (g + 1 < G ? g + 1 : g));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.x, ring[d][t].x, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.y, ring[d][t].y, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.z, ring[d][t].z, acc[t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(acur.w, ring[d][t].w, acc[t]);
+        if (g + R < G) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) ring[d][t] = wload(t, g + R);
+        }
+        acur = anext;
+        __builtin_amdgcn_sched_barrier(0);   // keep the ring depth: no hoisting of later groups' loads
+    }
+}
+
+// Grid barrier: arrival counter + abort word in pbar (zeroed before the launch).  The
+// workgroup's payload stores precede it in program order (thread 0 stores them or the
+// barrier below orders them); agent-scope release on arrival, acquire after the wait.
+__device__ inline bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(pbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(pbar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
+                __hip_atomic_store(pbar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *s_flag = ok;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// ---- per-iteration partials: data-tagged granules (no fences, no counter) ----
+// Each workgroup publishes its block partial as two 16-byte granules, each ONE write-through
+// (`sc1`) buffer store carrying the tag t + 1 in its last word:
+//   g0 = {sumvar lo, sumvar hi, notclose, tag},  g1 = {maxabs (f32 bits), minsecmax (f32 bits), 0, tag}
+// (maxabs / minsecmax are float32 values or NaN / inf: exact in f32).  Every workgroup then
+// sweeps all nwg granule pairs with `sc1` loads (L2/fabric-served, never a stale L1 line)
+// until every tag matches, and reduces them in one fixed order, so every workgroup derives
+// bit-identical batch scalars.  The granule block is zeroed before every launch (tag 0 never
+// matches).  MI355X_MICROARCH.md § visibility (R2 granules, allgather).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void part_publish(PartAcc p, __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned tag,
+                                             void* lds_scratch) {
+    part_wave_reduce(p);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    __syncthreads();
+    if (lane == 0) {
+        s[wave].sumvar = p.sumvar; s[wave].maxabs = p.maxabs;
+        s[wave].minsecmax = p.minsecmax; s[wave].notclose = p.notclose;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sv = s[0].sumvar, mx = s[0].maxabs, mn = s[0].minsecmax;
+        uint32_t nc = s[0].notclose;
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
+            sv += s[w].sumvar; mx = nan_max(mx, s[w].maxabs); mn = nan_min(mn, s[w].minsecmax); nc += s[w].notclose;
+        }
+        const unsigned long long b = (unsigned long long)__double_as_longlong(sv);
+        const u32x4 g0 = {(unsigned)b, (unsigned)(b >> 32), nc, tag};
+        const u32x4 g1 = {__float_as_uint((float)mx), __float_as_uint((float)mn), 0u, tag};
+        __builtin_amdgcn_raw_buffer_store_b128(g0, rs, (int)off, 0, 16);        // aux 16 = sc1
+        __builtin_amdgcn_raw_buffer_store_b128(g1, rs, (int)off + 16, 0, 16);
+    }
+}
+
+// Wave 0 sweeps the nwg (<= 256) granule pairs of one iteration; the result lands in every
+// thread.  A bounded spin (2 s) raises the abort word, as grid_sync does.
+__device__ __forceinline__ bool part_gather(__amdgpu_buffer_rsrc_t rs, unsigned off0, int nwg, unsigned tag,
+                                            unsigned* abort_word, PartAcc& out, void* lds_scratch, int* s_flag) {
+    Partial* s = reinterpret_cast<Partial*>(lds_scratch);
+    if ((threadIdx.x >> 6) == 0) {
+        const int lane = threadIdx.x & 63;
+        u32x4 a[4], b[4];
+        int ok_all = 1;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int w = lane + 64 * q;
+                if (w < nwg) {
+                    a[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off0 + 32u * w), 0, 16);
+                    b[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off0 + 32u * w + 16), 0, 16);
+                    ok &= (a[q].w == tag) & (b[q].w == tag);
+                }
+            }
+            if (__all(ok)) break;
+            if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                __builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
+                __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok_all = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        PartAcc p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (lane + 64 * q < nwg) {
+                p.sumvar += __longlong_as_double((long long)(((unsigned long long)a[q].y << 32) | a[q].x));
+                p.maxabs = nan_max(p.maxabs, (double)__uint_as_float(b[q].x));
+                p.minsecmax = nan_min(p.minsecmax, (double)__uint_as_float(b[q].y));
+                p.notclose += a[q].z;
+            }
+        }
+        part_wave_reduce(p);
+        if (lane == 0) {
+            s[0].sumvar = p.sumvar; s[0].maxabs = p.maxabs; s[0].minsecmax = p.minsecmax; s[0].notclose = p.notclose;
+            *s_flag = ok_all;
+        }
+    }
+    __syncthreads();
+    out.sumvar = s[0].sumvar; out.maxabs = s[0].maxabs; out.minsecmax = s[0].minsecmax; out.notclose = s[0].notclose;
+    const bool ok = *s_flag != 0;
+    __syncthreads();
+    return ok;
+}
+
+}  // namespace amp

@@ -10,108 +10,12 @@
 // exact-float64 fix-up workgroup.  The second GEMM's column tile holds whole coupling
 // blocks (2*Nt columns) so psi is formed in its epilogue.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
-#include "amp_denoise.h"
-#include "amp_gemm.h"
-#include "amp_host.h"
+#include "amp_scamp.h"
 
 namespace amp {
-
-constexpr int SRWG = 1024;
-constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in registers / LDS
-
-struct alignas(16) ScampIter {
-    int32_t stopped, T, fixed, fixed_all;
-    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done by scamp_fix_*,
-    // settled by scamp_fin): the exact batch max |xi| G, the float32 estimate's slack, and the
-    // allclose count before the fix-up
-    double G, slack;
-    uint32_t notclose;
-    int32_t active, pad[2];
-};
-
-struct ScampK {
-    int B, N, n, L, M, Nt, Nr, Na, Lin, Lout, bn;
-    int kapA, ncpA, kapB, ncpB;
-    int nblk, max_iter;
-    float sigma2;          // f32(noise_var) (scamp.py:51)
-    const float* W;        // [Lout][Lin]
-    const float* WA;       // [ncpA][kapA]  A xmmse
-    const float* WAH;      // [ncpB][kapB]  A^H (z/phi)
-    const float* y;        // [B][2n]
-    float* z;              // [B][2n]
-    float* s;              // [B][2n] z / phi_use
-    float* phi;            // [2][B][Lout] ping-pong
-    float* tau;            // [B][Lin] (per iteration)
-    float* xmap;           // caller [B][2N]
-    float* xm;             // caller [B][2N]
-    float* psi0;           // caller's psi [B][Lin] (even iterations)
-    float* psi1;           // workspace     (odd iterations)
-    float* secmax;         // [B*L] per-section max logit (fast path)
-    float* secabs;         // [B*L] per-section max |logit|
-    Partial* parts;
-    ScampIter* iters;
-    unsigned* psi_nc;      // [max_iter][psi_nblk] allclose counts of scamp_psi (split tiles only)
-    int psi_nblk, psi_split;
-    amp_status* status;
-    Const c;
-};
-
-struct ScampWs {
-    float *WA, *WAH, *z, *s, *phi, *tau, *psi1;
-    float *secmax, *secabs;
-    Partial* parts;
-    ScampIter* iters;
-    unsigned* psi_nc;
-    size_t bytes;
-};
-
-// 128 columns whenever a section fits (2M <= 128): twice the workgroups of a whole-coupling-
-// block tile (cfg3: 256 instead of 128).  A tile that does not hold whole coupling blocks
-// (2 Nt > BN) leaves psi to scamp_psi.
-static int scamp_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
-static int scamp_psi_nblk(const amp_dims* d) { return std::max(1, std::min(cdiv(d->B * d->Lin, AMP_WG / 64), 2048)); }
-
-static void scamp_geometry(const amp_dims* d, ScampK& P) {
-    P.B = d->B; P.N = d->N; P.n = d->n; P.L = d->L; P.M = d->M;
-    P.Nt = d->Nt; P.Nr = d->Nr; P.Na = d->Na; P.Lin = d->Lin; P.Lout = d->Lout;
-    P.bn = scamp_bn(d);
-    P.kapA = round_up(2 * d->N, GBK); P.ncpA = round_up(2 * d->n, 128);
-    P.kapB = round_up(2 * d->n, GBK); P.ncpB = round_up(2 * d->N, P.bn);
-    P.nblk = cdiv(d->B, GBM) * (P.ncpB / P.bn);
-}
-
-static ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
-    ScampK P;
-    scamp_geometry(d, P);
-    Carve cv(base);
-    ScampWs w;
-    w.WA = cv.take<float>((size_t)P.ncpA * P.kapA);
-    w.WAH = cv.take<float>((size_t)P.ncpB * P.kapB);
-    w.z = cv.take<float>((size_t)d->B * 2 * d->n);
-    w.s = cv.take<float>((size_t)d->B * 2 * d->n);
-    w.phi = cv.take<float>((size_t)2 * d->B * d->Lout);
-    w.tau = cv.take<float>((size_t)d->B * d->Lin);
-    w.psi1 = cv.take<float>((size_t)d->B * d->Lin);
-    w.secmax = cv.take<float>((size_t)d->B * d->L);
-    w.secabs = cv.take<float>((size_t)d->B * d->L);
-    w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
-    w.iters = cv.take<ScampIter>((size_t)max_iter + 1);
-    w.psi_nc = cv.take<unsigned>((size_t)max_iter * scamp_psi_nblk(d));
-    w.bytes = cv.off;
-    return w;
-}
-
-__device__ __forceinline__ float* spsi(const ScampK& P, int t) { return (t & 1) ? P.psi1 : P.psi0; }
-__device__ __forceinline__ float* sphi(const ScampK& P, int t) { return P.phi + (size_t)(t & 1) * P.B * P.Lout; }
-
-// gamma[lo] = (W psi)[lo] / Lc (scamp.py:45), float32 as torch's [Lout x Lin] @ [Lin] product
-__device__ __forceinline__ float scamp_gamma(const ScampK& P, const float* psi_row, int lo) {
-    float g = 0.f;
-    for (int lc = 0; lc < P.Lin; ++lc) g += P.W[lo * P.Lin + lc] * psi_row[lc];
-    return g / (float)P.Lin;
-}
 
 // z = y - A xmmse + b z ; phi = sigma2 + gamma ; s = z / phi   (scamp.py:45-51, 57)
 __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
@@ -544,9 +448,25 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.psi_nc = w.psi_nc; P.psi_nblk = scamp_psi_nblk(d); P.psi_split = (P.bn / 2 < P.Nt) ? 1 : 0;
+    P.nwg = cdiv(d->B, 16);
+    P.gen = 0;
+    P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
     P.c = to_const(c);
     c64 = to_const64(c);
     return AMP_OK;
+}
+
+// The persistent engine's operators (16x16x4-packed A and A^H) and zeroed barrier words, in one
+// launch; a fresh generation for the granule tags.
+static int scamp_persist_prepare(ScampK& P, const amp_scamp_args* a, hipStream_t st) {
+    static std::atomic<unsigned> gen{0};
+    P.gen = ++gen;
+    CWeightJob j[2];
+    //   A x       (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N
+    j[0] = CWeightJob{(const float2*)a->A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.n, WPACK16};
+    //   A^H s     (scamp.py:57)   X[o][j] = conj(A[j][o]),  o < N, j < n
+    j[1] = CWeightJob{(const float2*)a->A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.Wq2, 2 * P.n, 2 * P.N, WPACK16};
+    return build_cweights(j, 2, P.pbar, 64, st);
 }
 
 // Tracker (scamp.py:9-25): the two weights and the initial state.
@@ -589,12 +509,30 @@ static int scamp_finalize_impl(const ScampK& P, hipStream_t st) {
 
 extern "C" {
 
+int amp_scamp_select_engine(const amp_dims* d, int32_t engine) {
+    if (!d) return AMP_E_ARG;
+    const bool elig = scamp_persist_eligible(d, device_cu_count());
+    if (engine == AMP_ENGINE_PERSISTENT) return elig ? AMP_ENGINE_PERSISTENT : AMP_E_ARG;
+    if (engine == AMP_ENGINE_AUTO && elig) return AMP_ENGINE_PERSISTENT;
+    return engine == AMP_ENGINE_AUTO || engine == AMP_ENGINE_LAUNCHES ? AMP_ENGINE_LAUNCHES : AMP_E_ARG;
+}
+
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {
     ScampK P;
     Const64 c64;
     int rc = scamp_setup(d, c, a, P, c64);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    AMP_REQUIRE(a->engine >= AMP_ENGINE_AUTO && a->engine <= AMP_ENGINE_PERSISTENT, "amp_scamp_run: engine %d",
+                a->engine);
+    const bool elig = scamp_persist_eligible(d, device_cu_count());
+    AMP_REQUIRE(a->engine != AMP_ENGINE_PERSISTENT || elig,
+                "amp_scamp_run: persistent engine needs (2N, 2n) in {(128, 256), (256, 512), (256, 256)}, M <= 64 "
+                "and ceil(B/16) = %d <= %d CUs", cdiv(d->B, 16), device_cu_count());
+    if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
+        if ((rc = scamp_persist_prepare(P, a, st))) return rc;
+        return scamp_persist_launch(P, c64, st);
+    }
     if ((rc = scamp_prepare_impl(P, a, st))) return rc;
     for (int t = 0; t < P.max_iter; ++t)
         if ((rc = scamp_iterate_impl(P, c64, t, st))) return rc;

@@ -122,9 +122,13 @@ class SCAMPLayer(nn.Module):
 
 
 class SCAMP(LazyResult, nn.Module):
-    def __init__(self, config: Config) -> None:
+    """``engine``: nat.ENGINE_AUTO (the persistent single-launch engine when the shape allows it,
+    else seven launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h)."""
+
+    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO) -> None:
         super().__init__()
         self.config = config
+        self.engine = engine
         self.E = config.Na / config.Nr                                    # scamp.py:72
         self.layers = nn.ModuleList([SCAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
@@ -147,6 +151,7 @@ class SCAMP(LazyResult, nn.Module):
         """All iterations on the device, asynchronous (no host sync)."""
         with torch.cuda.device(y.device):
             T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
+            T.args.engine = self.engine
             T._call('amp_scamp_run')
         self._keep = T
         return T
@@ -156,6 +161,7 @@ class SCAMP(LazyResult, nn.Module):
         """scamp.py:77-107; the counters resolve lazily (see LazyResult)."""
         with torch.cuda.device(y.device):
             T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
+            T.args.engine = self.engine
             res, host = self._result_slot(T.y.device)
             T.res = res
             T.args.status = nat.dptr(res)

@@ -190,7 +190,7 @@ typedef struct amp_scamp_args {
     const void* A;      /* c64 [n][N] */
     const void* y;      /* c64 [B][n] */
     int32_t max_iter;
-    int32_t pad;
+    int32_t engine;     /* amp_scamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT (as for VAMP) */
     double noise_var;   /* Na/Nr/SNR (scamp.py:98) */
     void* xmap;         /* out c64 [B][N] (scamp.py:107) */
     void* xmmse;        /* out c64 [B][N] */
@@ -201,6 +201,14 @@ typedef struct amp_scamp_args {
 } amp_scamp_args;
 
 size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
+/* Engines of amp_scamp_run (same results up to f32 summation order):
+ *  LAUNCHES   seven launches per iteration (the layer-level path below);
+ *  PERSISTENT one launch for the whole loop: each workgroup keeps 16 trials' x, xmap, z in LDS
+ *             across iterations; one granule exchange per iteration carries the batch-global
+ *             max|xi| and allclose count (needs (2N, 2n) in {(128, 256), (256, 512), (256, 256)},
+ *             M <= 64 and ceil(B/16) workgroups co-resident);
+ *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
+int amp_scamp_select_engine(const amp_dims* d, int32_t engine);
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
 /* Layer-level pieces of amp_scamp_run, as for BAMP: prepare = Tracker (scamp.py:9-25), iterate(t)
  * = one SCAMPLayer.forward (scamp.py:43-59) + the allclose(psi) early exit of scamp.py:105,

@@ -34,6 +34,8 @@ CFGS = {
     'cfg1': ('bamp', 4, 1, 8, 100, 'QPSK', 10, 8.0),
     'cfg2': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
     'cfg3': ('scamp', 128, 8, 256, 4096, '16QAM', 20, 8.0),
+    'cfg3-launches': ('scamp', 128, 8, 256, 4096, '16QAM', 20, 8.0),   # the launch engine, for comparison
+    'cfg3-qpsk': ('scamp', 128, 8, 256, 4096, 'QPSK', 20, 2.0),
     'cfg4': ('vamp', 256, 8, 512, 4096, '16QAM', 20, 8.0),
 }
 
@@ -59,7 +61,8 @@ def main(steps=50, warmup=30, only=None):
             det, args = VAMP(cfg), (mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
             flop = 16.0 * Nt * min(Nt, Nr)
         elif algo == 'scamp':
-            det, args = SCAMP(cfg), (mv(W), mv(A), mv(y), SNR, mv(x), sym, idx)
+            eng = nat.ENGINE_LAUNCHES if name.endswith('launches') else nat.ENGINE_AUTO
+            det, args = SCAMP(cfg, engine=eng), (mv(W), mv(A), mv(y), SNR, mv(x), sym, idx)
             flop = 16.0 * Nr * Nt
         else:
             det, args = BAMP(cfg), (mv(A), mv(y), SNR, mv(x), sym, idx)
@@ -76,7 +79,7 @@ def main(steps=50, warmup=30, only=None):
         ms = (time.perf_counter() - t0) / steps * 1e3
         T = int(L.loss['T'])
         tf = B * T * flop / (ms * 1e-3) / 1e12
-        print(json.dumps({'config': name, 'algo': algo, 'Nt': Nt, 'Nr': Nr, 'Na': Na, 'alphabet': alph, 'B': B,
+        print(json.dumps({'config': name, 'algo': algo, 'engine': getattr(det, 'engine', None), 'Nt': Nt, 'Nr': Nr, 'Na': Na, 'alphabet': alph, 'B': B,
                           'EbN0': ebn0, 'T': T, 'ver': float(L.loss['ver']), 'ser': float(L.loss['ser']),
                           'ms_per_epoch': round(ms, 4), 'symbol_vectors_per_s': B / (ms * 1e-3),
                           'trial_iterations_per_s': B * T / (ms * 1e-3), 'achieved_TFLOPs': round(tf, 2),
