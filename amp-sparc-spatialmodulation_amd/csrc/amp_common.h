@@ -82,7 +82,7 @@ __device__ __forceinline__ bool torch_close(float a, float b) {
 // Butterfly steps run with the partner distance O ascending, so before step O every aligned
 // group of O lanes already holds one value and any pairing of the two halves of a 2O group
 // works: DPP quad_perm for O = 1, 2, row_half_mirror / row_mirror for O = 4, 8 (no LDS
-// traffic, foldable into the consuming VALU op), ds_swizzle xor for 16, bpermute for 32.
+// traffic, foldable into the consuming VALU op), permlane16 / permlane32 swaps for 16, 32.
 // Every lane ends with the same bits (the combining ops are commutative).
 template <int O>
 __device__ __forceinline__ int xl_i32(int v) {
@@ -90,8 +90,15 @@ __device__ __forceinline__ int xl_i32(int v) {
     else if constexpr (O == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
     else if constexpr (O == 4) return __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true); // row_half_mirror
     else if constexpr (O == 8) return __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true); // row_mirror
-    else if constexpr (O == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);            // xor 16 in 32
-    else return __shfl_xor(v, 32, 64);
+    else {
+        // xor 16 / xor 32: gfx950's v_permlane16_swap / v_permlane32_swap (VALU, no LDS round
+        // trip as ds_swizzle / ds_bpermute would take): r[0] holds the even half's value and
+        // r[1] the odd half's in every lane; the partner's is the other half's
+        const unsigned u = (unsigned)v;
+        const auto r = (O == 16) ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                                 : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        return (int)((threadIdx.x & O) ? r[0] : r[1]);
+    }
 }
 template <int O> __device__ __forceinline__ float xl(float v) { return __int_as_float(xl_i32<O>(__float_as_int(v))); }
 template <int O> __device__ __forceinline__ int xl(int v) { return xl_i32<O>(v); }
@@ -121,36 +128,54 @@ __device__ __forceinline__ void xl_pair(float v, float& lo, float& hi) {
         hi = odd ? v : p;
     }
 }
-template <int O, class Op>
-__device__ __forceinline__ float xl_op(float v, Op op) {
+// Group max of float32 values as an integer max over order-preserving keys: the DPP row
+// operations then fuse into v_max_i32_dpp (one instruction per butterfly step; fmaxf needs a
+// canonicalising v_max_f32 after every DPP move in IEEE mode).  Key order:
+// -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN, so a (positive, default) NaN wins like
+// torch.max; callers flag non-finite inputs separately (DenStat::st_bad).
+__device__ __forceinline__ int fkey(float f) {
+    const int b = __float_as_int(f);
+    return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float funkey(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+template <int O>
+__device__ __forceinline__ int imax_step(int v) {
     if constexpr (O == 16 || O == 32) {
-        float lo, hi;
-        xl_pair<O>(v, lo, hi);
-        return op(lo, hi);
+        const unsigned u = (unsigned)v;
+        const auto r = (O == 16) ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                                 : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        return max((int)r[0], (int)r[1]);
     } else {
-        return op(v, xl<O>(v));
+        return max(v, xl_i32<O>(v));
     }
 }
-template <int G, class Op>
-__device__ __forceinline__ float group_reduce_c(float v, Op op) {
-    if constexpr (G > 1) v = xl_op<1>(v, op);
-    if constexpr (G > 2) v = xl_op<2>(v, op);
-    if constexpr (G > 4) v = xl_op<4>(v, op);
-    if constexpr (G > 8) v = xl_op<8>(v, op);
-    if constexpr (G > 16) v = xl_op<16>(v, op);
-    if constexpr (G > 32) v = xl_op<32>(v, op);
+template <int G>
+__device__ __forceinline__ int group_imax_c(int v) {
+    if constexpr (G > 1) v = imax_step<1>(v);
+    if constexpr (G > 2) v = imax_step<2>(v);
+    if constexpr (G > 4) v = imax_step<4>(v);
+    if constexpr (G > 8) v = imax_step<8>(v);
+    if constexpr (G > 16) v = imax_step<16>(v);
+    if constexpr (G > 32) v = imax_step<32>(v);
     return v;
 }
 template <int G>
-__device__ __forceinline__ float group_fmax_c(float v) { return group_reduce_c<G>(v, [](float a, float b) { return fmaxf(a, b); }); }
-// Sum over the group (same bits in every lane) and, per lane, the sum of every OTHER lane of
-// the group: a sum of non-negative terms when the inputs are, so Z - Z_m needs no subtraction.
+__device__ __forceinline__ float group_fmax_c(float v) { return funkey(group_imax_c<G>(fkey(v))); }
+// Sum over the group (same bits in every lane: float addition is commutative) and, per lane,
+// the sum of every OTHER lane of the group: a sum of non-negative terms when the inputs are,
+// so Z - Z_m needs no subtraction.  DPP distances fuse into v_add_f32_dpp.
 template <int O>
 __device__ __forceinline__ void sum_excl_step(float& tot, float& excl) {
-    float lo, hi;
-    xl_pair<O>(tot, lo, hi);
-    excl += (threadIdx.x & O) ? lo : hi;
-    tot = lo + hi;
+    if constexpr (O == 16 || O == 32) {
+        float lo, hi;
+        xl_pair<O>(tot, lo, hi);
+        excl += (threadIdx.x & O) ? lo : hi;
+        tot = lo + hi;
+    } else {
+        const float p = xl<O>(tot);
+        excl += p;
+        tot = tot + p;
+    }
 }
 template <int G>
 __device__ __forceinline__ void group_sum_excl_c(float& tot, float& excl) {
@@ -287,9 +312,15 @@ __device__ __forceinline__ void nan_fill(float* xm, float* var, size_t n) {
 }
 
 // Constellation for the fast path (kept small: it lives in SGPRs of every fused kernel).
+// Product-grid decomposition (amp_denoise.h, denoise_step_grid): grid = R when every point is
+// (gre[i], gim[j]) of an R x R grid (R = 2, 4, 8, values ascending) with a multiplicity pattern
+// the kernels know at compile time: gfull = 1 every point once (GRID_FULL), 2 the reference's
+// 16-QAM table (GRID_REF16); otherwise grid = 0 and the direct form runs.
 struct Const {
     int K;
     float re[AMP_MAX_K], im[AMP_MAX_K];
+    int grid, gfull;
+    float gre[8], gim[8];
 };
 
 // Constellation in float64 for the reference-exact rare path (never in a hot kernel's args).

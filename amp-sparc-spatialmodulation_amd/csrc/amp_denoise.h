@@ -261,8 +261,215 @@ __device__ __forceinline__ void denoise_step_gp(const P& pol, int base, int nsec
     }
 }
 
+// ---- Product-grid form (square QAM-like alphabets: Const::grid == R) ----
+// Every point is (gre[i], gim[j]) of an R x R grid, so the logits and their exponentials factor
+// over rows and columns:
+//   xi_ij = X_i + Y_j,   X_i = Re(r / tau) gre_i,   Y_j = Im(r / tau) gim_j
+//   exp(xi_ij - smax) = er_i ei_j f,  er_i = exp(X_i - max X), ei_j = exp(Y_j - max Y),
+//                                     f = exp(max X + max Y - smax)
+// and every per-position sum of vamp.py:113-118 is a sum over rows of a row factor times a
+// column sum weighted by the table's multiplicities c_ij (0, 1, 2; all 1 for a full grid):
+//   z_m = f sum_i er_i S_i,           S_i = sum_j c_ij ei_j
+//   sum_k a_k eta_k = f (sum_i gre_i er_i S_i, sum_i er_i T_i),   T_i = sum_j c_ij gim_j ei_j
+//   sum_k |x - a_k|^2 eta_k = f sum_i er_i ((Re x - gre_i)^2 S_i + V_i),
+//                                     V_i = sum_j c_ij (Im x - gim_j)^2 ei_j
+// A position costs 2R + 1 exponentials and O(R^2) FMAs (O(R) for a full grid) instead of K
+// exponentials and ~12 K operations.  Every sum adds non-negative terms (a missing grid point
+// has weight 0: nothing is subtracted), so nothing cancels; the float32 rounding differs from
+// the direct form by a few ulp (the reference works in float64 throughout).  The max / min
+// logit of a position are max X + max Y / min X + min Y: a linear form over the grid takes its
+// extremes at the corners, which are in the table (checked on the host, amp_host.h).
+// Multiplicity patterns of the grid points (compile-time, so the unrolled sums below fold:
+// weight 0 drops a term, 1 is an add, 2 an FMA by 2):
+//   GRID_FULL  every grid point once (QPSK, square 64-QAM);
+//   GRID_REF16 the reference's 16-QAM table (config.py:112) on the sorted grid
+//              {-3,-1,1,3}/sqrt(10): -1+3j twice, 1-3j missing.
+enum { GRID_FULL = 1, GRID_REF16 = 2 };
+template <int PAT>
+__device__ __forceinline__ constexpr float grid_cnt(int i, int j) {
+    if constexpr (PAT == GRID_REF16) return (i == 1 && j == 3) ? 2.f : (i == 2 && j == 0) ? 0.f : 1.f;
+    else return 1.f;
+}
+
+template <int R>
+struct GridRegs {
+    float re[R], im[R];
+    __device__ __forceinline__ void load(const Const& c) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            re[i] = kval(c.gre[i]); im[i] = kval(c.gim[i]);
+            asm volatile("" : "+v"(re[i]), "+v"(im[i]));
+        }
+    }
+};
+
+template <bool kVar, int R, int PAT, int U, int G, class P>
+__device__ __forceinline__ void denoise_step_grid(const P& pol, int base, int nsec, const GridRegs<R>& Q,
+                                                  PartAcc& pa, DenStat& S) {
+    constexpr bool FULLG = PAT == GRID_FULL;
+    const int lane = threadIdx.x & 63;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    int sec[U];
+    bool act[U];
+    float X[U][R], Y[U][R], mx[U], my[U], lmx[U], smax[U], sabs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        sec[u] = base + u * gpw + gid;
+        act[u] = sec[u] < nsec;
+        float rr, ri, it;
+        pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
+        const float ur = rr * it, ui = ri * it;   // c64 / f32 == multiply by the reciprocal
+        S.st_bad |= act[u] && !(fabsf(ur) <= FLT_MAX && fabsf(ui) <= FLT_MAX);
+        float ax = -FLT_MAX, nx = FLT_MAX, ay = -FLT_MAX, ny = FLT_MAX;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            X[u][i] = ur * Q.re[i];
+            Y[u][i] = ui * Q.im[i];
+            ax = fmaxf(ax, X[u][i]); nx = fminf(nx, X[u][i]);
+            ay = fmaxf(ay, Y[u][i]); ny = fminf(ny, Y[u][i]);
+        }
+        mx[u] = ax; my[u] = ay;
+        lmx[u] = ax + ay;                          // max logit of the position (a corner)
+        smax[u] = lmx[u];
+        sabs[u] = fmaxf(lmx[u], -(nx + ny));       // max |logit|
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { smax[u] = group_fmax_c<G>(smax[u]); sabs[u] = group_fmax_c<G>(sabs[u]); }
+    float zt[U], ze[U], ar[U], ai[U], f[U];
+    float er[U][R], ei[U][R], Sr[U][FULLG ? 1 : R];
+    float SI[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        f[u] = __builtin_amdgcn_exp2f((lmx[u] - smax[u]) * AMP_LOG2E);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            er[u][i] = __builtin_amdgcn_exp2f((X[u][i] - mx[u]) * AMP_LOG2E);
+            ei[u][i] = __builtin_amdgcn_exp2f((Y[u][i] - my[u]) * AMP_LOG2E);
+        }
+        if constexpr (FULLG) {
+            float sr = 0.f, si = 0.f, a = 0.f, b = 0.f;
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                sr += er[u][i]; si += ei[u][i];
+                a = fmaf(Q.re[i], er[u][i], a);
+                b = fmaf(Q.im[i], ei[u][i], b);
+            }
+            SI[u] = si; Sr[u][0] = sr;
+            zt[u] = (sr * si) * f[u];
+            ar[u] = (a * si) * f[u];
+            ai[u] = (sr * b) * f[u];
+        } else {
+            float z = 0.f, a = 0.f, b = 0.f, w[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) w[j] = Q.im[j] * ei[u][j];
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                float si = 0.f, ti = 0.f;
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const float cw = grid_cnt<PAT>(i, j);
+                    if (cw == 1.f) { si += ei[u][j]; ti += w[j]; }
+                    else if (cw == 2.f) { si = fmaf(2.f, ei[u][j], si); ti = fmaf(2.f, w[j], ti); }
+                }
+                Sr[u][i] = si;
+                const float es = er[u][i] * si;
+                z += es;
+                a = fmaf(Q.re[i], es, a);
+                b = fmaf(er[u][i], ti, b);
+            }
+            zt[u] = z * f[u];
+            ar[u] = a * f[u];
+            ai[u] = b * f[u];
+        }
+        ze[u] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const float iz = __builtin_amdgcn_rcpf(zt[u]);
+        const float xr = ar[u] * iz, xi = ai[u] * iz;
+        float var = 0.f;
+        if (kVar) {
+            float vs;
+            if constexpr (FULLG) {
+                float vr = 0.f, vi = 0.f;
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    const float dr = xr - Q.re[i], di = xi - Q.im[i];
+                    vr = fmaf(dr * dr, er[u][i], vr);
+                    vi = fmaf(di * di, ei[u][i], vi);
+                }
+                vs = fmaf(vr, SI[u], Sr[u][0] * vi) * f[u];
+            } else {
+                float d[R];
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const float di = xi - Q.im[j];
+                    d[j] = (di * di) * ei[u][j];
+                }
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    float vi = 0.f;
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        const float cw = grid_cnt<PAT>(i, j);
+                        if (cw == 1.f) vi += d[j];
+                        else if (cw == 2.f) vi = fmaf(2.f, d[j], vi);
+                    }
+                    const float dr = xr - Q.re[i];
+                    acc = fmaf(er[u][i], fmaf(dr * dr, Sr[u][i], vi), acc);
+                }
+                vs = acc * f[u];
+            }
+            var = (xr * xr + xi * xi) * (ze[u] * iz) + vs * iz;
+        }
+        if (act[u]) {
+            pol.store(sec[u], g, xr, xi, var, pa);
+            S.st_abs = nan_max(S.st_abs, sabs[u]);
+            S.st_min = nan_min(S.st_min, smax[u]);
+            if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
+        }
+    }
+}
+
+// Grid dimension of a compile-time constellation size (0: no product-grid form).
+template <int KK>
+constexpr int grid_r() { return KK == 4 ? 2 : KK == 16 ? 4 : KK == 64 ? 8 : 0; }
+
+// The grid loop over this wave's sections; returns false (nothing done) when c is not a grid of
+// the size KK admits.  c.grid / c.gfull are kernel arguments: the branch is uniform.
+template <bool kVar, int KK, int U, int G, class P>
+__device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    constexpr int R = grid_r<KK>();
+    if constexpr (R == 0) {
+        return false;
+    } else {
+        const int grid = __builtin_amdgcn_readfirstlane(c.grid), gfull = __builtin_amdgcn_readfirstlane(c.gfull);
+        if (grid != R) return false;
+        const int wave = threadIdx.x >> 6;
+        constexpr int gpw = 64 / G;
+        const int nw = blockDim.x >> 6;
+        DenStat S;
+        GridRegs<R> Q;
+        Q.load(c);
+        if (gfull == GRID_FULL) {
+            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U)   // wave-uniform trip count
+                denoise_step_grid<kVar, R, GRID_FULL, U, G>(pol, base, nsec, Q, pa, S);
+        } else if constexpr (R == 4) {
+            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U)
+                denoise_step_grid<kVar, R, GRID_REF16, U, G>(pol, base, nsec, Q, pa, S);
+        }
+        S.fold(pa);
+        return true;
+    }
+}
+
 template <bool kVar, int KK, int U, int G, class P>
 __device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+    if (denoise_sections_grid<kVar, KK, U, G>(pol, nsec, c, pa)) return;
     const int wave = threadIdx.x >> 6;
     constexpr int gpw = 64 / G;
     const int nw = blockDim.x >> 6;
@@ -303,6 +510,7 @@ __device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M
 template <bool kVar, int KK, int G, class P>
 __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, const Const& c, PartAcc& pa) {
     static_assert(KK % 8 == 0, "chunks of 8 points");
+    if (denoise_sections_grid<kVar, KK, 1, G>(pol, nsec, c, pa)) return;   // square 64-QAM
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int gpw = 64 / G;
     const int gid = lane / G, g = lane % G;

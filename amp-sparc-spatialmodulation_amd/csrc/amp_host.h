@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <string>
+#include <algorithm>
+#include <stdlib.h>
 
 #include "amp_common.h"
 
@@ -48,6 +50,62 @@ struct Carve {
     }
 };
 
+// The product-grid form of the denoiser (amp_denoise.h) applies when the float32 points take
+// R distinct real and R distinct imaginary values with K = R^2 (R = 2, 4, 8), the grid's four
+// corners are in the table and the multiplicities follow a pattern the kernels know (every
+// point once, or the reference's 16-QAM table).  QPSK, the reference's
+// 16-QAM table (config.py:112: -1+3j twice, 1-3j missing) and square 64-QAM qualify; PSK and the
+// real alphabets keep the direct form.  AMP_GRID_DENOISER=0 disables it (A/B runs).
+inline bool grid_denoiser_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("AMP_GRID_DENOISER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+inline void grid_decompose(Const& k) {
+    k.grid = 0;
+    k.gfull = 0;
+    for (int i = 0; i < 8; ++i) k.gre[i] = k.gim[i] = 0.f;
+    if (!grid_denoiser_enabled()) return;
+    float re[8], im[8];
+    int nr = 0, ni = 0;
+    for (int p = 0; p < k.K; ++p) {
+        int a = 0, b = 0;
+        while (a < nr && re[a] != k.re[p]) ++a;
+        while (b < ni && im[b] != k.im[p]) ++b;
+        if (a == nr) { if (nr == 8) return; re[nr++] = k.re[p]; }
+        if (b == ni) { if (ni == 8) return; im[ni++] = k.im[p]; }
+    }
+    const int R = nr;
+    if (ni != R || !(R == 2 || R == 4 || R == 8) || R * R != k.K) return;
+    std::sort(re, re + R);
+    std::sort(im, im + R);
+    int cnt[8][8] = {};
+    for (int p = 0; p < k.K; ++p) {
+        const int a = (int)(std::find(re, re + R, k.re[p]) - re), b = (int)(std::find(im, im + R, k.im[p]) - im);
+        if (++cnt[a][b] > 2) return;
+    }
+    if (!cnt[0][0] || !cnt[0][R - 1] || !cnt[R - 1][0] || !cnt[R - 1][R - 1]) return;
+    bool full = true;
+    for (int a = 0; a < R; ++a)
+        for (int b = 0; b < R; ++b) full &= cnt[a][b] == 1;
+    int pat = full ? 1 : 0;                       // GRID_FULL (amp_denoise.h)
+    if (!full && R == 4) {
+        // GRID_REF16: config.py:112 on the sorted grid (-1+3j twice, 1-3j missing)
+        bool ref = true;
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                ref &= cnt[a][b] == ((a == 1 && b == 3) ? 2 : (a == 2 && b == 0) ? 0 : 1);
+        if (ref) pat = 2;
+    }
+    if (!pat) return;
+    for (int a = 0; a < R; ++a) { k.gre[a] = re[a]; k.gim[a] = im[a]; }
+    k.grid = R;
+    k.gfull = pat;
+}
+
 inline Const to_const(const amp_constellation* c) {
     Const k;
     k.K = c->K;
@@ -56,6 +114,7 @@ inline Const to_const(const amp_constellation* c) {
         k.re[i] = v ? c->re[i] : 0.f;
         k.im[i] = v ? c->im[i] : 0.f;
     }
+    grid_decompose(k);
     return k;
 }
 

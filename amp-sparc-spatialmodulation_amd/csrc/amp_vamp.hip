@@ -390,9 +390,9 @@ using namespace amp;
 extern "C" {
 
 // Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
-// boundary: trace[(wg * max_iter + t) * 8 + phase], phases = start, r~ built, GEMM1, w stored,
-// GEMM2 + r, denoiser + partial, barrier passed, scalars ready; then per workgroup
-// [nwg * max_iter * 8 + 2 * wg] = s_memtime / s_memrealtime at kernel start.
+// boundary: trace[(wg * max_iter + t) * 10 + phase], phases = start, r~ built, GEMM1, w stored,
+// GEMM2 + r, partial published, barrier passed, scalars ready, (unused), denoiser done; then per
+// workgroup [nwg * max_iter * 10 + 2 * wg] = s_memtime / s_memrealtime at kernel start.
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
                            void* stream) {
     VampK P;

@@ -32,6 +32,8 @@
 
 namespace amp {
 
+constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iteration)
+
 // LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the 16-row ds_read_b128 and the
 // accumulator stores conflict-free (row r and r+4 land 16 banks apart).
 struct PLayout {
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, 
 }
 
 // dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
-template <int NT, int KK, int NWV>
+template <int NT, int KK, int NWV, int DU>
 __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc) {
     constexpr int PWG = 64 * NWV;
     const Const64& c64 = dc;
@@ -248,11 +250,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
 
     unsigned long long* trc = P.trace;
     auto stamp = [&](int t, int ph) {
-        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * 8 + ph] = __builtin_amdgcn_s_memtime();
+        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * AMP_TRACE_STRIDE + ph] = __builtin_amdgcn_s_memtime();
     };
     if (trc && tid == 0) {
-        trc[(size_t)nwg * P.max_iter * 8 + 2 * wg] = __builtin_amdgcn_s_memtime();
-        trc[(size_t)nwg * P.max_iter * 8 + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg] = __builtin_amdgcn_s_memtime();
+        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
     }
     unsigned nbar = 0;
     const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
@@ -313,7 +315,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
         if constexpr (KK > 16)
             denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
         else
-            denoise_sections_u<true, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
+            denoise_sections_u<true, KK, DU>(pol, nrows * spr, M, P.c, pa);
+        stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
         stamp(t, 5);
@@ -462,6 +465,14 @@ static int persist_waves() {
     return w;
 }
 
+static int den_u() {
+    static int u = [] {
+        const char* e = getenv("AMP_DEN_U");
+        return e ? atoi(e) : 2;
+    }();
+    return u;
+}
+
 // Launch path: a plain launch after an explicit co-residency check (default), or
 // hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).  The cooperative path made processes
 // crash in exit-time teardown under rocprofv3 on the box (r01), the plain one does not.
@@ -473,9 +484,9 @@ static bool persist_coop() {
     return c;
 }
 
-template <int NT, int KK, int NWV>
+template <int NT, int KK, int NWV, int DU>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
     // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
@@ -511,7 +522,7 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
                   device_cu_count());
         return AMP_E_LAUNCH;
     }
-    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, dc);
+    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV, DU>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, dc);
     e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
@@ -523,12 +534,18 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
 template <int NT, int NWV>
 static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV>(P, dc, st);
-    case 16: return persist_launch_t<NT, 16, NWV>(P, dc, st);
-    default: return persist_launch_t<NT, 64, NWV>(P, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV, 4>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV, 4>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV, 4>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV, 2>(P, dc, st);
+    case 16:
+        // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8)
+        switch (den_u()) {
+        case 4: return persist_launch_t<NT, 16, NWV, 4>(P, dc, st);
+        case 8: return persist_launch_t<NT, 16, NWV, 8>(P, dc, st);
+        default: return persist_launch_t<NT, 16, NWV, 2>(P, dc, st);
+        }
+    default: return persist_launch_t<NT, 64, NWV, 1>(P, dc, st);
     }
 }
 

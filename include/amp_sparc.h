@@ -115,7 +115,7 @@ typedef struct amp_vamp_args {
  * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
- * phase into trace (device, nwg * max_iter * 8 + 2 * nwg uint64; layout in amp_vamp.hip). */
+ * phase into trace (device, nwg * max_iter * 10 + 2 * nwg uint64; layout in amp_vamp.hip). */
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
                            void* stream);
 size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter);

@@ -16,7 +16,9 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch        # noqa: E402
 
-PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser + partial', 'partial gather', 'scalars']
+PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser', 'partial publish', 'partial gather', 'scalars']
+STRIDE = 10   # stamps per (workgroup, iteration): amp_vamp_persist.hip AMP_TRACE_STRIDE
+ORDER = [0, 1, 2, 3, 4, 8, 5, 6, 7]   # stamp slots in time order
 
 
 def main():
@@ -38,7 +40,7 @@ def main():
         det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     nwg = (B + 15) // 16
-    tr = torch.zeros(nwg * iters * 8 + 2 * nwg, dtype=torch.int64, device=dev)
+    tr = torch.zeros(nwg * iters * STRIDE + 2 * nwg, dtype=torch.int64, device=dev)
     s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0.record()
     nat.check(nat.lib().amp_vamp_persist_trace(C.byref(T.dims), C.byref(T.const), C.byref(T.args), nat.dptr(tr),
@@ -47,11 +49,11 @@ def main():
     torch.cuda.synchronize()
     ms = s0.elapsed_time(e0)
     a = tr.cpu().numpy()
-    st = a[:nwg * iters * 8].reshape(nwg, iters, 8).astype(np.int64)
+    st = a[:nwg * iters * STRIDE].reshape(nwg, iters, STRIDE).astype(np.int64)[:, :, ORDER]
     Tn = int(T.status().T)
     st = st[:, :Tn]
-    d = np.diff(st, axis=2)                       # [nwg, T, 7]
-    total_cyc = np.median(st[:, -1, 7] - st[:, 0, 0])
+    d = np.diff(st, axis=2)                       # [nwg, T, 8]
+    total_cyc = np.median(st[:, -1, -1] - st[:, 0, 0])
     print(f'T={Tn}  nwg={nwg}  kernel+prepare {ms:.3f} ms (events)  median loop cycles {total_cyc:.0f}')
     per_it = np.median(st[:, 1:, 0] - st[:, :-1, 0]) if Tn > 1 else 0
     print(f'median cycles per iteration {per_it:.0f}')
@@ -62,7 +64,7 @@ def main():
     # arrival skew at the barrier: spread of stamp 5 across workgroups per iteration (same clock
     # domain only within an XCD; reported as a rough indicator)
     print('  barrier arrival spread (max - min of stamp 5, cycles, median over t):',
-          np.median(st[:, 1:, 5].max(0) - st[:, 1:, 5].min(0)) if Tn > 1 else 0)
+          np.median(st[:, 1:, 6].max(0) - st[:, 1:, 6].min(0)) if Tn > 1 else 0)
 
 
 if __name__ == '__main__':

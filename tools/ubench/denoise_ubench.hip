@@ -93,14 +93,14 @@ extern "C" int ubench_main() {
     hipMalloc(&dsink, 256 * 8 * 8);
     hipMemcpy(dr, r.data(), r.size() * 4, hipMemcpyHostToDevice);
     const float inv = 1.0f / 0.02f;
-    run<16, 1, 4, false>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 2, 4, false>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 1, 8, false>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 2, 8, false>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 1, 4, true>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 2, 4, true>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 1, 8, true>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
-    run<16, 2, 8, true>("cfg4 16QAM", dr, c, N, M, inv, dout, dsink);
+    c.grid = 0; c.gfull = 0;
+    run<16, 2, 4, true>("cfg4 16QAM direct", dr, c, N, M, inv, dout, dsink);
+    run<16, 2, 8, true>("cfg4 16QAM direct", dr, c, N, M, inv, dout, dsink);
+    grid_decompose(c);
+    printf("grid %d full %d\n", c.grid, c.gfull);
+    run<16, 1, 4, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 2, 4, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 2, 8, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
     fflush(stdout);
     return 0;
 }
