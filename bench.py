@@ -29,8 +29,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vec
 HBM_PEAK_GBS = 8000.0
 # time(oracle) / time(reference) on the same 8 cores of the build container, same cfg4 workload
 # (tools/cpu_ratio.py; the reference cannot travel to the GPU box): the port's CPU speed relative
-# to the reference's CPU path.  None until measured.
-PORT_OVER_REFERENCE = None
+# to the reference's CPU path: the two take the same time.
+PORT_OVER_REFERENCE = 1.004   # profiles/r02_cpu_ratio.json (cfg4, 1024 trials, 8 threads, median of 3)
 
 CONFIGS = {
     # name: (Nt, Na, Nr, B, alphabet, iterations)
