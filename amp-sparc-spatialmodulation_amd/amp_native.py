@@ -41,11 +41,12 @@ class AmpCounts(C.Structure):
 
 
 ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2   # amp_vamp_args.engine
+GEMM_AUTO, GEMM_F32, GEMM_X3 = 0, 1, 2                       # amp_vamp_args.gemm
 
 
 class AmpVampArgs(C.Structure):
     _fields_ = [('U', C.c_void_p), ('s', C.c_void_p), ('Vh', C.c_void_p), ('y', C.c_void_p),
-                ('k', C.c_int32), ('max_iter', C.c_int32), ('engine', C.c_int32), ('pad', C.c_int32),
+                ('k', C.c_int32), ('max_iter', C.c_int32), ('engine', C.c_int32), ('gemm', C.c_int32),
                 ('noise_var', C.c_double), ('sparsity', C.c_double),
                 ('r', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p), ('status', C.c_void_p),
                 ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]

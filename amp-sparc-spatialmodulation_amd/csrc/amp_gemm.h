@@ -65,6 +65,16 @@ __host__ __device__ __forceinline__ size_t wpack16_index(int n, int k, int kap) 
     return (((size_t)ct * (kap >> 4) + g) * 64 + lane) * 4 + (w & 3);
 }
 
+// Packing for the split-precision complex form (gemm_x3, amp_persist.h): X[o][j] (o < O complex
+// outputs, j < J complex inputs, J % 32 == 0) as bf16 pieces; 16-column tile ct = o >> 4, group
+// g = j >> 5, plane f (0-2: Re x0 x1 x2, 3-5: Im x0 x1 x2), lane (o & 15) + 16 ((j & 31) >> 3),
+// element j & 7: one 16-byte buffer load per lane and plane.
+__host__ __device__ __forceinline__ size_t x3_index(int o, int j, int f, int J) {
+    const int kk = j & 31;
+    const int lane = (o & 15) + 16 * (kk >> 3);
+    return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 6 + f) * 64 + lane) * 8 + (kk & 7);
+}
+
 // XCD-aware tile order.  Workgroups are dispatched in linear order (x fastest) round-robin over
 // the 8 XCDs, each with its own 4 MB L2.  The row-block-fastest grid would make every XCD sweep
 // ALL column blocks, i.e. the whole packed weight (8 MB for BAMP's H at cfg5) through each L2.

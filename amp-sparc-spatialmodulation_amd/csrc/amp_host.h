@@ -139,7 +139,7 @@ int device_cu_count();   // compute units of the current device (cached)
 inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
 
 // Expanded-weight builders (amp_weights.hip)
-enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2 };
+enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2, WPACKX3 = 3 };   // WPACKX3: bf16x3 planes, kap = J, ncp = O
 int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J,
                   float* wt, int kap, int ncp, hipStream_t st, int packed = WPACK32);
 // One job of build_cweights: the expanded weight of X[o][j] = rowscale_o *

@@ -17,6 +17,7 @@ namespace amp {
 constexpr int PRING = 4;   // W groups in flight per wave
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -73,6 +74,124 @@ __device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __
     }
 }
 
+// ---- split-precision complex GEMM (bf16x3) ----
+// x = x0 + x1 + x2 with bf16 pieces (round-to-nearest-even; each residual is exact in f32), so
+// a product a.b keeps the six terms a0b0 a0b1 a1b0 a0b2 a1b1 a2b0 (dropped terms <= 2^-24 |ab|)
+// and sums them on v_mfma_f32_16x16x32_bf16: the f32 products at 2.7x the f32-MFMA rate, with the
+// vector ALU free for 8 of every 16 MFMA cycles.  A non-finite x keeps x0 = x and zero residuals.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned bf16_bits(float x) {
+    return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x);
+}
+
+__device__ __forceinline__ void split3(float x, unsigned& p0, unsigned& p1, unsigned& p2) {
+    const __bf16 b0 = (__bf16)x;
+    const float r1 = __builtin_isfinite(x) ? x - (float)b0 : 0.0f;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    p0 = (unsigned)__builtin_bit_cast(unsigned short, b0);
+    p1 = (unsigned)__builtin_bit_cast(unsigned short, b1);
+    p2 = bf16_bits(r2);
+}
+
+// Eight consecutive complex values of one row -> the six bf16 planes (Re x0 x1 x2, Im x0 x1 x2)
+// of an x3 A operand: plane f, row `row`, elements j0 .. j0+7 (one 16-byte store each).
+__device__ __forceinline__ void x3_store8(unsigned short* sP, int ldx, int row, int j0, const float (&re)[8],
+                                          const float (&im)[8]) {
+    u32x4 q[6];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
+        split3(re[2 * h], a0, a1, a2);
+        split3(re[2 * h + 1], b0, b1, b2);
+        split3(im[2 * h], c0, c1, c2);
+        split3(im[2 * h + 1], d0, d1, d2);
+        q[0][h] = a0 | (b0 << 16); q[1][h] = a1 | (b1 << 16); q[2][h] = a2 | (b2 << 16);
+        q[3][h] = c0 | (d0 << 16); q[4][h] = c1 | (d1 << 16); q[5][h] = c2 | (d2 << 16);
+    }
+#pragma unroll
+    for (int f = 0; f < 6; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + j0) = q[f];
+}
+
+// One complex value -> its six plane entries (GEMM epilogues, accumulator layout).
+__device__ __forceinline__ void x3_store1(unsigned short* sP, int ldx, int row, int j, float re, float im) {
+    unsigned a0, a1, a2, b0, b1, b2;
+    split3(re, a0, a1, a2);
+    split3(im, b0, b1, b2);
+    unsigned short* p = sP + row * ldx + j;
+    const int pl = 16 * ldx;
+    p[0] = (unsigned short)a0; p[pl] = (unsigned short)a1; p[2 * pl] = (unsigned short)a2;
+    p[3 * pl] = (unsigned short)b0; p[4 * pl] = (unsigned short)b1; p[5 * pl] = (unsigned short)b2;
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// C[16 x 16 NT] (complex; Re in cr, Im in ci; this wave's complex column tiles ct0 ...) =
+// A[16 x 32 G] (complex, six bf16 planes in LDS, plane row stride ldx) . X^T, X packed by
+// x3_index (amp_gemm.h) as six planes per (tile, group).  Cr = Ar.Xr - Ai.Xi, Ci = Ar.Xi + Ai.Xr:
+// only the operator's unique values are streamed (12 bytes per complex entry, 0.75x the f32
+// real expansion).  Accumulator t, register r: row 4*(lane>>4) + r, complex column
+// 16*(ct0 + t) + (lane & 15).
+template <int NT, int G, int R = 2>
+__device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
+                                        f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
+    constexpr int RR = G < R ? G : R;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { cr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; ci[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 6 * 1024, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = lane * 16;
+    u32x4 ring[RR][NT][6];
+#pragma unroll
+    for (int d = 0; d < RR; ++d)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int f = 0; f < 6; ++f)
+                ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 6 + f) * 1024, 0);
+    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * (lane >> 4);
+    const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int d = g % RR;
+        u32x4 a[6], na[3];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * g);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const u32x4* w = ring[d][t];
+#define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
+            // smallest terms first
+            AMP_MF(cr[t], a[0], w[2]);  AMP_MF(ci[t], a[0], w[5]);
+            AMP_MF(cr[t], a[1], w[1]);  AMP_MF(ci[t], a[1], w[4]);
+            AMP_MF(cr[t], a[2], w[0]);  AMP_MF(ci[t], a[2], w[3]);
+            AMP_MF(cr[t], na[0], w[5]); AMP_MF(ci[t], a[3], w[2]);
+            AMP_MF(cr[t], na[1], w[4]); AMP_MF(ci[t], a[4], w[1]);
+            AMP_MF(cr[t], na[2], w[3]); AMP_MF(ci[t], a[5], w[0]);
+            AMP_MF(cr[t], a[0], w[1]);  AMP_MF(ci[t], a[0], w[4]);
+            AMP_MF(cr[t], a[1], w[0]);  AMP_MF(ci[t], a[1], w[3]);
+            AMP_MF(cr[t], na[0], w[4]); AMP_MF(ci[t], a[3], w[1]);
+            AMP_MF(cr[t], na[1], w[3]); AMP_MF(ci[t], a[4], w[0]);
+            AMP_MF(cr[t], a[0], w[0]);  AMP_MF(ci[t], a[0], w[3]);
+            AMP_MF(cr[t], na[0], w[3]); AMP_MF(ci[t], a[3], w[0]);
+#undef AMP_MF
+        }
+        if (g + RR < G) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int f = 0; f < 6; ++f)
+                    ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + RR) * 6 + f) * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Grid barrier: arrival counter + abort word in pbar (zeroed before the launch).  The
 // workgroup's payload stores precede it in program order (thread 0 stores them or the
 // barrier below orders them); agent-scope release on arrival, acquire after the wait.
@@ -108,8 +227,6 @@ __device__ inline bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
 // until every tag matches, and reduces them in one fixed order, so every workgroup derives
 // bit-identical batch scalars.  The granule block is zeroed before every launch (tag 0 never
 // matches).  MI355X_MICROARCH.md § visibility (R2 granules, allgather).
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
 }

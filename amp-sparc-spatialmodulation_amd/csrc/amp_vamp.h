@@ -52,6 +52,9 @@ struct VampK {
     DecWG* dwg;                 // [nwg] per-workgroup records
     amp_counts* counts;         // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
+    int x3;                      // persistent engine GEMMs on the bf16x3 engine (Wx1 / Wx2)
+    const void* Wx1;             // Vh X3-packed (x3_index, O = k, J = N)
+    const void* Wx2;             // V  X3-packed (O = N, J = k)
     Const c;
 };
 
@@ -61,6 +64,7 @@ struct VampWs {
     Partial* parts;
     VampIter* iters;
     float *Wq0, *Wq1, *Wq2;
+    float *Wx1, *Wx2;
     Partial* pparts;
     double* pxch;
     unsigned* pbar;
@@ -98,6 +102,8 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.Wq0 = cv.take<float>((size_t)2 * k * 2 * d->n);
     w.Wq1 = cv.take<float>((size_t)2 * k * 2 * d->N);
     w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * k);
+    w.Wx1 = cv.take<float>((size_t)3 * k * d->N);      // 6 bf16 per complex entry
+    w.Wx2 = cv.take<float>((size_t)3 * k * d->N);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(64);                          // 256 B: pbar and the granules that
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // follow it are zeroed by one memset
@@ -227,6 +233,7 @@ struct PDenoisePolicy {
 constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);
+bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);
 int device_cu_count();

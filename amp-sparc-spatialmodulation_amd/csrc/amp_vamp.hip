@@ -232,6 +232,15 @@ __global__ void vamp_output_kernel(VampK P) {
         P.var0[e] = P.var1[e];
 }
 
+// AMP_VAMP_GEMM=f32: AMP_GEMM_AUTO keeps the f32-MFMA persistent GEMMs (measurement / A-B runs)
+static bool gemm_f32_requested() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_VAMP_GEMM");
+        return e && e[0] == 'f';
+    }();
+    return v;
+}
+
 static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64) {
     int rc = check_dims(d, c);
     if (rc) return rc;
@@ -262,6 +271,12 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
+    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_X3, "amp_vamp: gemm %d", a->gemm);
+    const bool x3_fits = vamp_persist_x3_fits(d->N, a->k, d->L);
+    AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || x3_fits, "amp_vamp: the bf16x3 engine needs k == N, N %% 64 == 0 and "
+                "its LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
+    P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && x3_fits && !gemm_f32_requested())) ? 1 : 0;
+    P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     return AMP_OK;
 }
 
@@ -348,13 +363,20 @@ static bool ytil_in_kernel_requested() {
 static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st) {
     static std::atomic<unsigned> gen{0};
     P.gen = ++gen;
-    P.ytil_in_kernel = (ytil_in_kernel_requested() && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
+    P.ytil_in_kernel = (!P.x3 && ytil_in_kernel_requested() && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
     const bool yk = P.ytil_in_kernel != 0;
     CWeightJob j[3];
+    if (P.x3) {
+        //   q = Vh r~    (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N   (bf16x3 planes)
+        j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wx1, P.N, P.k, WPACKX3};
+        //   V (x~ - q)   (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
+        j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wx2, P.k, P.N, WPACKX3};
+    } else {
     //   q = Vh r~        (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
     j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.k, WPACK16};
     //   V (x~ - q)       (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
     j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wq2, 2 * P.k, 2 * P.N, WPACK16};
+    }
     //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     j[2] = yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
               : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};

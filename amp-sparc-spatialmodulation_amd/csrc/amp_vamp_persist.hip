@@ -7,7 +7,8 @@
 //   max / max|xi| of the last denoiser call, and the GEMM A operand (r~, then w).
 // Per iteration t:
 //   1. A <- r~ = (xmmse - dxdr r) * normScalar                         (vamp.py:89-91)
-//   2. q = Vh r~ on v_mfma_f32_16x16x4_f32; w = scale (y~ + vr q) - q    (vamp.py:67-72)
+//   2. q = Vh r~ on v_mfma_f32_16x16x4_f32 (or the split-precision bf16x3 engine, below);
+//      w = scale (y~ + vr q) - q                                         (vamp.py:67-72)
 //   3. x~ - r~ = V w; r = (x~ - alpha r~) / (1 - alpha)                  (vamp.py:72-79)
 //   4. section denoiser on r (amp_denoise.h)                           (vamp.py:84, 96-119)
 //   5. one grid barrier: every workgroup reduces the same per-workgroup partials in the same
@@ -17,6 +18,10 @@
 // The weights are streamed from L2 by each wave in 16x16x4-packed order (amp_gemm.h,
 // wpack16_index): a wave owns 16*NT output columns, NT independent accumulators.
 // y~ = (s Uh) y comes from the launch engine's GEMM once per forward (amp_vamp.hip).
+// X3 (default where the LDS fits): both GEMMs as 6-term bf16x3 products on
+// v_mfma_f32_16x16x32_bf16 (amp_persist.h gemm_x3), A in LDS as six bf16 planes, the operators
+// complex-planar (12 bytes per entry instead of the real expansion's 16); instantiated in
+// amp_vamp_persist_x3.hip.  The kernel template lives in amp_vamp_persist_kernel.h.
 //
 // Co-residency: ceil(B/16) <= #CUs workgroups, one per CU by its LDS footprint; the launch
 // checks occupancy x CUs >= grid first (or uses hipLaunchCooperativeKernel, which makes the
@@ -27,407 +32,13 @@
 #include <algorithm>
 #include <mutex>
 
-#include "amp_persist.h"
-#include "amp_vamp.h"
+#include "amp_vamp_persist_kernel.h"
 
 namespace amp {
-
-constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iteration)
-
-// LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the 16-row ds_read_b128 and the
-// accumulator stores conflict-free (row r and r+4 land 16 banks apart).
-struct PLayout {
-    int lda, ldr;
-    int offA, offR, offX, offV0, offV1, offSM, offSA, offScr, total;
-};
-
-__host__ __device__ inline PLayout playout(int N, int k, int L) {
-    PLayout y;
-    y.lda = (2 * N > 2 * k ? 2 * N : 2 * k) + 4;
-    y.ldr = 2 * N + 4;
-    int o = 0;
-    y.offA = o; o += PBM * y.lda;
-    y.offR = o; o += PBM * y.ldr;
-    y.offX = o; o += PBM * y.ldr;
-    y.offV0 = o; o += PBM * N;
-    y.offV1 = o; o += PBM * N;
-    y.offSM = o; o += PBM * L;
-    y.offSA = o; o += PBM * L;
-    o = (o + 3) & ~3;
-    y.offScr = o; o += 1024;
-    y.total = o;
-    return y;
-}
-
-// Fused MAP decision + error counters (Loss.error_rate, loss.py:67-179, via amp_decide.h) on
-// this workgroup's rows while r (the decision input, vamp.py:187) and xmmse are still in LDS;
-// per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
-// mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
-template <int PWG, int KK>
-__device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
-                                int nrows, float* sT, void* lab_lds, void* scr) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int M = P.M, L = P.L, N = P.N;
-    const int S = nrows * L;
-    // one coalesced bulk load of this workgroup's truth rows and labels into LDS (a per-section
-    // global load inside the decision loop left every round waiting on HBM latency)
-    long long* lsym = reinterpret_cast<long long*>(lab_lds);
-    long long* lidx = lsym + S;
-    unsigned char* mism = reinterpret_cast<unsigned char*>(lidx + S);
-    {
-        // PBM rows of 2N floats = PBM * N / 2 float4: all loads in flight before the LDS stores
-        constexpr int CH = 8;
-        const int tot = nrows * (N >> 1);
-        for (int e0 = 0; e0 < tot; e0 += PWG * CH) {
-            float4 v[CH];
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    v[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.xtrue) +
-                                                            (size_t)(row0 + row) * 2 * N + c4);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    *reinterpret_cast<float4*>(sT + row * ldr + c4) = v[u];
-                }
-            }
-        }
-    }
-    for (int e = tid; e < S; e += PWG) {
-        lsym[e] = P.sym[(size_t)row0 * L + e];
-        lidx[e] = P.idx[(size_t)row0 * L + e];
-    }
-    __syncthreads();
-    const long long ibmask = dec_ibmask(P.ibits);
-    DecPart q = decpart_zero();
-    // one section per group of DG = 4 lanes (two DPP steps per reduction), float32 prefilter
-    constexpr int DG = 4;
-    const int g = lane % DG;
-    for (int base = wave * (64 / DG); base < S; base += (PWG / 64) * (64 / DG)) {   // wave-uniform
-        const int ls = base + lane / DG;
-        const bool act = ls < S;
-        const int lsc = act ? ls : S - 1;
-        const int row = lsc / L, l = lsc - row * L;
-        const float* rp = sR + row * ldr + 2 * l * M;
-        const float* xp = sX + row * ldr + 2 * l * M;
-        const float* tp = sT + row * ldr + 2 * l * M;
-        auto ld = [&](int m, float2& xv, float2& xt, float2& xe) {
-            xv = *reinterpret_cast<const float2*>(rp + 2 * m);
-            xe = *reinterpret_cast<const float2*>(xp + 2 * m);
-            xt = *reinterpret_cast<const float2*>(tp + 2 * m);
-        };
-        int bi, mm;
-        double se;
-        decide_section<KK, DG, true>(dc, M, g, ld, bi, mm, se);
-        if (act && g == 0) {
-            const long long s = (long long)(row0 + row) * L + l;
-            mism[lsc] = (unsigned char)mm;
-            count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
-        }
-    }
-    __syncthreads();
-    // channel uses (Na sections each) and trials with any mismatch (loss.py:133-136, 150)
-    long long ver = 0, verf = 0, verm = 0, verL = 0, fer = 0;
-    for (int row = tid; row < nrows; row += PWG) {
-        int trial = 0;
-        for (int lin = 0; lin < P.Lin; ++lin) {
-            int cu = 0;
-            for (int a = 0; a < P.Na; ++a) cu |= mism[row * L + lin * P.Na + a];
-            ver += cu;
-            if (lin == 0) verf += cu;
-            if (lin == P.Lin / 2) verm += cu;
-            if (lin == P.Lin - 1) verL += cu;
-            trial |= cu;
-        }
-        fer += trial;
-    }
-    q.ier = group_sum(q.ier, 64); q.ser = group_sum(q.ser, 64); q.iber = group_sum(q.iber, 64);
-    q.sber = group_sum(q.sber, 64);
-    q.mse = group_sum(q.mse, 64); q.msef = group_sum(q.msef, 64); q.msem = group_sum(q.msem, 64);
-    q.mseL = group_sum(q.mseL, 64);
-    ver = group_sum(ver, 64); verf = group_sum(verf, 64); verm = group_sum(verm, 64); verL = group_sum(verL, 64);
-    fer = group_sum(fer, 64);
-    DecWG* sw = reinterpret_cast<DecWG*>(scr);
-    if (lane == 0) {
-        DecWG w;
-        w.p = q; w.ver = ver; w.verf = verf; w.verm = verm; w.verL = verL; w.fer = fer;
-        w.pad[0] = w.pad[1] = w.pad[2] = 0;
-        sw[wave] = w;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        DecWG o = sw[0];
-        for (int v = 1; v < PWG / 64; ++v) {
-            decpart_add(o.p, sw[v].p);
-            o.ver += sw[v].ver; o.verf += sw[v].verf; o.verm += sw[v].verm; o.verL += sw[v].verL; o.fer += sw[v].fer;
-        }
-        P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
-                                 // an agent-scope release writes back the L2 and cost ~90 us)
-    }
-}
 
 __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out) {
     __shared__ DecWG s[16];
     dec_fold_block(w, n, out, s);
-}
-
-// dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
-template <int NT, int KK, int NWV, int DU>
-__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc) {
-    constexpr int PWG = 64 * NWV;
-    const Const64& c64 = dc;
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ int s_flag;
-    __shared__ double s_d[PWG / 64][4];
-    const PLayout Y = playout(P.N, P.k, P.L);
-    float* sA = lds + Y.offA;
-    float* sR = lds + Y.offR;
-    float* sX = lds + Y.offX;
-    float* sM = lds + Y.offSM;
-    float* sS = lds + Y.offSA;
-    float* scr = lds + Y.offScr;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wg = blockIdx.x, nwg = gridDim.x;
-    const int row0 = wg * PBM, nrows = min(PBM, P.B - row0);
-    const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
-    const int ldr = Y.ldr, lda = Y.lda;
-    const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
-
-    // y~ rows and s^2 of this wave's GEMM1 columns, in the accumulator layout
-    float yt[NT][4], s2c[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int col = 16 * (ct0 + t) + (lane & 15);
-        const float sv = P.s[col >> 1];
-        s2c[t] = sv * sv;                                   // vamp.py:17
-    }
-    if (P.ytil_in_kernel) {
-        // y~ = (s Uh) y (vamp.py:22) for this workgroup's rows: y staged in LDS over the A/R/X
-        // region (row stride 2n + 4 = 4N + 4), GEMM on the packed s Uh operand (K = 2n = 4N)
-        const int ldy = 4 * N + 4;
-        for (int e = tid; e < PBM * N; e += PWG) {          // float4 units: 4N floats per row
-            const int row = e / N, c4 = 4 * (e - row * N);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 4 * N + c4);
-            *reinterpret_cast<float4*>(lds + row * ldy + c4) = v;
-        }
-        __syncthreads();
-        f32x4 acc[NT];
-        gemm16<NT, 2 * NT * NWV>(lds, ldy, P.Wq0, ct0, acc);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) yt[t][r] = acc[t][r];
-        __syncthreads();
-    } else {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int col = 16 * (ct0 + t) + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 4 * (lane >> 4) + r;
-                yt[t][r] = (row < nrows) ? P.ytil[(size_t)(row0 + row) * twok + col] : 0.f;
-            }
-        }
-    }
-    VampIter cur = vamp_first_iter(P, scr);   // vamp.py:26, 66-82 at t = 0
-    // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
-    {
-        const float p = (float)P.sparsity;
-        for (int e = tid; e < PBM * twoN; e += PWG) {
-            const int row = e / twoN, col = e - row * twoN;
-            sR[row * ldr + col] = 0.f;
-            sX[row * ldr + col] = (row < nrows && (col & 1) == 0) ? p : 0.f;
-        }
-        for (int e = tid; e < PBM * N; e += PWG) lds[Y.offV1 + e] = 1.0f;
-    }
-
-    unsigned long long* trc = P.trace;
-    auto stamp = [&](int t, int ph) {
-        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * AMP_TRACE_STRIDE + ph] = __builtin_amdgcn_s_memtime();
-    };
-    if (trc && tid == 0) {
-        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg] = __builtin_amdgcn_s_memtime();
-        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-    unsigned nbar = 0;
-    const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
-    int fixed = 0, last_t = 0, aborted = 0;
-    VampIter nx = cur;
-
-    for (int t = 0; t < P.max_iter; ++t) {
-        last_t = t;
-        stamp(t, 0);
-        const float* vprev = lds + ((t & 1) ? Y.offV0 : Y.offV1);
-        float* vnew = lds + ((t & 1) ? Y.offV1 : Y.offV0);
-        // 1. A <- r~ (vamp.py:91; t = 0: dxdr 0, normScalar 1)
-        for (int e = tid; e < PBM * (twoN >> 2); e += PWG) {
-            const int row = e / (twoN >> 2), c4 = 4 * (e - row * (twoN >> 2));
-            const float4 x = *reinterpret_cast<const float4*>(sX + row * ldr + c4);
-            const float4 q = *reinterpret_cast<const float4*>(sR + row * ldr + c4);
-            *reinterpret_cast<float4*>(sA + row * lda + c4) =
-                make_float4((x.x - cur.dxdr_prev * q.x) * cur.ns_prev, (x.y - cur.dxdr_prev * q.y) * cur.ns_prev,
-                            (x.z - cur.dxdr_prev * q.z) * cur.ns_prev, (x.w - cur.dxdr_prev * q.w) * cur.ns_prev);
-        }
-        __syncthreads();
-        stamp(t, 1);
-        // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
-        f32x4 acc[NT];
-        gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
-        __syncthreads();
-        stamp(t, 2);
-#pragma unroll
-        for (int t2 = 0; t2 < NT; ++t2) {
-            const int col = 16 * (ct0 + t2) + (lane & 15);
-            const float sc = 1.0f / (s2c[t2] + cur.vr);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float q = acc[t2][r];
-                sA[(4 * (lane >> 4) + r) * lda + col] = sc * (yt[t2][r] + cur.vr * q) - q;
-            }
-        }
-        __syncthreads();
-        stamp(t, 3);
-        // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
-        gemm16<NT, NT * NWV>(sA, lda, P.Wq2, ct0, acc);
-#pragma unroll
-        for (int t2 = 0; t2 < NT; ++t2) {
-            const int col = 16 * (ct0 + t2) + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int o = (4 * (lane >> 4) + r) * ldr + col;
-                const float rt = (sX[o] - cur.dxdr_prev * sR[o]) * cur.ns_prev;
-                const float xt = acc[t2][r] + rt;
-                sR[o] = (xt - cur.alpha * rt) * cur.inv1ma;
-            }
-        }
-        __syncthreads();
-        stamp(t, 4);
-        // 4. denoiser (vamp.py:84)
-        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
-        PartAcc pa;
-        if constexpr (KK > 16)
-            denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
-        else
-            denoise_sections_u<true, KK, DU>(pol, nrows * spr, M, P.c, pa);
-        stamp(t, 8);
-        const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
-        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
-        stamp(t, 5);
-        // 5. batch scalars: every workgroup gathers and reduces every partial
-        PartAcc g;
-        if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, tag, P.pbar + 1, g, scr, &s_flag)) {
-            aborted = 1;
-            break;
-        }
-        stamp(t, 6);
-        fixed = 0;
-        if (part_allnan(g)) {
-            // the reference's G is NaN / inf: every section of this iteration is NaN
-            if (!cur.fixed_all) {
-                const float qn = __int_as_float(0x7fc00000);
-                for (int e = tid; e < nrows * twoN; e += PWG) sX[(e / twoN) * ldr + e % twoN] = qn;
-                for (int e = tid; e < nrows * N; e += PWG) vnew[e] = qn;
-            }
-            g.sumvar = __longlong_as_double(0x7ff8000000000000LL);
-            g.notclose = 1;
-            fixed = -1;
-        } else if (part_danger(g)) {
-            // (a) exact float64 G over the candidate sections of every workgroup
-            const double G32 = g.maxabs, slack = logit_slack(G32);
-            const float inv = cur.inv_sigma2;
-            auto ldf = [=](int s) {
-                const int row = s / spr, sj = s - row * spr;
-                const float* rp = sR + row * ldr + 2 * sj * M;
-                return [=](int m, float& rr, float& ri, float& it) {
-                    rr = rp[2 * m]; ri = rp[2 * m + 1]; it = inv;
-                };
-            };
-            double gm = 0.0;
-            for (int s = tid; s < nrows * spr; s += PWG)
-                if ((double)sS[s] >= G32 - slack) gm = fmax(gm, section_absmax_f64(ldf(s), M, c64));
-            gm = group_max(gm, 64);
-            if (lane == 0) s_d[wave][0] = gm;
-            __syncthreads();
-            if (tid == 0) {
-                double m4 = 0.0;
-                for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
-                P.pxch[((size_t)t * nwg + wg) * 4 + 0] = m4;
-            }
-            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
-            double G = 0.0;
-            for (int w = 0; w < nwg; ++w) G = fmax(G, P.pxch[((size_t)t * nwg + w) * 4 + 0]);
-            // (b) exact recompute of this workgroup's sections below the danger line
-            double dsum = 0.0;
-            int dnc = 0, cnt = 0;
-            for (int s = tid; s < nrows * spr; s += PWG) {
-                if (!((double)sM[s] - G < AMP_DANGER + slack)) continue;
-                ++cnt;
-                const int row = s / spr, sj = s - row * spr;
-                float* xp = sX + row * ldr + 2 * sj * M;
-                const int v0 = row * N + sj * M;
-                auto st = [&](int m, float xr, float xi, float var) {
-                    const float old = vnew[v0 + m];
-                    dsum += (double)var - (double)old;
-                    dnc += (torch_close(var, vprev[v0 + m]) ? 0 : 1) - (torch_close(old, vprev[v0 + m]) ? 0 : 1);
-                    xp[2 * m] = xr; xp[2 * m + 1] = xi;
-                    vnew[v0 + m] = var;
-                };
-                exact_section_f64<true>(ldf(s), st, M, c64, G);
-            }
-            dsum = group_sum(dsum, 64);
-            dnc = group_sum(dnc, 64);
-            cnt = group_sum(cnt, 64);
-            __syncthreads();
-            if (lane == 0) { s_d[wave][1] = dsum; s_d[wave][2] = (double)dnc; s_d[wave][3] = (double)cnt; }
-            __syncthreads();
-            if (tid == 0) {
-                double a = 0.0, b = 0.0, c = 0.0;
-                for (int w = 0; w < PWG / 64; ++w) { a += s_d[w][1]; b += s_d[w][2]; c += s_d[w][3]; }
-                P.pxch[((size_t)t * nwg + wg) * 4 + 1] = a;
-                P.pxch[((size_t)t * nwg + wg) * 4 + 2] = b;
-                P.pxch[((size_t)t * nwg + wg) * 4 + 3] = c;
-            }
-            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
-            double a = 0.0, b = 0.0, c = 0.0;
-            for (int w = 0; w < nwg; ++w) {
-                const double* q = P.pxch + ((size_t)t * nwg + w) * 4;
-                a += q[1]; b += q[2]; c += q[3];
-            }
-            g.sumvar += a;   // (sum - old) + new, in float64
-            g.notclose = (uint32_t)((long long)g.notclose + (long long)b);
-            g.maxabs = G;
-            fixed = (int)c;
-        }
-        nx = vamp_advance(P, cur, g, fixed, t, scr);
-        stamp(t, 7);
-        if (nx.stopped || t + 1 == P.max_iter) break;
-        cur = nx;
-    }
-    __syncthreads();
-    // outputs: r (decision input, vamp.py:187), xmmse, var of the last executed iteration
-    const float* vlast = lds + ((last_t & 1) ? Y.offV1 : Y.offV0);
-    for (int e = tid; e < nrows * twoN; e += PWG) {
-        const int row = e / twoN, col = e - row * twoN;
-        P.r[(size_t)(row0 + row) * twoN + col] = sR[row * ldr + col];
-        P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldr + col];
-    }
-    for (int e = tid; e < nrows * N; e += PWG) P.var0[(size_t)row0 * N + e] = vlast[e];
-    if (wg == 0 && tid == 0) {
-        amp_status s = vamp_make_status(P, cur, nx, fixed);
-        if (aborted) s.nan_state = -1;
-        *P.status = s;
-    }
-    if (P.dec_on) {
-        __syncthreads();   // the V0/V1 region (vlast) becomes the label / mismatch scratch
-        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldr, row0, nrows, sA, lds + Y.offV0, scr);
-    }
 }
 
 static std::once_flag g_pers_once;
@@ -448,108 +59,18 @@ bool vamp_persist_ytil_in_kernel(const VampK& P) {
     return P.n == 2 * P.N && PBM * (2 * P.n + 4) <= playout(P.N, P.k, P.L).offV0;
 }
 
+bool vamp_persist_x3_fits(int N, int k, int L) {
+    return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
+}
+
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
     if (cdiv(d->B, PBM) > ncu) return false;
     return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
 }
 
-// Waves per workgroup (one workgroup per CU): 4 = one wave per SIMD, 8 = two (the second
-// wave hides LDS / cross-lane latency in the denoiser and keeps more weight loads in flight).
-static int persist_waves() {
-    static int w = [] {
-        const char* e = getenv("AMP_PERSIST_WAVES");
-        const int v = e ? atoi(e) : 4;
-        return (v == 8) ? 8 : 4;
-    }();
-    return w;
-}
-
-static int den_u() {
-    static int u = [] {
-        const char* e = getenv("AMP_DEN_U");
-        return e ? atoi(e) : 2;
-    }();
-    return u;
-}
-
-// Launch path: a plain launch after an explicit co-residency check (default), or
-// hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).  The cooperative path made processes
-// crash in exit-time teardown under rocprofv3 on the box (r01), the plain one does not.
-static bool persist_coop() {
-    static bool c = [] {
-        const char* e = getenv("AMP_PERSIST_LAUNCH");
-        return e && e[0] == 'c';
-    }();
-    return c;
-}
-
-template <int NT, int KK, int NWV, int DU>
-static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU>;
-    const size_t lds = (size_t)playout(P.N, P.k, P.L).total * 4;
-    // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
-    // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
-    static size_t attr_lds = 0;
-    static int per_cu = 0;
-    hipError_t e = hipSuccess;
-    if (attr_lds != lds) {
-        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) {
-            set_error("vamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
-            return AMP_E_LAUNCH;
-        }
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * NWV, lds);
-        if (e != hipSuccess) per_cu = 0;
-        attr_lds = lds;
-    }
-    if (persist_coop()) {
-        VampK Pc = P;
-        DecConst dd = dc;
-        void* args[] = {(void*)&Pc, (void*)&dd};
-        e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
-        if (e != hipSuccess) {
-            set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
-                      hipGetErrorString(e));
-            return AMP_E_LAUNCH;
-        }
-        return AMP_OK;
-    }
-    // plain launch: co-residency checked here (resident workgroups per CU x CUs >= grid), the
-    // check hipLaunchCooperativeKernel would make; the bounded barrier spins stay as the backstop
-    if (per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
-        set_error("vamp_persist: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", P.nwg, per_cu,
-                  device_cu_count());
-        return AMP_E_LAUNCH;
-    }
-    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV, DU>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, dc);
-    e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
-        return AMP_E_LAUNCH;
-    }
-    return AMP_OK;
-}
-
-template <int NT, int NWV>
-static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
-    switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV, 4>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV, 4>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV, 4>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV, 2>(P, dc, st);
-    case 16:
-        // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8)
-        switch (den_u()) {
-        case 4: return persist_launch_t<NT, 16, NWV, 4>(P, dc, st);
-        case 8: return persist_launch_t<NT, 16, NWV, 8>(P, dc, st);
-        default: return persist_launch_t<NT, 16, NWV, 2>(P, dc, st);
-        }
-    default: return persist_launch_t<NT, 64, NWV, 1>(P, dc, st);
-    }
-}
-
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
+int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_x3.hip
 
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
@@ -567,18 +88,19 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) {
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
+    if (P.x3) return persist_dispatch_x3(P, dc, st);
     if (persist_waves() == 4) {
         switch (P.N) {
-        case 64: return persist_launch_nt<2, 4>(P, dc, st);
-        case 128: return persist_launch_nt<4, 4>(P, dc, st);
-        case 256: return persist_launch_nt<8, 4>(P, dc, st);
+        case 64: return persist_launch_nt<2, 4, false>(P, dc, st);
+        case 128: return persist_launch_nt<4, 4, false>(P, dc, st);
+        case 256: return persist_launch_nt<8, 4, false>(P, dc, st);
         default: break;
         }
     } else {
         switch (P.N) {
-        case 64: return persist_launch_nt<1, 8>(P, dc, st);
-        case 128: return persist_launch_nt<2, 8>(P, dc, st);
-        case 256: return persist_launch_nt<4, 8>(P, dc, st);
+        case 64: return persist_launch_nt<1, 8, false>(P, dc, st);
+        case 128: return persist_launch_nt<2, 8, false>(P, dc, st);
+        case 256: return persist_launch_nt<4, 8, false>(P, dc, st);
         default: break;
         }
     }

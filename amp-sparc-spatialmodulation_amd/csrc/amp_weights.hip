@@ -5,6 +5,7 @@
 
 #include "amp_gemm.h"
 #include "amp_host.h"
+#include "amp_persist.h"
 
 namespace amp {
 
@@ -116,6 +117,31 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
     const CWeightJob J = P.j[blockIdx.y];
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = threadIdx.x; i < P.nzero; i += blockDim.x) P.zero[i] = 0u;
+    if (J.packed == WPACKX3) {
+        // bf16x3 planes of X itself (no real expansion): kap = J, ncp = O (complex counts)
+        unsigned short* w3 = reinterpret_cast<unsigned short*>(J.wt);
+        const long tot = (long)J.ncp * J.kap;
+        for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+            const int o = (int)(e / J.kap), j = (int)(e % J.kap);
+            float xr = 0.f, xi = 0.f;
+            if (o < J.O && j < J.J) {
+                const float2 v = J.src[o * J.so + j * J.sj];
+                xr = v.x;
+                xi = J.conj ? -v.y : v.y;
+                if (J.rowscale) {
+                    const float s = J.rowscale[o];
+                    xr = s * xr;
+                    xi = s * xi;
+                }
+            }
+            unsigned p[6];
+            split3(xr, p[0], p[1], p[2]);
+            split3(xi, p[3], p[4], p[5]);
+#pragma unroll
+            for (int f = 0; f < 6; ++f) w3[x3_index(o, j, f, J.kap)] = (unsigned short)p[f];
+        }
+        return;
+    }
     const long total = (long)(J.ncp / 2) * (J.kap / 2);
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / (J.kap / 2)), j = (int)(e % (J.kap / 2));
@@ -143,12 +169,13 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     long most = 0;
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
-        AMP_REQUIRE(2 * J.J <= J.kap && 2 * J.O <= J.ncp &&
+        AMP_REQUIRE((J.packed == WPACKX3 ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
-                         (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0)),
+                         (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||
+                         (J.packed == WPACKX3 && J.kap % 32 == 0 && J.ncp % 16 == 0)),
                     "build_cweights: job %d kap %d / ncp %d not tiled for layout %d", i, J.kap, J.ncp, J.packed);
         P.j[i] = J;
-        most = std::max(most, (long)(J.ncp / 2) * (J.kap / 2));
+        most = std::max(most, J.packed == WPACKX3 ? (long)J.ncp * J.kap : (long)(J.ncp / 2) * (J.kap / 2));
     }
     P.zero = zero;
     P.nzero = zero ? nzero : 0;

@@ -204,12 +204,15 @@ class LazyResult:
 
 class VAMP(LazyResult, nn.Module):
     """``engine``: nat.ENGINE_AUTO (persistent single-launch engine when the shape allows it,
-    else three launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h)."""
+    else three launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h).
+    ``gemm``: the persistent engine's GEMM arithmetic, nat.GEMM_AUTO (split-precision bf16x3
+    where it fits, else f32 MFMA), GEMM_F32 or GEMM_X3 (amp_sparc.h)."""
 
-    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO) -> None:
+    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO, gemm: int = nat.GEMM_AUTO) -> None:
         super().__init__()
         self.config = config
         self.engine = engine
+        self.gemm = gemm
         self.E = config.Na / config.Nr                                   # vamp.py:154
         self.sparsity = config.Na / config.Nt                            # vamp.py:155
         self.layers = nn.ModuleList([VAMPLayer(config, i) for i in range(config.N_Layers)])
@@ -222,6 +225,7 @@ class VAMP(LazyResult, nn.Module):
         with torch.cuda.device(y.device):
             T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
             T.args.engine = self.engine
+            T.args.gemm = self.gemm
             nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
                       'amp_vamp_run')
         return T
@@ -241,6 +245,7 @@ class VAMP(LazyResult, nn.Module):
     def _forward(self, U, s, Vh, y, SNR, x, symbols, indices) -> Loss:
         T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._bufs)
         T.args.engine = self.engine
+        T.args.gemm = self.gemm
         res, host = self._result_slot(T.y.device)
         T.res = res
         T.args.status = nat.dptr(res)

@@ -89,7 +89,7 @@ typedef struct amp_vamp_args {
     int32_t k;          /* min(n, N) */
     int32_t max_iter;   /* config.N_Layers */
     int32_t engine;     /* amp_vamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT */
-    int32_t pad;
+    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 */
     double noise_var;   /* Na/Nr/SNR (vamp.py:179) */
     double sparsity;    /* Na/Nt (vamp.py:155) */
     void* r;            /* out c64 [B][N]: decision input T.r (vamp.py:187) */
@@ -107,6 +107,16 @@ typedef struct amp_vamp_args {
  *             batch-global scalars (needs k == N, N % 32 == 0, N <= 256, M <= 64 and
  *             ceil(B/16) workgroups co-resident: B <= 16 x #CUs);
  *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
+/* Persistent-engine GEMM arithmetic (amp_vamp_args.gemm):
+ *  F32   v_mfma_f32_16x16x4_f32 on the real expansion of each operator;
+ *  X3    split precision: every f32 operand as three bf16 pieces, six bf16 MFMA products per
+ *        product (terms below 2^-24 relative dropped), f32 accumulation — the f32 GEMM's
+ *        accuracy at 2.7x the MFMA rate (needs k == N, N % 64 == 0 and 160 KB of LDS);
+ *  AUTO  X3 where it fits, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32). */
+#define AMP_GEMM_AUTO 0
+#define AMP_GEMM_F32 1
+#define AMP_GEMM_X3 2
+
 #define AMP_ENGINE_AUTO 0
 #define AMP_ENGINE_LAUNCHES 1
 #define AMP_ENGINE_PERSISTENT 2

@@ -263,6 +263,70 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
     return dict(r=r, xmmse=xm, var=var, T=t + 1)
 
 
+# vamp2.py:48-49 — torch.tensor(...) float32 0-dim clamps of the damped VAMP
+V2_VAR_MIN = F32(1.0e-11)
+V2_VAR_MAX = F32(1.0e11)
+
+
+def vamp2_denoise(r: np.ndarray, tau, cfg: OracleConfig):
+    """vamp2 ``VAMPLayer.segmented_denoiser`` (vamp2.py:79-88): the same float64 logits and
+    batch-global shift as vamp.py, variance as E|a|^2 - |xmmse|^2 (vamp2.py:85-87)."""
+    B = r.shape[0]
+    sym = cfg.symbols
+    xi = _logits(r, tau, cfg, B)
+    with np.errstate(under='ignore', invalid='ignore', divide='ignore', over='ignore'):
+        eta = np.exp(xi - np.abs(xi).max())                                    # vamp2.py:83
+        z = eta.sum(axis=-1).sum(axis=2, keepdims=True)
+        xm = (sym * eta).sum(axis=-1) / z                                      # vamp2.py:86
+        var = (np.abs(sym) ** 2 * eta).sum(axis=-1) / z - np.abs(xm) ** 2       # vamp2.py:85, 87
+    return xm.astype(C64).reshape(B, -1), var.astype(F32).reshape(B, -1)
+
+
+def vamp2_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, damping: float = 1.0,
+                 trace: list | None = None):
+    """Damped "Rangan" VAMP: Tracker (vamp2.py:12-26), VAMPLayer.forward (vamp2.py:52-77),
+    VAMP.forward loop + early exit on var (vamp2.py:123-131).
+
+    U [n,k] c64, s [k] f32, Vh [k,N] c64, y [B,n] c64.  Returns dict(r, xmmse, var, T).
+    """
+    U = np.asarray(U, C64); Vh = np.asarray(Vh, C64); y = np.asarray(y, C64)
+    s = np.asarray(s, F32)
+    B, N = y.shape[0], Vh.shape[1]
+    sigma2 = cfg.Na / cfg.Nr / SNR                                # vamp2.py:98, 123 (Python float)
+    Uh = np.conj(U).T
+    s2 = (s * s).astype(F32)                                      # vamp2.py:17
+    ytil = _div_real((y @ Uh.T).astype(C64), s[None, :])          # vamp2.py:22
+    eta = Vh.shape[1] / s.shape[0]                                # vamp2.py:26
+    Vt_eta = (F32(eta) * np.conj(Vh)).astype(C64)                 # (eta * V)^T, V = Vh^H: vamp2.py:77
+    rho = F32(damping)
+    gamma = F32(1.0)                                              # vamp2.py:21
+    r = np.zeros((B, N), C64)
+    var = np.ones((B, N), F32)
+    xm_state = np.zeros((B, N), C64)
+    t = 0
+    with np.errstate(invalid='ignore', over='ignore', divide='ignore'):
+        for t in range(cfg.N_Layers):
+            prev = var
+            xm, var = vamp2_denoise(r, gamma, cfg)                                # vamp2.py:62
+            xm_state = (rho * xm + F32(1 - damping) * xm_state).astype(C64)       # vamp2.py:63
+            alpha = F32(F32(np.sum(var, dtype=np.float64) / var.size) * gamma)    # vamp2.py:64
+            rt = _div_real(xm_state - alpha * r, F32(1) - alpha)                  # vamp2.py:66
+            gt = F32(F32(gamma * F32(F32(1) - alpha)) / alpha)                    # vamp2.py:67
+            gt = _clamp(gt, V2_VAR_MIN, V2_VAR_MAX)                               # vamp2.py:68-69
+            d = (s2 / (s2 + F32(F32(sigma2) * gt))).astype(F32)                   # vamp2.py:71
+            dm = F32(np.sum(d, dtype=np.float64) / d.size)
+            g = F32(F32(gt * dm) / F32(F32(eta) - dm))                            # vamp2.py:72
+            gamma = F32(rho * g + F32(1 - damping) * gamma)                       # vamp2.py:73
+            z = ((d / dm).astype(F32) * (ytil - (rt @ Vh.T).astype(C64))).astype(C64)
+            r = (rt + (z @ Vt_eta).astype(C64)).astype(C64)                       # vamp2.py:77
+            if trace is not None:
+                trace.append(dict(r=r.copy(), xmmse=xm_state.copy(), var=var.copy(), gamma=gamma,
+                                  alpha=alpha, r_tilde=rt.copy()))
+            if allclose_f32(var, prev):                                           # vamp2.py:129
+                break
+    return dict(r=r, xmmse=xm_state, var=var, T=t + 1)
+
+
 def bamp_random_denoise(r, cov, cfg: OracleConfig):
     """BAMPLayer.random_denoiser (bamp.py:79-88): element-wise Bayes posterior under the P0/Ps
     prior.  G(0) in float32 (r - 0 stays complex64); G(a_k) in float64 (complex64 - complex128:

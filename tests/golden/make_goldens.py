@@ -32,6 +32,7 @@ Groups:
   g10 the reference's own Model.simulate drivers (vamp/bamp/scamp_model.py) end to end: every
       {EbN0}.json they write, seeded once before the Model is built
   g11 ISI / spatial coupling (Lin > 1, Lh > 1, tail) Loss dicts for VAMP, BAMP and SCAMP
+  g12 vamp2.py damped VAMP: per-iteration traces and Loss dicts (sparc mode)
 
 Usage: python tests/golden/make_goldens.py [g1 g2 g3 g4 ...]
 """
@@ -729,6 +730,56 @@ def g11():
 
 
 # ---------------------------------------------------------------------------
+G12_CASES = [
+    # (alphabet, EbN0, seed, damping, Nt, Na, Nr, B): vamp2's VAMP takes damping = 1.0 by default
+    # (vamp2.py:96); 0.97 is VAMPLayer's own default (vamp2.py:29)
+    ('QPSK', 0.0, 0, 1.0, 16, 2, 32, 8), ('QPSK', 6.0, 0, 1.0, 16, 2, 32, 8), ('QPSK', 20.0, 1, 1.0, 16, 2, 32, 8),
+    ('16QAM', 6.0, 0, 1.0, 16, 2, 32, 8), ('16QAM', 20.0, 1, 1.0, 16, 2, 32, 8),
+    ('QPSK', 6.0, 0, 0.97, 16, 2, 32, 8), ('16QAM', 12.0, 2, 0.97, 16, 2, 32, 8),
+    ('QPSK', 8.0, 0, 1.0, 64, 4, 128, 64), ('16QAM', 8.0, 0, 1.0, 64, 4, 128, 64),
+]
+
+
+def g12():
+    """vamp2.py (damped "Rangan" VAMP, vamp2.py:12-131): per-iteration traces (r, xmmse, var,
+    gamma after every layer) and the Loss dict, inputs stored.  Sparc mode only: the reference
+    crashes in 'random' / 'segmented' mode."""
+    import vamp2 as ref_vamp2
+    out = {}
+    for alph, EbN0, seed, damp, Nt, Na, Nr, B in G12_CASES:
+        cfg = cfg_of(Nt, Na, Nr, B, alph)
+        inp = gen_inputs(cfg, seed, EbN0)
+        trace = []
+        orig = ref_vamp2.VAMPLayer.forward
+
+        def hook(self, T, _o=orig):
+            _o(self, T)
+            trace.append(dict(r=c(T.r), xmmse=c(T.xmmse), var=c(T.var), gamma=float(T.gamma)))
+        ref_vamp2.VAMPLayer.forward = hook
+        try:
+            L = ref_vamp2.VAMP(cfg, damping=damp)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'],
+                                                  inp['sym'], inp['idx'])
+        finally:
+            ref_vamp2.VAMPLayer.forward = orig
+        key = f'vamp2_{alph}_{Nt}_{EbN0:g}_{seed}_{damp:g}'
+        rec = dict(Nt=Nt, Na=Na, Nr=Nr, B=B, iters=cfg.N_Layers, SNR=inp['SNR'], damping=damp,
+                   U=c(inp['U']), s=c(inp['s']), Vh=c(inp['Vh']), y=c(inp['y']), x=c(inp['x']), sym=inp['sym'],
+                   idx=inp['idx'], T=len(trace), loss=json.dumps(loss_to_json(L.loss)))
+        keep = range(len(trace)) if Nt <= 16 else [0, len(trace) - 1]
+        for t in keep:
+            for k, v in trace[t].items():
+                rec[f'it{t}_{k}'] = v
+        out[key] = rec
+        print(key, 'T=', len(trace), 'ver', float(L.loss['ver']), 'gamma', [round(t['gamma'], 4) for t in trace][:6],
+              flush=True)
+    flat = {}
+    for key, rec in out.items():
+        for k, v in rec.items():
+            flat[f'{key}/{k}'] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, 'g12_vamp2.npz'), **flat)
+
+
+# ---------------------------------------------------------------------------
 G4_CONFIGS = {
     # name: (algo, Nt, Na, Nr, B, alphabet, iterations, EbN0 grid, seeds)
     # (round 2: seeds {0, 1, 2} over EbN0 0-20 step 1 for cfg2-cfg4, SURVEY.md §8(d))
@@ -829,3 +880,5 @@ if __name__ == '__main__':
             g4p(names or None)
         elif w == 'g11':
             g11()
+        elif w == 'g12':
+            g12()

@@ -214,20 +214,24 @@ VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk'
 
 
 ENGINES = {'launches': 1, 'persistent': 2}   # amp_native.ENGINE_*
+# (engine, persistent GEMM arithmetic): 'persistent' = the product default (bf16x3 where it fits)
+VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1)}
 
 
-@pytest.mark.parametrize('engine', sorted(ENGINES))
+@pytest.mark.parametrize('variant', sorted(VARIANTS))
 @pytest.mark.parametrize('name,key', VAMP_POINTS)
-def test_vamp_curve_point(device, name, key, engine):
+def test_vamp_curve_point(device, name, key, variant):
     """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar),
-    for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible)."""
+    for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible) and both
+    GEMM arithmetics of the persistent engine (split bf16x3, the default, and f32 MFMA)."""
     from vamp import VAMP
     ent = CURVES[name]
     ref = ent['points'][key]
     seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
     cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
     inp = _regen_inputs(cfg, seed, EbN0)
-    det = VAMP(cfg, engine=ENGINES[engine])
+    eng, gemm = VARIANTS[variant]
+    det = VAMP(cfg, engine=eng, gemm=gemm)
     L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
@@ -261,6 +265,33 @@ def test_vamp_engines_agree(device, ebn0):
         rs.append(T.r.clone())
     scale = float(rs[0].abs().max())
     assert torch.allclose(rs[0], rs[1], rtol=0, atol=2e-6 * scale), float((rs[0] - rs[1]).abs().max())
+
+
+@pytest.mark.parametrize('name', ['cfg4_vamp_16qam', 'cfg2_vamp_qpsk'])
+@pytest.mark.parametrize('iters', [1, 3])
+def test_vamp_x3_gemm_matches_f32(device, name, iters):
+    """The split-precision bf16x3 persistent GEMMs against the f32-MFMA ones, both measured
+    against the numpy oracle (f32 BLAS GEMMs in yet another summation order): after 1 and 3
+    iterations r of the x3 engine is as close to the oracle as the f32 engine's (tolerance: 4x
+    the f32 engine's own deviation, floored at 2e-6 of max|r|)."""
+    from vamp import VAMP
+    import amp_native as nat
+    ent = CURVES[name]
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=iters)
+    inp = _regen_inputs(cfg, 0, 8.0)
+    assert nat.lib().amp_vamp_select_engine(cfg.dims(), ent['Nt'], nat.ENGINE_AUTO) == nat.ENGINE_PERSISTENT
+    r = {}
+    for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+        T = VAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm).detect(inp['U'], inp['s'], inp['Vh'], inp['y'],
+                                                                     inp['SNR'])
+        r[gemm] = T.r.clone().cpu().numpy()[..., 0]
+    ocfg = OracleConfig(ent['Nt'], ent['Na'], ent['Nr'], B=ent['B'], alphabet=ent['alphabet'], iterations=iters)
+    c = lambda t: t.cpu().numpy()[..., 0] if t.dim() == 3 else t.cpu().numpy()   # noqa: E731
+    o = vamp_detect(c(inp['U']), c(inp['s']), c(inp['Vh']), c(inp['y']), float(inp['SNR']), ocfg)['r']
+    scale = float(np.abs(o).max())
+    e32 = float(np.abs(r[nat.GEMM_F32] - o).max())
+    ex3 = float(np.abs(r[nat.GEMM_X3] - o).max())
+    assert ex3 <= max(4 * e32, 2e-6 * scale), (ex3, e32, scale)
 
 
 def _check_T(got, ref, max_iter, ver_ref=0.0, ref_pert=None):
