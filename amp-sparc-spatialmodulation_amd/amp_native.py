@@ -52,6 +52,13 @@ class AmpVampArgs(C.Structure):
                 ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
 
+class AmpVamp2Args(C.Structure):
+    _fields_ = [('U', C.c_void_p), ('s', C.c_void_p), ('Vh', C.c_void_p), ('y', C.c_void_p),
+                ('k', C.c_int32), ('max_iter', C.c_int32), ('sigma2', C.c_double), ('damping', C.c_double),
+                ('r', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p), ('status', C.c_void_p),
+                ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
+
+
 class AmpVampDecideArgs(C.Structure):
     _fields_ = [('x', C.c_void_p), ('sym', C.c_void_p), ('idx', C.c_void_p), ('ibits_trunc', C.c_int32),
                 ('pad', C.c_int32), ('counts', C.c_void_p)]
@@ -79,6 +86,9 @@ _K = C.POINTER(AmpConstellation)
 SIGNATURES = {
     'amp_vamp_workspace_bytes': (C.c_size_t, [_D, _I, _I]),
     'amp_vamp_select_engine': (C.c_int, [_D, _I, _I]),
+    'amp_vamp_select_gemm': (C.c_int, [_D, _I, _I]),
+    'amp_vamp2_workspace_bytes': (C.c_size_t, [_D, _I]),
+    'amp_vamp2_run': (C.c_int, [_D, _K, C.POINTER(AmpVamp2Args), _P]),
     'amp_vamp_persist_trace': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P, _P]),
     'amp_vamp_run': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),

@@ -14,8 +14,9 @@
 namespace amp {
 
 struct DnK {
-    int N, L, M, S, mode;
+    int N, L, M, S, mode;   // mode 3 (internal): tau = tau[0], a device scalar (vamp2's gamma)
     float tau_scalar_inv;
+    const int* skip;        // non-null and set: every launch is a no-op (a stopped loop)
     const float2* r;
     const float* tau;
     float2* xm;
@@ -37,7 +38,7 @@ struct DnPolicy {
         const size_t o = (size_t)(sec0 + sec) * P->M + m;
         const float2 v = P->r[o];
         rr = v.x; ri = v.y;
-        it = (P->mode == 0) ? P->tau_scalar_inv : 1.0f / (P->tau[o] * 0.5f);
+        it = (P->mode == 0) ? P->tau_scalar_inv : (P->mode == 3) ? 1.0f / P->tau[0] : 1.0f / (P->tau[o] * 0.5f);
     }
     __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
         const size_t o = (size_t)(sec0 + sec) * P->M + m;
@@ -53,6 +54,7 @@ struct DnPolicy {
 
 template <int KK>
 __global__ __launch_bounds__(AMP_WG) void denoise_kernel(DnK P) {
+    if (P.skip && *P.skip) return;
     __shared__ __attribute__((aligned(16))) float lds[64];
     const int G = P.M < 64 ? P.M : 64;
     const int per = (AMP_WG / 64) * (64 / G);       // sections per workgroup pass
@@ -74,11 +76,12 @@ struct DnLoad {
     __device__ __forceinline__ void operator()(int m, float& rr, float& ri, float& it) const {
         const float2 v = P->r[o0 + m];
         rr = v.x; ri = v.y;
-        it = (P->mode == 0) ? P->tau_scalar_inv : 1.0f / (P->tau[o0 + m] * 0.5f);
+        it = (P->mode == 0) ? P->tau_scalar_inv : (P->mode == 3) ? 1.0f / P->tau[0] : 1.0f / (P->tau[o0 + m] * 0.5f);
     }
 };
 
 __global__ __launch_bounds__(DRWG) void denoise_reduce_kernel(DnK P, Const64 c64) {
+    if (P.skip && *P.skip) return;
     __shared__ __attribute__((aligned(16))) float lds[512];
     __shared__ double s_d[DRWG / 64];
     const PartAcc pa = part_reduce_all(P.parts, P.nblk, lds);
@@ -107,6 +110,7 @@ __global__ __launch_bounds__(DRWG) void denoise_reduce_kernel(DnK P, Const64 c64
 }
 
 __global__ void denoise_fix_kernel(DnK P, Const64 c64) {
+    if (P.skip && *P.skip) return;
     const double G = P.G[0], act = P.G[1], slack = P.G[2];
     if (act == 0.0) return;
     if (act == 2.0) {
@@ -138,37 +142,14 @@ static int dn_nblk(const amp_dims* d) {
     return std::max(1, std::min(cdiv(d->B * d->L, per), 2048));
 }
 
-}  // namespace amp
-
-using namespace amp;
-
-extern "C" {
-
-size_t amp_block_denoise_workspace_bytes(const amp_dims* d) {
-    if (!d) return 0;
-    Carve cv(nullptr);
-    cv.take<float>((size_t)d->B * d->L);
-    cv.take<float>((size_t)d->B * d->L);
-    cv.take<Partial>((size_t)dn_nblk(d));
-    cv.take<double>(4);
-    return cv.off;
-}
-
-int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void* r, int32_t tau_mode,
-                      float tau_scalar, const void* tau_vec, void* xmmse, void* var, void* ws, size_t ws_bytes,
-                      void* stream) {
-    int rc = check_dims(d, c, false);
-    if (rc) return rc;
-    AMP_REQUIRE(r && xmmse && ws, "amp_block_denoise: null pointer argument");
-    AMP_REQUIRE(tau_mode >= 0 && tau_mode <= 2, "amp_block_denoise: tau_mode %d", tau_mode);
-    AMP_REQUIRE(tau_mode == 0 || tau_vec, "amp_block_denoise: tau_vec required for tau_mode %d", tau_mode);
-    AMP_REQUIRE(tau_mode == 2 || var, "amp_block_denoise: var output required");
-    AMP_REQUIRE(ws_bytes >= amp_block_denoise_workspace_bytes(d), "amp_block_denoise: workspace too small");
+static int denoise_launch(const amp_dims* d, const amp_constellation* c, const float2* r, int mode, float tau_inv,
+                          const float* tau, float2* xmmse, float* var, void* ws, const int* skip, hipStream_t st) {
     DnK P;
-    P.N = d->N; P.L = d->L; P.M = d->M; P.S = d->B * d->L; P.mode = tau_mode;
-    P.tau_scalar_inv = 1.0f / tau_scalar;
-    P.r = (const float2*)r; P.tau = (const float*)tau_vec; P.xm = (float2*)xmmse;
-    P.var = (tau_mode == 2) ? nullptr : (float*)var;
+    P.N = d->N; P.L = d->L; P.M = d->M; P.S = d->B * d->L; P.mode = mode;
+    P.tau_scalar_inv = tau_inv;
+    P.skip = skip;
+    P.r = r; P.tau = tau; P.xm = xmmse;
+    P.var = var;
     Carve cv(ws);
     P.secmax = cv.take<float>((size_t)P.S);
     P.secabs = cv.take<float>((size_t)P.S);
@@ -177,7 +158,6 @@ int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void*
     P.G = cv.take<double>(4);
     P.c = to_const(c);
     const Const64 c64 = to_const64(c);
-    hipStream_t st = (hipStream_t)stream;
     switch (P.c.K) {
     case 1: hipLaunchKernelGGL(denoise_kernel<1>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
     case 2: hipLaunchKernelGGL(denoise_kernel<2>, dim3(P.nblk), dim3(AMP_WG), 0, st, P); break;
@@ -193,6 +173,43 @@ int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void*
     hipLaunchKernelGGL(denoise_fix_kernel, dim3(g), dim3(256), 0, st, P, c64);
     AMP_LAUNCH_CHECK("denoise_fix");
     return AMP_OK;
+}
+
+size_t block_denoise_ws_bytes(const amp_dims* d) {
+    Carve cv(nullptr);
+    cv.take<float>((size_t)d->B * d->L);
+    cv.take<float>((size_t)d->B * d->L);
+    cv.take<Partial>((size_t)dn_nblk(d));
+    cv.take<double>(4);
+    return cv.off;
+}
+
+// The denoiser at tau = *tau_dev (a device scalar; vamp2's gamma), skipped while *skip != 0.
+int block_denoise_dev(const amp_dims* d, const amp_constellation* c, const float2* r, const float* tau_dev,
+                      float2* xm, float* var, void* ws, const int* skip, hipStream_t st) {
+    return denoise_launch(d, c, r, 3, 0.0f, tau_dev, xm, var, ws, skip, st);
+}
+
+}  // namespace amp
+
+using namespace amp;
+
+extern "C" {
+
+size_t amp_block_denoise_workspace_bytes(const amp_dims* d) { return d ? block_denoise_ws_bytes(d) : 0; }
+
+int amp_block_denoise(const amp_dims* d, const amp_constellation* c, const void* r, int32_t tau_mode,
+                      float tau_scalar, const void* tau_vec, void* xmmse, void* var, void* ws, size_t ws_bytes,
+                      void* stream) {
+    int rc = check_dims(d, c, false);
+    if (rc) return rc;
+    AMP_REQUIRE(r && xmmse && ws, "amp_block_denoise: null pointer argument");
+    AMP_REQUIRE(tau_mode >= 0 && tau_mode <= 2, "amp_block_denoise: tau_mode %d", tau_mode);
+    AMP_REQUIRE(tau_mode == 0 || tau_vec, "amp_block_denoise: tau_vec required for tau_mode %d", tau_mode);
+    AMP_REQUIRE(tau_mode == 2 || var, "amp_block_denoise: var output required");
+    AMP_REQUIRE(ws_bytes >= amp_block_denoise_workspace_bytes(d), "amp_block_denoise: workspace too small");
+    return denoise_launch(d, c, (const float2*)r, tau_mode, 1.0f / tau_scalar, (const float*)tau_vec, (float2*)xmmse,
+                          (tau_mode == 2) ? nullptr : (float*)var, ws, nullptr, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -81,18 +81,23 @@ __device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __
 // vector ALU free for 8 of every 16 MFMA cycles.  A non-finite x keeps x0 = x and zero residuals.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ unsigned bf16_bits(float x) {
-    return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x);
-}
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void split3(float x, unsigned& p0, unsigned& p1, unsigned& p2) {
-    const __bf16 b0 = (__bf16)x;
-    const float r1 = __builtin_isfinite(x) ? x - (float)b0 : 0.0f;
-    const __bf16 b1 = (__bf16)r1;
-    const float r2 = r1 - (float)b1;
-    p0 = (unsigned)__builtin_bit_cast(unsigned short, b0);
-    p1 = (unsigned)__builtin_bit_cast(unsigned short, b1);
-    p2 = bf16_bits(r2);
+// Two values -> their three packed bf16 pieces (x in the low half): v_cvt_pk_bf16_f32 and
+// v_pk_add_f32, ~14 instructions per pair.
+__device__ __forceinline__ void split3x2(float x, float y, unsigned& p0, unsigned& p1, unsigned& p2) {
+    const f32x2_t v = {x, y};
+    const bf16x2_t b0 = __builtin_convertvector(v, bf16x2_t);
+    f32x2_t r1 = v - __builtin_convertvector(b0, f32x2_t);
+    r1.x = __builtin_isfinite(x) ? r1.x : 0.0f;
+    r1.y = __builtin_isfinite(y) ? r1.y : 0.0f;
+    const bf16x2_t b1 = __builtin_convertvector(r1, bf16x2_t);
+    const f32x2_t r2 = r1 - __builtin_convertvector(b1, f32x2_t);
+    const bf16x2_t b2 = __builtin_convertvector(r2, bf16x2_t);
+    p0 = __builtin_bit_cast(unsigned, b0);
+    p1 = __builtin_bit_cast(unsigned, b1);
+    p2 = __builtin_bit_cast(unsigned, b2);
 }
 
 // Eight consecutive complex values of one row -> the six bf16 planes (Re x0 x1 x2, Im x0 x1 x2)
@@ -102,27 +107,51 @@ __device__ __forceinline__ void x3_store8(unsigned short* sP, int ldx, int row, 
     u32x4 q[6];
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-        unsigned a0, a1, a2, b0, b1, b2, c0, c1, c2, d0, d1, d2;
-        split3(re[2 * h], a0, a1, a2);
-        split3(re[2 * h + 1], b0, b1, b2);
-        split3(im[2 * h], c0, c1, c2);
-        split3(im[2 * h + 1], d0, d1, d2);
-        q[0][h] = a0 | (b0 << 16); q[1][h] = a1 | (b1 << 16); q[2][h] = a2 | (b2 << 16);
-        q[3][h] = c0 | (d0 << 16); q[4][h] = c1 | (d1 << 16); q[5][h] = c2 | (d2 << 16);
+        unsigned a0, a1, a2, b0, b1, b2;
+        split3x2(re[2 * h], re[2 * h + 1], a0, a1, a2);
+        split3x2(im[2 * h], im[2 * h + 1], b0, b1, b2);
+        q[0][h] = a0; q[1][h] = a1; q[2][h] = a2; q[3][h] = b0; q[4][h] = b1; q[5][h] = b2;
     }
 #pragma unroll
     for (int f = 0; f < 6; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + j0) = q[f];
 }
 
-// One complex value -> its six plane entries (GEMM epilogues, accumulator layout).
-__device__ __forceinline__ void x3_store1(unsigned short* sP, int ldx, int row, int j, float re, float im) {
-    unsigned a0, a1, a2, b0, b1, b2;
-    split3(re, a0, a1, a2);
-    split3(im, b0, b1, b2);
-    unsigned short* p = sP + row * ldx + j;
+__device__ __forceinline__ float dpp_swap_pair(float v) {   // lane l <-> l ^ 1 (quad_perm [1,0,3,2])
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+// One accumulator tile's values (this lane: rows 4*(lane>>4) + r, complex column o) -> the six
+// planes, as 32-bit words of column pairs: the even lane of each pair writes rows +0 / +1, the
+// odd lane rows +2 / +3 (one DPP swap per sent value; no 16-bit LDS stores).
+__device__ __forceinline__ void x3_store_acc(unsigned short* sP, int ldx, int o, const float (&vr)[4],
+                                             const float (&vi)[4]) {
+    const int lane = threadIdx.x & 63;
+    const bool odd = (lane & 1) != 0;
+    float gr[2], gi[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        gr[h] = dpp_swap_pair(odd ? vr[h] : vr[2 + h]);
+        gi[h] = dpp_swap_pair(odd ? vi[h] : vi[2 + h]);
+    }
+    const int row0 = 4 * (lane >> 4) + (odd ? 2 : 0);
+    unsigned short* p = sP + row0 * ldx + (o & ~1);
     const int pl = 16 * ldx;
-    p[0] = (unsigned short)a0; p[pl] = (unsigned short)a1; p[2 * pl] = (unsigned short)a2;
-    p[3 * pl] = (unsigned short)b0; p[4 * pl] = (unsigned short)b1; p[5 * pl] = (unsigned short)b2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float mr = odd ? vr[2 + h] : vr[h], mi = odd ? vi[2 + h] : vi[h];
+        unsigned q[6];
+        split3x2(odd ? gr[h] : mr, odd ? mr : gr[h], q[0], q[1], q[2]);
+        split3x2(odd ? gi[h] : mi, odd ? mi : gi[h], q[3], q[4], q[5]);
+#pragma unroll
+        for (int f = 0; f < 6; ++f) *reinterpret_cast<unsigned*>(p + f * pl + h * ldx) = q[f];
+    }
+}
+
+// Scalar form (weight builder): the three pieces of one value.
+__device__ __forceinline__ void split3(float x, unsigned& p0, unsigned& p1, unsigned& p2) {
+    unsigned q0, q1, q2;
+    split3x2(x, 0.0f, q0, q1, q2);
+    p0 = q0 & 0xffffu; p1 = q1 & 0xffffu; p2 = q2 & 0xffffu;
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -133,7 +162,9 @@ __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast
 // only the operator's unique values are streamed (12 bytes per complex entry, 0.75x the f32
 // real expansion).  Accumulator t, register r: row 4*(lane>>4) + r, complex column
 // 16*(ct0 + t) + (lane & 15).
-template <int NT, int G, int R = 2>
+// Weight ring: R groups in flight (R = 1 measured best: the MFMA queue of one group covers the
+// next group's loads, tools/ubench/gemm_x3_ubench.hip); the A fragments are read one group ahead.
+template <int NT, int G, int R = 1>
 __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
                                         f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
     constexpr int RR = G < R ? G : R;
@@ -154,12 +185,19 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
                 ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 6 + f) * 1024, 0);
     const unsigned short* ap = sP + (lane & 15) * ldx + 8 * (lane >> 4);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+    u32x4 an[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int d = g % RR;
         u32x4 a[6], na[3];
 #pragma unroll
-        for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * g);
+        for (int f = 0; f < 6; ++f) a[f] = an[f];
+        if (g + 1 < G) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * (g + 1));
+        }
 #pragma unroll
         for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
 #pragma unroll

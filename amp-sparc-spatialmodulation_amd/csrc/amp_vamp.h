@@ -120,16 +120,12 @@ __device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1
 // ---------------------------------------------------------------------------
 __device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
     const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
+    // every wave sums all k terms in the same order (no LDS round trip, no barrier): the
+    // workgroup's waves hold bit-identical scalars
+    (void)lds;
     double ss = 0.0;
-    for (int i = threadIdx.x; i < P.k; i += blockDim.x) ss += (double)(1.0f / (P.s[i] * P.s[i] + vr));  // vamp.py:17, 68
+    for (int i = threadIdx.x & 63; i < P.k; i += 64) ss += (double)(1.0f / (P.s[i] * P.s[i] + vr));  // vamp.py:17, 68
     ss = group_sum(ss, 64);
-    double* sl = reinterpret_cast<double*>(lds);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sl[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    ss = 0.0;
-    for (int w = 0; w < (int)(blockDim.x / 64); ++w) ss += sl[w];
-    __syncthreads();
     const float varL = (float)(ss / (double)P.k) * (float)P.noise_var;                         // vamp.py:71
     const double eta = (double)P.k / (double)P.N;                                              // vamp.py:28
     float xtv, s2t32;

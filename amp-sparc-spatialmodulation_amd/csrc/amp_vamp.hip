@@ -430,6 +430,13 @@ int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const 
     return vamp_persist_launch(P, c64, DecConst{}, st, ncu);
 }
 
+int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
+    if (!d || k <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_X3) return AMP_E_ARG;
+    const bool fits = vamp_persist_x3_fits(d->N, k, d->L);
+    if (gemm == AMP_GEMM_X3) return fits ? AMP_GEMM_X3 : AMP_E_ARG;
+    return (gemm == AMP_GEMM_AUTO && fits && !gemm_f32_requested()) ? AMP_GEMM_X3 : AMP_GEMM_F32;
+}
+
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine) {
     if (!d || k <= 0) return AMP_E_ARG;
     const bool elig = vamp_persist_eligible(d, k, device_cu_count());

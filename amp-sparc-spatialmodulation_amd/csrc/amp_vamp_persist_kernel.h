@@ -168,9 +168,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
     constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
-    // weight groups in flight: one at four complex tiles per wave (the MFMA queue of a group
-    // covers the next group's loads; a second ring stage spills at N = 256), else two
-    constexpr int X3R = NC >= 4 ? 1 : 2;
+    constexpr int X3R = 1;                     // weight groups in flight (gemm_x3)
     const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
@@ -313,12 +311,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lane & 15);
                 const float sc = 1.0f / (s2c[t2] + cur.vr);
+                float wr[4], wi[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float qr = cr[t2][r], qi = ci[t2][r];
-                    x3_store1(sP, ldx, 4 * (lane >> 4) + r, o, sc * (yt[2 * t2][r] + cur.vr * qr) - qr,
-                              sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi);
+                    wr[r] = sc * (yt[2 * t2][r] + cur.vr * qr) - qr;
+                    wi[r] = sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi;
                 }
+                x3_store_acc(sP, ldx, o, wr, wi);
             }
         } else
 #pragma unroll

@@ -26,6 +26,7 @@ import numpy as np  # noqa: E402
 import torch        # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 HBM_PEAK_GBS = 8000.0
 # time(oracle) / time(reference) on the same 8 cores of the build container, same cfg4 workload
 # (tools/cpu_ratio.py; the reference cannot travel to the GPU box): the port's CPU speed relative
@@ -225,6 +226,7 @@ def main():
         kern, flops_launch = 'vamp_k2 (GEMM2 + Onsager update + section denoiser)', flops_mv
         kms = {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}
     achieved = flops_launch / (ms[1] * 1e-3) / 1e12
+    x3 = persistent and nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) == nat.GEMM_X3
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -246,8 +248,14 @@ def main():
                    'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),
-                     'kernel': kern, 'flop_per_launch': flops_launch},
+                     'kernel': kern, 'flop_per_launch': flops_launch,
+                     'gemm': 'bf16x3' if x3 else 'f32'},
     }
+    if x3:
+        # the f32 products run as six bf16 MFMA products each (amp_persist.h gemm_x3): the matrix
+        # cores' own rate is 6x the f32-equivalent one, against the dense bf16 peak
+        out['roofline']['bf16_issued'] = {'achieved': 6 * achieved, 'peak': BF16_MFMA_PEAK_TFLOPS,
+                                          'frac': 6 * achieved / BF16_MFMA_PEAK_TFLOPS}
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args.config, args.ebn0, args.seed, args.cpu_sample)
     print(json.dumps(out), flush=True)

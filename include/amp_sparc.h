@@ -124,6 +124,9 @@ typedef struct amp_vamp_args {
 /* The engine amp_vamp_run will use for this shape on the current device (LAUNCHES or
  * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
+/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_X3 or AMP_GEMM_F32
+ * (AMP_E_ARG when `gemm` is AMP_GEMM_X3 and the shape does not fit it). */
+int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
  * phase into trace (device, nwg * max_iter * 10 + 2 * nwg uint64; layout in amp_vamp.hip). */
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
@@ -295,6 +298,29 @@ int amp_gemm_nt_f32(const void* a, int32_t lda, int32_t rows, int32_t ka, const 
 /* Real expansion of a complex operator X[o][j] = rowscale[o] * op(src[o*so + j*sj]) into Wt. */
 int amp_build_cweight(const void* src, int64_t so, int64_t sj, int32_t conj, const void* rowscale,
                       int32_t O, int32_t J, void* wt, int32_t kap, int32_t ncp, void* stream);
+
+/* ---- damped "Rangan" VAMP — replaces vamp2.py's VAMP.forward (vamp2.py:103-135), Tracker
+ *      (:12-26) and VAMPLayer.forward (:52-77) with its segmented denoiser (:79-88).  The
+ *      reference's VAMP passes damping = 1.0 (vamp2.py:96); sparc mode only (the reference crashes
+ *      in 'random' / 'segmented' mode).  status.last_scalar = {gamma, alpha, gamma~, d.mean()}. */
+typedef struct amp_vamp2_args {
+    const void* U;      /* c64 [n][k] */
+    const void* s;      /* f32 [k] */
+    const void* Vh;     /* c64 [k][N] */
+    const void* y;      /* c64 [B][n] */
+    int32_t k;          /* min(n, N) */
+    int32_t max_iter;   /* config.N_Layers */
+    double sigma2;      /* Na/Nr/SNR (vamp2.py:123, Python float) */
+    double damping;     /* rho (vamp2.py:50) */
+    void* r;            /* out c64 [B][N]: T.r, the decision input (vamp2.py:131) */
+    void* xmmse;        /* out c64 [B][N]: the damped T.xmmse */
+    void* var;          /* out f32 [B][N] */
+    void* status;       /* out amp_status (device) */
+    void* ws;           /* workspace, amp_vamp2_workspace_bytes() bytes */
+    size_t ws_bytes;
+} amp_vamp2_args;
+size_t amp_vamp2_workspace_bytes(const amp_dims* d, int32_t k);
+int amp_vamp2_run(const amp_dims* d, const amp_constellation* c, const amp_vamp2_args* a, void* stream);
 
 /* Diagnostics. */
 const char* amp_last_error(void);

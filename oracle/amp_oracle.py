@@ -614,7 +614,8 @@ def shrink_sw_ook(r, cov, B, L, M):
     return x.reshape(B, L * M).astype(C64), var.reshape(B, L * M)
 
 
-__all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect',
+__all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect', 'vamp2_detect',
+           'vamp2_denoise',
            'bamp_detect', 'scamp_detect', 'map_decision', 'error_rates', 'loss_dict', 'allclose_f32',
            'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX',
            'shrink_bayes', 'shrink_ook', 'shrink_sw_ook', 'segmented_decision',

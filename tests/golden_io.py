@@ -32,6 +32,16 @@ def g1_cases():
     return cases
 
 
+def g12_cases():
+    """{name: Case} — vamp2.py (damped VAMP) reference traces with their stored inputs."""
+    cases = _group(np.load(os.path.join(GOLDEN, 'g12_vamp2.npz')))
+    for name, c in cases.items():
+        _, alph, nt, ebn0, seed, damp = name.split('_')
+        c['alphabet'], c['EbN0'], c['seed'] = alph, float(ebn0), int(seed)
+        c['loss_ref'] = json.loads(str(c['loss']))
+    return cases
+
+
 def g2_cases():
     return _group(np.load(os.path.join(GOLDEN, 'g2_denoiser.npz')))
 

@@ -23,7 +23,7 @@ constexpr int LDA = KC + 8;   // bf16 elements per LDS row (16-byte pad)
 
 __device__ __forceinline__ bf16x8 as_bf(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
-template <int NT, int G, int R, int AUX = 0>
+template <int NT, int G, int R, int AUX = 0, int MODE = 0, bool PF = false>
 __device__ __forceinline__ void gemm_x3(const unsigned short* sA, const void* wq, int ct0, f32x4 (&cr)[NT],
                                         f32x4 (&ci)[NT]) {
     const int lane = threadIdx.x & 63;
@@ -41,18 +41,32 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sA, const void* wq
 #pragma unroll
             for (int f = 0; f < 6; ++f) ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 6 + f) * 1024, AUX);
     const unsigned short* ap = sA + (lane & 15) * LDA + 8 * (lane >> 4);
+    u32x4 an[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int d = g % R;
         u32x4 a[6];
 #pragma unroll
-        for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA + 32 * g);
+        for (int f = 0; f < 6; ++f) a[f] = an[f];
+        if (PF && g + 1 < G) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA + 32 * (g + 1));
+        } else if (!PF) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA + 32 * g);
+        }
         u32x4 na[3];
 #pragma unroll
         for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const u32x4* w = ring[d][t];
+            if constexpr (MODE == 1) {
+                for (int f = 0; f < 6; ++f) cr[t][f & 3] += __builtin_bit_cast(float, w[f].x ^ a[f].y);
+                continue;
+            }
             // smallest terms first
 #define MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(x), as_bf(y), acc, 0, 0, 0)
             MF(cr[t], a[0], w[2]); MF(ci[t], a[0], w[5]);
@@ -69,7 +83,7 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sA, const void* wq
             MF(cr[t], na[0], w[3]); MF(ci[t], a[3], w[0]);
 #undef MF
         }
-        if (g + R < G) {
+        if (MODE != 2 && g + R < G) {
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -80,7 +94,7 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sA, const void* wq
     }
 }
 
-template <int R, int AUX = 0>
+template <int R, int AUX = 0, int MODE = 0, bool PF = false>
 __global__ __launch_bounds__(256, 1) void kx3(const unsigned short* apieces, const void* wq, float* out,
                                                unsigned long long* cyc) {
     __shared__ unsigned short sA[6 * 16 * LDA];
@@ -94,7 +108,7 @@ __global__ __launch_bounds__(256, 1) void kx3(const unsigned short* apieces, con
     f32x4 cr[NT], ci[NT];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int rep = 0; rep < REPS; ++rep) {
-        gemm_x3<NT, G, R, AUX>(sA, wq, wave * NT, cr, ci);
+        gemm_x3<NT, G, R, AUX, MODE, PF>(sA, wq, wave * NT, cr, ci);
         __syncthreads();
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -129,8 +143,8 @@ static void split3(float x, unsigned short p[3]) {
     p[2] = bf16_rn(r2);
 }
 
-template <int R, int AUX = 0>
-static void run(const std::vector<unsigned short>& ap, const std::vector<unsigned short>& wp,
+template <int R, int AUX = 0, int MODE = 0, bool PF = false>
+static void run(int nwg, const std::vector<unsigned short>& ap, const std::vector<unsigned short>& wp,
                 const std::vector<double>& ref, const std::vector<float>& f32c) {
     unsigned short *dA;
     void* dW;
@@ -142,10 +156,10 @@ static void run(const std::vector<unsigned short>& ap, const std::vector<unsigne
     hipMalloc(&dc, NWG * 8);
     hipMemcpy(dA, ap.data(), ap.size() * 2, hipMemcpyHostToDevice);
     hipMemcpy(dW, wp.data(), wp.size() * 2, hipMemcpyHostToDevice);
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((kx3<R, AUX>), dim3(NWG), dim3(256), 0, 0, dA, dW, dO, dc);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((kx3<R, AUX, MODE, PF>), dim3(nwg), dim3(256), 0, 0, dA, dW, dO, dc);
     hipDeviceSynchronize();
-    std::vector<unsigned long long> c(NWG);
-    hipMemcpy(c.data(), dc, NWG * 8, hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> c(NWG, 0);
+    hipMemcpy(c.data(), dc, nwg * 8, hipMemcpyDeviceToHost);
     std::sort(c.begin(), c.end());
     std::vector<float> o(16 * OC * 2);
     hipMemcpy(o.data(), dO, o.size() * 4, hipMemcpyDeviceToHost);
@@ -155,8 +169,8 @@ static void run(const std::vector<unsigned short>& ap, const std::vector<unsigne
         ef = std::max(ef, fabs(f32c[i] - ref[i]));
         nrm = std::max(nrm, fabs(ref[i]));
     }
-    printf("bf16x3 AUX=%d R=%d: cycles per GEMM median %.0f  max %.0f   max|err| x3 %.3e  f32-seq %.3e  (max|C| %.3f)\n", AUX, R,
-           (double)c[NWG / 2] / REPS, (double)c[NWG - 1] / REPS, ex3, ef, nrm);
+    printf("bf16x3 PF=%d MODE=%d nwg=%d AUX=%d R=%d: cycles per GEMM median %.0f  max %.0f   max|err| x3 %.3e  f32-seq %.3e  (max|C| %.3f)\n", (int)PF, MODE, nwg, AUX, R,
+           (double)c[NWG - nwg + nwg / 2] / REPS, (double)c[NWG - 1] / REPS, ex3, ef, nrm);
     hipFree(dA); hipFree(dW); hipFree(dO); hipFree(dc);
 }
 
@@ -209,10 +223,11 @@ int main() {
             ref[(r * OC + o) * 2] = sr; ref[(r * OC + o) * 2 + 1] = si;
             f32c[(r * OC + o) * 2] = fr; f32c[(r * OC + o) * 2 + 1] = fi;
         }
-    run<2, 0>(ap, wp, ref, f32c);
-    run<2, 1>(ap, wp, ref, f32c);
-    run<2, 2>(ap, wp, ref, f32c);
-    run<2, 3>(ap, wp, ref, f32c);
-    run<2, 16>(ap, wp, ref, f32c);
+    run<2, 0, 0, false>(256, ap, wp, ref, f32c);
+    run<2, 0, 2, false>(256, ap, wp, ref, f32c);
+    run<1, 0, 0, true>(256, ap, wp, ref, f32c);
+    run<2, 0, 0, true>(256, ap, wp, ref, f32c);
+    run<3, 0, 0, true>(256, ap, wp, ref, f32c);
+    run<2, 0, 2, true>(256, ap, wp, ref, f32c);
     return 0;
 }
