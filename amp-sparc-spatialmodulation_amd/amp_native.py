@@ -73,7 +73,8 @@ class AmpBampArgs(C.Structure):
 
 class AmpScampArgs(C.Structure):
     _fields_ = [('W', C.c_void_p), ('A', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32),
-                ('engine', C.c_int32), ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p),
+                ('engine', C.c_int32), ('gemm', C.c_int32), ('pad', C.c_int32), ('noise_var', C.c_double),
+                ('xmap', C.c_void_p), ('xmmse', C.c_void_p),
                 ('psi', C.c_void_p), ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
 

@@ -55,6 +55,9 @@ struct ScampK {
     Partial* pparts;       // [max_iter][nwg] 32-B granule pairs
     double* pxch;          // [max_iter][nwg][4] rare-path exchange
     unsigned* pbar;        // [0] arrivals, [1] abort flag (zeroed by the prepare launch)
+    int x3;                // persistent GEMMs on the bf16x3 engine (Wx1 / Wx2)
+    const void* Wx1;       // A    X3-packed (x3_index, O = n, J = N)
+    const void* Wx2;       // A^H  X3-packed (O = N, J = n)
     Const c;
 };
 
@@ -64,7 +67,7 @@ struct ScampWs {
     Partial* parts;
     ScampIter* iters;
     unsigned* psi_nc;
-    float *Wq1, *Wq2;
+    float *Wq1, *Wq2, *Wx1, *Wx2;
     unsigned* pbar;
     Partial* pparts;
     double* pxch;
@@ -106,6 +109,8 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     const int nwg = cdiv(d->B, 16);
     w.Wq1 = cv.take<float>((size_t)2 * d->n * 2 * d->N);
     w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * d->n);
+    w.Wx1 = cv.take<float>((size_t)3 * d->n * d->N);    // 6 bf16 per complex entry
+    w.Wx2 = cv.take<float>((size_t)3 * d->N * d->n);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(64);
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);
@@ -124,6 +129,7 @@ __device__ __forceinline__ float scamp_gamma(const ScampK& P, const float* psi_r
 }
 
 bool scamp_persist_eligible(const amp_dims* d, int ncu);
+bool scamp_persist_x3_fits(const amp_dims* d);
 int scamp_persist_launch(const ScampK& P, const Const64& c64, hipStream_t st);
 
 }  // namespace amp

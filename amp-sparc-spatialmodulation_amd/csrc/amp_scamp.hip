@@ -426,6 +426,15 @@ size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter) {
 
 namespace amp {
 
+// AMP_SCAMP_GEMM=f32: AMP_GEMM_AUTO keeps the f32-MFMA persistent GEMMs (A/B runs)
+static bool scamp_gemm_f32_requested() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_SCAMP_GEMM");
+        return e && e[0] == 'f';
+    }();
+    return v;
+}
+
 static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, ScampK& P,
                        Const64& c64) {
     int rc = check_dims(d, c);
@@ -451,8 +460,13 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.nwg = cdiv(d->B, 16);
     P.gen = 0;
     P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
+    P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.c = to_const(c);
     c64 = to_const64(c);
+    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_X3, "amp_scamp: gemm %d", a->gemm);
+    const bool fits = scamp_persist_x3_fits(d);
+    AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || fits, "amp_scamp: the bf16x3 engine's LDS carve exceeds 160 KB");
+    P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && fits && !scamp_gemm_f32_requested())) ? 1 : 0;
     return AMP_OK;
 }
 
@@ -462,6 +476,13 @@ static int scamp_persist_prepare(ScampK& P, const amp_scamp_args* a, hipStream_t
     static std::atomic<unsigned> gen{0};
     P.gen = ++gen;
     CWeightJob j[2];
+    if (P.x3) {
+        //   A x     (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N   (bf16x3 planes)
+        j[0] = CWeightJob{(const float2*)a->A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wx1, P.N, P.n, WPACKX3};
+        //   A^H s   (scamp.py:57)   X[o][j] = conj(A[j][o]),  o < N, j < n
+        j[1] = CWeightJob{(const float2*)a->A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.Wx2, P.n, P.N, WPACKX3};
+        return build_cweights(j, 2, P.pbar, 64, st);
+    }
     //   A x       (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N
     j[0] = CWeightJob{(const float2*)a->A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.n, WPACK16};
     //   A^H s     (scamp.py:57)   X[o][j] = conj(A[j][o]),  o < N, j < n

@@ -123,12 +123,15 @@ class SCAMPLayer(nn.Module):
 
 class SCAMP(LazyResult, nn.Module):
     """``engine``: nat.ENGINE_AUTO (the persistent single-launch engine when the shape allows it,
-    else seven launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h)."""
+    else seven launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h).
+    ``gemm``: the persistent engine's GEMM arithmetic, nat.GEMM_AUTO (split-precision bf16x3 where
+    it fits, else f32 MFMA), GEMM_F32 or GEMM_X3 (amp_sparc.h)."""
 
-    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO) -> None:
+    def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO, gemm: int = nat.GEMM_AUTO) -> None:
         super().__init__()
         self.config = config
         self.engine = engine
+        self.gemm = gemm
         self.E = config.Na / config.Nr                                    # scamp.py:72
         self.layers = nn.ModuleList([SCAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
@@ -152,6 +155,7 @@ class SCAMP(LazyResult, nn.Module):
         with torch.cuda.device(y.device):
             T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
             T.args.engine = self.engine
+            T.args.gemm = self.gemm
             T._call('amp_scamp_run')
         self._keep = T
         return T
@@ -162,6 +166,7 @@ class SCAMP(LazyResult, nn.Module):
         with torch.cuda.device(y.device):
             T = Tracker(W, A, y, self.E / SNR, self.config, self._bufs)
             T.args.engine = self.engine
+            T.args.gemm = self.gemm
             res, host = self._result_slot(T.y.device)
             T.res = res
             T.args.status = nat.dptr(res)

@@ -204,6 +204,8 @@ typedef struct amp_scamp_args {
     const void* y;      /* c64 [B][n] */
     int32_t max_iter;
     int32_t engine;     /* amp_scamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT (as for VAMP) */
+    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 (as for VAMP) */
+    int32_t pad;
     double noise_var;   /* Na/Nr/SNR (scamp.py:98) */
     void* xmap;         /* out c64 [B][N] (scamp.py:107) */
     void* xmmse;        /* out c64 [B][N] */

@@ -49,14 +49,17 @@ def _points(name, every=1):
     return [(name, k) for k in keys[::every]]
 
 
-POINTS = ([(n, k, 0) for n, k in _points('cfg1_bamp_qpsk')] +
-          [(n, k, e) for n, k in _points('cfg3_scamp_16qam') + _points('cfg3_scamp_qpsk') for e in (1, 2)])
+# SCAMP variants: (engine, persistent GEMM arithmetic); 'persistent' is the product default
+# (bf16x3 where it fits), 'persistent-f32' the f32-MFMA form
+SVARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1)}
+POINTS = ([(n, k, 'bamp') for n, k in _points('cfg1_bamp_qpsk')] +
+          [(n, k, e) for n, k in _points('cfg3_scamp_16qam') + _points('cfg3_scamp_qpsk') for e in sorted(SVARIANTS)])
 
 
 @pytest.mark.parametrize('name,key,engine', POINTS)
 def test_curve_point(device, name, key, engine):
     """VER / SER within 1e-3 of the reference on the same seeds; SCAMP on both of its engines
-    (cfg3 is persistent-eligible: 1 = launches, 2 = persistent)."""
+    (cfg3 is persistent-eligible) and both GEMM arithmetics of the persistent one."""
     from bamp import BAMP
     from scamp import SCAMP
     ent = CURVES[name]
@@ -67,7 +70,9 @@ def test_curve_point(device, name, key, engine):
     if ent['algo'] == 'bamp':
         L = BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
     else:
-        L = SCAMP(cfg, engine=engine)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        eng, gemm = SVARIANTS[engine]
+        L = SCAMP(cfg, engine=eng, gemm=gemm)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'],
+                                              inp['idx'])
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
@@ -105,6 +110,40 @@ def test_layer_level_equals_forward(device, name):
     assert T.status().T == ref[2] == int(c.T)
     assert gio.bits_equal(a, ref[0]) and gio.bits_equal(b, ref[1])
 
+
+
+@pytest.mark.parametrize('ebn0', [0.0, 8.0])
+@pytest.mark.parametrize('alph', ['QPSK', '16QAM'])
+def test_scamp_x3_matches_f32(device, alph, ebn0):
+    """The persistent SCAMP engine's bf16x3 GEMMs against its f32-MFMA GEMMs at cfg3: after one
+    and three iterations xmap agrees to float32 GEMM summation-order noise, the full detection to
+    the same T and counting metrics within 1e-3."""
+    import torch
+    import amp_native as nat
+    from scamp import SCAMP
+    inp = None
+    for iters in (1, 3):
+        cfg = _config(128, 8, 256, 4096, alph, iterations=iters)
+        if inp is None:
+            inp = _regen_inputs(cfg, 0, ebn0, svd=False)
+        xs = []
+        for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+            det = SCAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm)
+            det.detect(inp['W'], inp['A'], inp['y'], inp['SNR'])
+            xs.append(det.xmap.clone())
+        scale = float(torch.nan_to_num(xs[0]).abs().max())
+        assert torch.allclose(xs[0], xs[1], rtol=0, atol=4e-6 * scale, equal_nan=True), \
+            (iters, float((xs[0] - xs[1]).abs().nan_to_num().max()), scale)
+    cfg = _config(128, 8, 256, 4096, alph, iterations=20)
+    outs = []
+    for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+        L = SCAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'],
+                                                                inp['sym'], inp['idx'])
+        outs.append({k: float(np.asarray(v)) for k, v in L.loss.items()})
+    a, b = outs
+    assert abs(a['T'] - b['T']) <= 1, (a['T'], b['T'])
+    for k in ('ver', 'ser', 'fer', 'ier'):
+        assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
 
 
 @pytest.mark.parametrize('ebn0', [0.0, 4.0, 8.0, 20.0])
