@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """BASELINE cfg5 shape on one MI355X: BAMP Nt=512 Nr=1024 Na=16, B=8192 trials, on the
-correlated channel (rho = 0.5), QPSK / 16-QAM twins of the 64-QAM that Config rejects.
+correlated channel (rho = 0.5): 64-QAM as named (injected into Config, which rejects it like the
+reference, exactly as tests/cfg5_inputs.py does) and its QPSK / 16-QAM twins.
 
 Times `amp_bamp_run` (detector iterations only: 5 GEMM-class launches per iteration) and the
 whole forward (+ GPU decision / counters + the 256-byte readback) with HIP events on the stream
@@ -31,9 +32,12 @@ PEAK_TF = 157.3
 
 def main():
     dev = torch.device('cuda:0')
-    for alph, ebn0 in (('QPSK', 2.0), ('16QAM', 10.0)):
-        cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=20, alphabet=alph,
+    for alph, ebn0 in (('64QAM', 16.0), ('QPSK', 2.0), ('16QAM', 10.0)):
+        cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=20,
+                     alphabet='16QAM' if alph == '64QAM' else alph,
                      channel_profile='uniform', channel_truncation='tail', device='cpu')
+        if alph == '64QAM':
+            cfg.inject_square_qam(64)
         np.random.seed(0)
         torch.manual_seed(0)
         ch, da = Channel(cfg), Data(cfg)
