@@ -78,6 +78,10 @@ class AmpScampArgs(C.Structure):
                 ('psi', C.c_void_p), ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t)]
 
 
+# amp_allreduce_fn (include/amp_sparc.h): all-reduce `count` float64 words at a device pointer
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
+ALLREDUCE_SUM, ALLREDUCE_MAX = 0, 1
+
 _P = C.c_void_p
 _I = C.c_int32
 _D = C.POINTER(AmpDims)
@@ -97,6 +101,12 @@ SIGNATURES = {
     'amp_vamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_profile': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(C.c_float), _P]),
     'amp_vamp_detect_count': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _P]),
+    'amp_vamp_epochs_workspace_bytes': (C.c_size_t, [_D, _I, _I, _I]),
+    'amp_set_allreduce_hook': (C.c_int, [_P, _P]),
+    'amp_vamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
+    'amp_map_decide_count_rows': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, C.c_int64, _P, _P, _P, C.c_size_t, _P]),
+    'amp_vamp_detect_count_epochs': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
+                                               _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_bamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),

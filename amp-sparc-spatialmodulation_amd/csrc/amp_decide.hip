@@ -23,6 +23,7 @@ constexpr int AMP_DEC_MAX_NA = 64;
 struct DecK {
     int B, L, M, Na, Lin, S;
     int ibits;
+    long long s_off;    // section offset of these rows in the whole batch (trial-sharded decision)
     const float2* xmap;
     const float2* xmmse;
     const float2* x;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(AMP_WG) void map_decide_kernel(DecK P) {
         if (act && g == 0) {
             P.mism[s] = (unsigned char)mm;
             if (P.dec) P.dec[s] = bi;
-            count_section<KK>(P.c, s, M, P.L, P.Na, P.Lin, bi, se, P.sym[s], P.idx[s], ibmask, q);
+            count_section<KK>(P.c, s + P.s_off, M, P.L, P.Na, P.Lin, bi, se, P.sym[s], P.idx[s], ibmask, q);
         }
     }
     long long ier = q.ier, ser = q.ser, iber = q.iber, sber = q.sber;
@@ -289,7 +290,7 @@ size_t amp_map_decide_workspace_bytes(const amp_dims* d) {
 
 static int decide_count(int rule, const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
                         const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
-                        void* decisions, void* ws, size_t ws_bytes, void* stream) {
+                        void* decisions, void* ws, size_t ws_bytes, void* stream, long long row0 = 0) {
     int rc = check_dims(d, c, false);
     if (rc) return rc;
     AMP_REQUIRE(xmap && xmmse && x && sym && idx && counts && ws, "amp_map_decide_count: null pointer argument");
@@ -298,6 +299,7 @@ static int decide_count(int rule, const amp_dims* d, const amp_constellation* c,
     DecK P;
     P.B = d->B; P.L = d->L; P.M = d->M; P.Na = d->Na; P.Lin = d->Lin; P.S = d->B * d->L;
     P.ibits = ibits_trunc;
+    P.s_off = row0 * d->L;
     P.xmap = (const float2*)xmap; P.xmmse = (const float2*)xmmse; P.x = (const float2*)x;
     P.sym = (const long long*)sym; P.idx = (const long long*)idx;
     Carve cv(ws);
@@ -322,6 +324,14 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
     return decide_count(0, d, c, xmap, xmmse, x, sym, idx, ibits_trunc, counts, decisions, ws, ws_bytes, stream);
 }
 
+int amp_map_decide_count_rows(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
+                              const void* x, const void* sym, const void* idx, int32_t ibits_trunc, int64_t row0,
+                              void* counts, void* decisions, void* ws, size_t ws_bytes, void* stream) {
+    AMP_REQUIRE(row0 >= 0, "amp_map_decide_count_rows: row0 = %lld", (long long)row0);
+    return decide_count(0, d, c, xmap, xmmse, x, sym, idx, ibits_trunc, counts, decisions, ws, ws_bytes, stream,
+                        (long long)row0);
+}
+
 int amp_segmented_decide_count(const amp_dims* d, const amp_constellation* c, const void* xmap, const void* xmmse,
                                const void* x, const void* sym, const void* idx, int32_t ibits_trunc, void* counts,
                                void* decisions, void* ws, size_t ws_bytes, void* stream) {
@@ -341,6 +351,7 @@ int amp_random_decide_count(const amp_dims* d, const amp_constellation* c, const
     DecK P;
     P.B = d->B; P.L = d->L; P.M = d->M; P.Na = d->Na; P.Lin = d->Lin; P.S = d->B * d->L;
     P.ibits = ibits_trunc;
+    P.s_off = 0;
     P.xmap = (const float2*)xmap; P.xmmse = (const float2*)xmmse; P.x = (const float2*)x;
     P.sym = (const long long*)sym; P.idx = (const long long*)idx;
     Carve cv(ws);

@@ -134,6 +134,37 @@ inline Const64 to_const64(const amp_constellation* c) {
 int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
 int device_cu_count();   // compute units of the current device (cached)
 
+// Launch path of the persistent (grid-synchronising) engines: a plain launch after the
+// co-residency check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
+inline bool persist_coop() {
+    static const bool c = [] {
+        const char* e = getenv("AMP_PERSIST_LAUNCH");
+        return e && e[0] == 'c';
+    }();
+    return c;
+}
+
+// One persistent grid: nwg workgroups of `threads`, `lds` bytes of dynamic LDS, kernel
+// arguments `args` (hipLaunchCooperativeKernel's array form, also used for the plain launch
+// through hipLaunchKernel).  per_cu: resident workgroups per CU from the occupancy query.
+inline int persist_grid_launch(const char* what, const void* fn, int nwg, int threads, size_t lds, int per_cu,
+                               void** args, hipStream_t st) {
+    if (per_cu < 1 || (long)per_cu * device_cu_count() < nwg) {
+        set_error("%s: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", what, nwg, per_cu,
+                  device_cu_count());
+        return AMP_E_LAUNCH;
+    }
+    const hipError_t e = persist_coop()
+        ? hipLaunchCooperativeKernel(fn, dim3(nwg), dim3(threads), args, (unsigned)lds, st)
+        : hipLaunchKernel(fn, dim3(nwg), dim3(threads), args, lds, st);
+    if (e != hipSuccess) {
+        set_error("%s: %s launch (%d x %d, %zu B LDS): %s", what, persist_coop() ? "cooperative" : "plain", nwg,
+                  threads, lds, hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    return AMP_OK;
+}
+
 // Column tile width of the section-fused GEMMs: a multiple of 2M so no section straddles
 // two workgroups.
 inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }

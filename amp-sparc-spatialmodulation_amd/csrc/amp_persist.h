@@ -233,18 +233,20 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
 // Grid barrier: arrival counter + abort word in pbar (zeroed before the launch).  The
 // workgroup's payload stores precede it in program order (thread 0 stores them or the
 // barrier below orders them); agent-scope release on arrival, acquire after the wait.
-__device__ inline bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
+// grid_sync_on: the same over a group of workgroups with its own arrival counter `cnt` (the
+// persistent VAMP engine's side-by-side epochs); `abort_w` is shared by the whole grid.
+__device__ inline bool grid_sync_on(unsigned* cnt, unsigned* abort_w, unsigned target, int* s_flag) {
     __syncthreads();
     if (threadIdx.x == 0) {
         int ok = 1;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(pbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load(pbar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
-                __hip_atomic_store(pbar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = 0;
                 break;
             }
@@ -254,6 +256,10 @@ __device__ inline bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
     }
     __syncthreads();
     return *s_flag != 0;
+}
+
+__device__ inline bool grid_sync(unsigned* pbar, unsigned target, int* s_flag) {
+    return grid_sync_on(pbar, pbar + 1, target, s_flag);
 }
 
 // ---- per-iteration partials: data-tagged granules (no fences, no counter) ----

@@ -414,16 +414,12 @@ static int spersist_launch_t(const ScampK& P, const Const64& c64, hipStream_t st
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess) per_cu = 0;
         attr_lds = lds;
     }
-    // plain launch after the co-residency check a cooperative launch would make; every barrier
-    // spin is bounded (2 s) as the backstop
-    if (per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
-        set_error("scamp_persist: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", P.nwg, per_cu,
-                  device_cu_count());
-        return AMP_E_LAUNCH;
-    }
-    hipLaunchKernelGGL((scamp_persist<NT1, G1, NT2, G2, KK, X3>), dim3(P.nwg), dim3(256), lds, st, P, c64);
-    AMP_LAUNCH_CHECK("scamp_persist");
-    return AMP_OK;
+    // persist_grid_launch (amp_host.h): plain launch after the co-residency check, or the
+    // cooperative one; every barrier spin is bounded (2 s) as the backstop
+    ScampK Pc = P;
+    Const64 cc = c64;
+    void* args[] = {(void*)&Pc, (void*)&cc};
+    return persist_grid_launch("scamp_persist", fn, P.nwg, 256, lds, per_cu, args, st);
 }
 
 template <int NT1, int G1, int NT2, int G2, bool X3>

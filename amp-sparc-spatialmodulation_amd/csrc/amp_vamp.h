@@ -11,9 +11,23 @@
 namespace amp {
 
 constexpr int RWG = 1024;   // threads of the reduction / fix-up workgroup
+constexpr int PBAR_EPOCH = 64;                 // first per-epoch barrier counter in pbar
+constexpr int PBAR_WORDS = PBAR_EPOCH + 256;   // one counter per epoch (E <= 256 workgroups)
+
+// Batch-global values of one trial-sharded iteration (amp_vamp_run_sharded): each stage's
+// float64 words are all-reduced across the ranks by the registered hook between launches.
+struct XState {
+    double sum[2];    // SUM: sum var, not-close count (vamp.py:85, 185)
+    double mx[2];     // MAX: max|xi| (NaN -> +inf), -min section max (vamp.py:112)
+    double gmax[2];   // MAX: exact float64 max|xi| over the candidate sections (rare path); [1] pad
+    double fix[4];    // SUM: rare-path var delta, not-close delta, recomputed sections; [3] pad
+    int mode;         // 2: this iteration takes the rare path (xr3 / xr4 act), else 0
+    int pad[3];
+};
 
 struct VampK {
     int B, N, n, k, L, M;
+    int Bmean;          // the batch var.mean() runs over (vamp.py:85): B, or the whole batch when sharded
     int kap0, ncp0, kap1, ncp1, kap2, ncp2, bn2;
     int nblk2, max_iter;
     double noise_var, sparsity;
@@ -34,12 +48,15 @@ struct VampK {
     VampIter* iters;    // [max_iter + 1]: iters[t] drives iteration t
     amp_status* status;
     // persistent engine
-    int nwg;            // ceil(B / PBM) workgroups
+    int nwg;            // workgroups: E * wpe
+    int E, wpe;         // side-by-side epochs (independent batches of B trials, one channel) and
+                        // workgroups per epoch (ceil(B / PBM)); E = 1 outside amp_vamp_detect_count_epochs
     const float* Wq1;   // Vh   16x16x4-packed [2k][2N]
     const float* Wq2;   // V    16x16x4-packed [2N][2k]
     Partial* pparts;    // [max_iter][nwg] 32-B granule pairs (amp_vamp_persist.hip), right after pbar
     double* pxch;       // [max_iter][nwg][4] rare-path exchange
-    unsigned* pbar;     // [0] arrivals, [1] abort flag (zeroed by the prepare launch)
+    unsigned* pbar;     // [0] arrivals, [1] abort flag, [PBAR_EPOCH + e] epoch e's arrivals
+                        // (PBAR_WORDS words zeroed by the prepare launch)
     unsigned gen;       // launch generation: granule tags are gen * (max_iter + 1) + t + 1
     int ytil_in_kernel; // y~ = (s Uh) y computed by the persistent kernel itself (n == 2N)
     const float* Wq0;   // s Uh 16x16x4-packed [2k][2n] (ytil_in_kernel)
@@ -55,6 +72,7 @@ struct VampK {
     int x3;                      // persistent engine GEMMs on the bf16x3 engine (Wx1 / Wx2)
     const void* Wx1;             // Vh X3-packed (x3_index, O = k, J = N)
     const void* Wx2;             // V  X3-packed (O = N, J = k)
+    XState* xs;                  // trial-sharded exchange words (amp_vamp_run_sharded)
     Const c;
 };
 
@@ -69,6 +87,7 @@ struct VampWs {
     double* pxch;
     unsigned* pbar;
     DecWG* dwg;
+    XState* xs;
     size_t bytes;
 };
 
@@ -105,9 +124,10 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.Wx1 = cv.take<float>((size_t)3 * k * d->N);      // 6 bf16 per complex entry
     w.Wx2 = cv.take<float>((size_t)3 * k * d->N);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
-    w.pbar = cv.take<unsigned>(64);                          // 256 B: pbar and the granules that
-    w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // follow it are zeroed by one memset
+    w.pbar = cv.take<unsigned>(PBAR_WORDS);                  // barrier words (zeroed per launch); the
+    w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // granules carry generation tags
     w.dwg = cv.take<DecWG>((size_t)nwg);
+    w.xs = cv.take<XState>(1);
     w.bytes = cv.off;
     return w;
 }
@@ -174,7 +194,7 @@ __device__ inline VampIter vamp_advance(const VampK& P, const VampIter& cur, con
         nx.fixed = fixed;
     } else {
         // var.mean() (vamp.py:85): float64 sum of the float32 values, NaN / inf propagate
-        const float mean = (float)(pa.sumvar / ((double)P.B * (double)P.N));
+        const float mean = (float)(pa.sumvar / ((double)P.Bmean * (double)P.N));
         const float dxdr = clampf_t(mean / cur.sigma2, AMP_VAR_RATIO_MIN, 1.0f - AMP_VAR_RATIO_MIN);  // vamp.py:85-87
         const float ns = 1.0f / (1.0f - dxdr);                                                        // vamp.py:89
         const float s2t = clampf_t((cur.sigma2 * dxdr) * ns, AMP_VAR_MIN, AMP_VAR_MAX);              // vamp.py:92-94
@@ -228,7 +248,7 @@ struct PDenoisePolicy {
 
 constexpr int PBM = 16;   // trials per workgroup
 
-bool vamp_persist_eligible(const amp_dims* d, int k, int ncu);
+bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs = 1);
 bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);

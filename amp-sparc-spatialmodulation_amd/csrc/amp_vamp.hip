@@ -209,6 +209,167 @@ __global__ __launch_bounds__(RWG) void vamp_r(VampK P, Const64 c64, int t) {
     }
 }
 
+// ---- trial-sharded iteration (amp_vamp_run_sharded; SURVEY §8(e) exact-compat mode) ----
+// Each rank holds a contiguous slice of the batch; vamp_k1 / vamp_k2 run on it unchanged.  The
+// batch-global values of vamp_r (sum var, allclose count, max|xi|, min section max, and on the
+// rare path the exact float64 max|xi| and the recomputed sections' deltas) go through the
+// registered all-reduce hook in three stages, so every rank derives the scalars a single
+// whole-batch forward derives (up to the float64 summation order of var.mean()).
+//   xr1: local partials -> xs.sum / xs.mx            [hook: SUM sum[2], MAX mx[2]]
+//   xr2: all-NaN / no-danger iterations advance here; the rare path publishes its local
+//        exact max|xi| candidate -> xs.gmax          [hook: MAX gmax[1]]
+//   xr3: rare path: exact recompute of the local out-of-range sections -> xs.fix
+//                                                     [hook: SUM fix[3]]
+//   xr4: rare path: fold the deltas and advance.
+// Every stage runs on every rank every iteration (stopped iterations carry zeros), so the
+// hook calls match across ranks with no host synchronisation.
+__device__ inline PartAcc xs_global(const XState& x) {
+    PartAcc pa;
+    pa.sumvar = x.sum[0];
+    pa.notclose = (uint32_t)x.sum[1];
+    pa.maxabs = x.mx[0];
+    pa.minsecmax = -x.mx[1];
+    return pa;
+}
+
+__global__ __launch_bounds__(RWG) void vamp_xr1(VampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    XState* xs = P.xs;
+    if (P.iters[t].stopped) {
+        if (threadIdx.x == 0) { xs->sum[0] = xs->sum[1] = 0.0; xs->mx[0] = xs->mx[1] = 0.0; }
+        return;
+    }
+    const PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk2, P.nblk2, lds);
+    if (threadIdx.x == 0) {
+        xs->sum[0] = pa.sumvar;
+        xs->sum[1] = (double)pa.notclose;
+        // a NaN / inf max|xi| (the reference's all-NaN iteration) must win the MAX: +inf
+        xs->mx[0] = (pa.maxabs <= 1.7976931348623157e308) ? pa.maxabs : INFINITY;
+        xs->mx[1] = (pa.minsecmax == pa.minsecmax) ? -pa.minsecmax : INFINITY;
+    }
+}
+
+__global__ __launch_bounds__(RWG) void vamp_xr2(VampK P, Const64 c64, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    XState* xs = P.xs;
+    const VampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) { P.iters[t + 1] = cur; xs->mode = 0; xs->gmax[0] = 0.0; }
+        return;
+    }
+    PartAcc pa = xs_global(*xs);
+    if (!part_allnan(pa) && part_danger(pa)) {
+        // the rare path: this rank's exact float64 max|xi| over its candidate sections
+        const float inv = cur.inv_sigma2;
+        const float2* r2 = reinterpret_cast<const float2*>(P.r);
+        const int M = P.M;
+        const double G32 = pa.maxabs, slack = logit_slack(G32);
+        double gm = 0.0;
+        for (int s = threadIdx.x; s < P.B * P.L; s += blockDim.x) {
+            if (!((double)P.secabs[s] >= G32 - slack)) continue;
+            const size_t o0 = (size_t)s * M;
+            gm = fmax(gm, section_absmax_f64([=](int m, float& rr, float& ri, float& it) {
+                const float2 v = r2[o0 + m];
+                rr = v.x; ri = v.y; it = inv;
+            }, M, c64));
+        }
+        gm = group_max(gm, 64);
+        double* sd = reinterpret_cast<double*>(lds);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) sd[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double G = 0.0;
+            for (int w = 0; w < RWG / 64; ++w) G = fmax(G, sd[w]);
+            xs->gmax[0] = G;
+            xs->mode = 2;
+        }
+        return;
+    }
+    int fixed = 0;
+    if (part_allnan(pa)) {
+        if (!cur.fixed_all) nan_fill(P.xm, var_buf(P, t), (size_t)P.B * P.N);
+        pa.sumvar = __longlong_as_double(0x7ff8000000000000LL);
+        pa.notclose = 1;
+        fixed = -1;
+    }
+    const VampIter nx = vamp_advance(P, cur, pa, fixed, t, lds);
+    if (threadIdx.x == 0) {
+        P.iters[t + 1] = nx;
+        if (nx.stopped || t + 1 == P.max_iter) *P.status = vamp_make_status(P, cur, nx, fixed);
+        xs->mode = 0;
+        xs->gmax[0] = 0.0;
+    }
+}
+
+__global__ __launch_bounds__(RWG) void vamp_xr3(VampK P, Const64 c64, int t) {
+    __shared__ double s_d[3][RWG / 64];
+    XState* xs = P.xs;
+    if (xs->mode != 2) {
+        if (threadIdx.x == 0) xs->fix[0] = xs->fix[1] = xs->fix[2] = 0.0;
+        return;
+    }
+    const VampIter cur = P.iters[t];
+    const PartAcc pa = xs_global(*xs);
+    const double G = xs->gmax[0], slack = logit_slack(pa.maxabs);
+    float* vn = var_buf(P, t);
+    const float* vp = var_buf(P, t + 1);
+    const float inv = cur.inv_sigma2;
+    const float2* r2 = reinterpret_cast<const float2*>(P.r);
+    float2* x2 = reinterpret_cast<float2*>(P.xm);
+    const int M = P.M;
+    double dsum = 0.0;
+    int dnc = 0, cnt = 0;
+    for (int s = threadIdx.x; s < P.B * P.L; s += blockDim.x) {
+        if (!((double)P.secmax[s] - G < AMP_DANGER + slack)) continue;
+        ++cnt;
+        const size_t o0 = (size_t)s * M;
+        exact_section_f64<true>(
+            [=](int m, float& rr, float& ri, float& it) {
+                const float2 v = r2[o0 + m];
+                rr = v.x; ri = v.y; it = inv;
+            },
+            [&](int m, float xr, float xi, float var) {
+                const size_t o = o0 + m;
+                const float old = vn[o];
+                dsum += (double)var - (double)old;
+                dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(old, vp[o]) ? 0 : 1);
+                x2[o] = make_float2(xr, xi);
+                vn[o] = var;
+            },
+            M, c64, G);
+    }
+    dsum = group_sum(dsum, 64);
+    dnc = group_sum(dnc, 64);
+    cnt = group_sum(cnt, 64);
+    if ((threadIdx.x & 63) == 0) {
+        s_d[0][threadIdx.x >> 6] = dsum; s_d[1][threadIdx.x >> 6] = (double)dnc; s_d[2][threadIdx.x >> 6] = (double)cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0, c = 0.0;
+        for (int w = 0; w < RWG / 64; ++w) { a += s_d[0][w]; b += s_d[1][w]; c += s_d[2][w]; }
+        xs->fix[0] = a; xs->fix[1] = b; xs->fix[2] = c;
+    }
+}
+
+__global__ __launch_bounds__(RWG) void vamp_xr4(VampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    const XState* xs = P.xs;
+    if (xs->mode != 2) return;
+    const VampIter cur = P.iters[t];
+    PartAcc pa = xs_global(*xs);
+    pa.sumvar += xs->fix[0];                                   // (sum - old) + new, in float64
+    pa.notclose = (uint32_t)((long long)pa.notclose + (long long)xs->fix[1]);
+    pa.maxabs = xs->gmax[0];
+    const int fixed = (int)xs->fix[2];
+    const VampIter nx = vamp_advance(P, cur, pa, fixed, t, lds);
+    if (threadIdx.x == 0) {
+        P.iters[t + 1] = nx;
+        if (nx.stopped || t + 1 == P.max_iter) *P.status = vamp_make_status(P, cur, nx, fixed);
+    }
+}
+
 __global__ void vamp_init_kernel(VampK P) {
     // Tracker (vamp.py:22-26) in the form the fused kernels consume:
     //   xmmse = p, r = 0 so that r~ = (xmmse - 0*r)*1 = p   (vamp.py:25)
@@ -262,6 +423,10 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.nwg = cdiv(d->B, PBM);
+    P.Bmean = d->B;
+    P.xs = w.xs;
+    P.E = 1;
+    P.wpe = P.nwg;
     P.Wq0 = w.Wq0; P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
     P.gen = 0;
     P.ytil_in_kernel = 0;
@@ -380,11 +545,12 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     j[2] = yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
               : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
-    int rc = build_cweights(j, 3, P.pbar, 64, st);
+    int rc = build_cweights(j, 3, P.pbar, PBAR_WORDS, st);
     if (rc || yk) return rc;
     rc = vamp_attrs();
     if (rc) return rc;
-    return gemm_store((const float*)a->y, 2 * P.n, P.B, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k, 2 * P.k, st);
+    return gemm_store((const float*)a->y, 2 * P.n, P.B * P.E, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k,
+                      2 * P.k, st);
 }
 
 static int vamp_iterate_impl(const VampK& P, const Const64& c64, int t, hipStream_t st) {
@@ -405,11 +571,63 @@ static int vamp_finalize_impl(const VampK& P, hipStream_t st) {
     return AMP_OK;
 }
 
+static amp_allreduce_fn g_hook = nullptr;
+static void* g_hook_ctx = nullptr;
+
+static int call_hook(double* buf, int count, int op, hipStream_t st) {
+    const int rc = g_hook((void*)buf, count, op, (void*)st, g_hook_ctx);
+    if (rc) set_error("amp_vamp_run_sharded: all-reduce hook returned %d", rc);
+    return rc ? AMP_E_LAUNCH : AMP_OK;
+}
+
+static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipStream_t st) {
+    dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
+    hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_k1");
+    launch_k2(P, t, st);
+    AMP_LAUNCH_CHECK("vamp_k2");
+    hipLaunchKernelGGL(vamp_xr1, dim3(1), dim3(RWG), 0, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_xr1");
+    int rc = call_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
+    if (!rc) rc = call_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(vamp_xr2, dim3(1), dim3(RWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("vamp_xr2");
+    if ((rc = call_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hipLaunchKernelGGL(vamp_xr3, dim3(1), dim3(RWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("vamp_xr3");
+    if ((rc = call_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hipLaunchKernelGGL(vamp_xr4, dim3(1), dim3(RWG), 0, st, P, t);
+    AMP_LAUNCH_CHECK("vamp_xr4");
+    return AMP_OK;
+}
+
 }  // namespace amp
 
 using namespace amp;
 
 extern "C" {
+
+int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx) {
+    g_hook = fn;
+    g_hook_ctx = ctx;
+    return AMP_OK;
+}
+
+int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t B_global,
+                         void* stream) {
+    VampK P;
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(g_hook, "amp_vamp_run_sharded: no all-reduce hook registered (amp_set_allreduce_hook)");
+    AMP_REQUIRE(B_global >= d->B, "amp_vamp_run_sharded: B_global = %d < this rank's B = %d", B_global, d->B);
+    P.Bmean = B_global;
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_prepare_impl(P, a, st);
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = vamp_iterate_sharded(P, c64, t, st);
+    return rc ? rc : vamp_finalize_impl(P, st);
+}
 
 // Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
 // boundary: trace[(wg * max_iter + t) * 10 + phase], phases = start, r~ built, GEMM1, w stored,
@@ -517,6 +735,48 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
     AMP_REQUIRE(a->engine != AMP_ENGINE_LAUNCHES && vamp_persist_eligible(d, a->k, ncu),
                 "amp_vamp_detect_count: needs the persistent engine (k == N in {64, 128, 256}, M <= 64, "
                 "ceil(B/16) = %d <= %d CUs)", cdiv(d->B, PBM), ncu);
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_persist_prepare(P, a, st);
+    if (rc) return rc;
+    P.dec_on = 1;
+    P.ibits = dec->ibits_trunc;
+    P.xtrue = (const float2*)dec->x;
+    P.sym = (const long long*)dec->sym;
+    P.idx = (const long long*)dec->idx;
+    P.counts = (amp_counts*)dec->counts;
+    return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
+}
+
+size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs) {
+    if (!d || k <= 0 || max_iter <= 0 || epochs < 1 || (long)d->B * epochs > (1L << 30)) return 0;
+    amp_dims de = *d;
+    de.B = d->B * epochs;   // the carve holds every epoch's rows and one granule pair per workgroup
+    return vamp_carve(&de, k, max_iter, nullptr).bytes;
+}
+
+int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                 const amp_vamp_decide_args* dec, int32_t epochs, void* stream) {
+    AMP_REQUIRE(d && epochs >= 1 && (long)d->B * epochs <= (1L << 30), "amp_vamp_detect_count_epochs: epochs = %d",
+                epochs);
+    const int ncu = device_cu_count();
+    AMP_REQUIRE(a && a->engine != AMP_ENGINE_LAUNCHES && vamp_persist_eligible(d, a->k, ncu, epochs),
+                "amp_vamp_detect_count_epochs: needs the persistent engine (k == N in {64, 128, 256}, M <= 64, "
+                "B %% 16 == 0 when epochs > 1, epochs * ceil(B/16) = %d <= %d CUs)", epochs * cdiv(d->B, PBM), ncu);
+    amp_dims de = *d;
+    de.B = d->B * epochs;
+    VampK P;
+    Const64 c64;
+    int rc = vamp_setup(&de, c, a, P, c64);   // carve and buffers over all epochs' rows
+    if (rc) return rc;
+    P.B = d->B;                               // the batch of one epoch (mean var, vamp.py:85)
+    P.Bmean = d->B;
+    P.E = epochs;
+    P.wpe = cdiv(d->B, PBM);
+    P.nwg = P.E * P.wpe;
+    AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts,
+                "amp_vamp_detect_count_epochs: null pointer argument");
+    AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_vamp_detect_count_epochs: ibits_trunc");
+    AMP_REQUIRE(d->Lin * d->Na * d->M == d->N, "amp_vamp_detect_count_epochs: inconsistent dims");
     hipStream_t st = (hipStream_t)stream;
     rc = vamp_persist_prepare(P, a, st);
     if (rc) return rc;

@@ -36,9 +36,10 @@
 
 namespace amp {
 
+// one workgroup per epoch: epoch e's n per-workgroup records -> out[e]
 __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out) {
     __shared__ DecWG s[16];
-    dec_fold_block(w, n, out, s);
+    dec_fold_block(w + (size_t)blockIdx.x * n, n, out + blockIdx.x, s);
 }
 
 static std::once_flag g_pers_once;
@@ -63,9 +64,9 @@ bool vamp_persist_x3_fits(int N, int k, int L) {
     return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
 }
 
-bool vamp_persist_eligible(const amp_dims* d, int k, int ncu) {
+bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
-    if (cdiv(d->B, PBM) > ncu) return false;
+    if (epochs < 1 || (epochs > 1 && d->B % PBM != 0) || (long)epochs * cdiv(d->B, PBM) > ncu) return false;
     return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
 }
 
@@ -80,7 +81,7 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
     static_cast<Const64&>(d2) = c64;
     int rc = persist_dispatch(P, d2, st);
     if (rc || !P.dec_on) return rc;
-    hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.wpe, P.counts);
     AMP_LAUNCH_CHECK("vamp_decide_fold");
     return AMP_OK;
 }

@@ -47,9 +47,11 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // this workgroup's rows while r (the decision input, vamp.py:187) and xmmse are still in LDS;
 // per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
 // mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
+// row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
+// (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
 template <int PWG, int KK>
 __device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
-                                int nrows, float* sT, void* lab_lds, void* scr) {
+                                int lrow0, int nrows, float* sT, void* lab_lds, void* scr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int M = P.M, L = P.L, N = P.N;
     const int S = nrows * L;
@@ -110,7 +112,7 @@ __device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float*
         double se;
         decide_section<KK, DG, true>(dc, M, g, ld, bi, mm, se);
         if (act && g == 0) {
-            const long long s = (long long)(row0 + row) * L + l;
+            const long long s = (long long)(lrow0 + row) * L + l;
             mism[lsc] = (unsigned char)mm;
             count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
         }
@@ -182,7 +184,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
     float* scr = lds + Y.offScr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wg = blockIdx.x, nwg = gridDim.x;
-    const int row0 = wg * PBM, nrows = min(PBM, P.B - row0);
+    // side-by-side epochs: workgroups [ep * wpe, (ep + 1) * wpe) hold epoch ep's B trials and
+    // exchange its batch scalars among themselves only
+    const int ep = wg / P.wpe, wl = wg - ep * P.wpe, wg0 = ep * P.wpe;
+    const int lrow0 = wl * PBM;                       // first trial within the epoch
+    const int row0 = ep * P.B + lrow0, nrows = min(PBM, P.B - lrow0);
+    unsigned* ebar = P.pbar + (P.E > 1 ? PBAR_EPOCH + ep : 0);   // this epoch's arrival counter
     const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
     const int ldr = Y.ldr, lda = Y.lda;
     const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
         stamp(t, 5);
         // 5. batch scalars: every workgroup gathers and reduces every partial
         PartAcc g;
-        if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, tag, P.pbar + 1, g, scr, &s_flag)) {
+        if (!part_gather(grs, ((unsigned)t * nwg + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) {
             aborted = 1;
             break;
         }
@@ -416,9 +423,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
                 for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
                 P.pxch[((size_t)t * nwg + wg) * 4 + 0] = m4;
             }
-            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+            if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) { aborted = 1; break; }
             double G = 0.0;
-            for (int w = 0; w < nwg; ++w) G = fmax(G, P.pxch[((size_t)t * nwg + w) * 4 + 0]);
+            for (int w = wg0; w < wg0 + P.wpe; ++w) G = fmax(G, P.pxch[((size_t)t * nwg + w) * 4 + 0]);
             // (b) exact recompute of this workgroup's sections below the danger line
             double dsum = 0.0;
             int dnc = 0, cnt = 0;
@@ -450,9 +457,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
                 P.pxch[((size_t)t * nwg + wg) * 4 + 2] = b;
                 P.pxch[((size_t)t * nwg + wg) * 4 + 3] = c;
             }
-            if (!grid_sync(P.pbar, ++nbar * (unsigned)nwg, &s_flag)) { aborted = 1; break; }
+            if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) { aborted = 1; break; }
             double a = 0.0, b = 0.0, c = 0.0;
-            for (int w = 0; w < nwg; ++w) {
+            for (int w = wg0; w < wg0 + P.wpe; ++w) {
                 const double* q = P.pxch + ((size_t)t * nwg + w) * 4;
                 a += q[1]; b += q[2]; c += q[3];
             }
@@ -475,14 +482,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
         P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldr + col];
     }
     for (int e = tid; e < nrows * N; e += PWG) P.var0[(size_t)row0 * N + e] = vlast[e];
-    if (wg == 0 && tid == 0) {
+    if (wl == 0 && tid == 0) {
         amp_status s = vamp_make_status(P, cur, nx, fixed);
         if (aborted) s.nan_state = -1;
-        *P.status = s;
+        P.status[ep] = s;
     }
     if (P.dec_on) {
         __syncthreads();   // the V0/V1 region (vlast) becomes the label / mismatch scratch
-        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldr, row0, nrows, sA, lds + Y.offV0, scr);
+        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldr, row0, lrow0, nrows, sA, lds + Y.offV0, scr);
     }
 }
 
@@ -507,17 +514,8 @@ static inline int den_u() {
     return u;
 }
 
-// Launch path: a plain launch after an explicit co-residency check (default), or
-// hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).  The cooperative path made processes
-// crash in exit-time teardown under rocprofv3 on the box (r01), the plain one does not.
-static inline bool persist_coop() {
-    static bool c = [] {
-        const char* e = getenv("AMP_PERSIST_LAUNCH");
-        return e && e[0] == 'c';
-    }();
-    return c;
-}
-
+// Launch path: persist_grid_launch (amp_host.h): a plain launch after an explicit co-residency
+// check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
 template <int NT, int KK, int NWV, int DU, bool X3>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
     const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3>;
@@ -537,32 +535,11 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
         if (e != hipSuccess) per_cu = 0;
         attr_lds = lds;
     }
-    if (persist_coop()) {
-        VampK Pc = P;
-        DecConst dd = dc;
-        void* args[] = {(void*)&Pc, (void*)&dd};
-        e = hipLaunchCooperativeKernel(fn, dim3(P.nwg), dim3(64 * NWV), args, (unsigned)lds, st);
-        if (e != hipSuccess) {
-            set_error("vamp_persist: hipLaunchCooperativeKernel(%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds,
-                      hipGetErrorString(e));
-            return AMP_E_LAUNCH;
-        }
-        return AMP_OK;
-    }
-    // plain launch: co-residency checked here (resident workgroups per CU x CUs >= grid), the
-    // check hipLaunchCooperativeKernel would make; the bounded barrier spins stay as the backstop
-    if (per_cu < 1 || (long)per_cu * device_cu_count() < P.nwg) {
-        set_error("vamp_persist: grid of %d workgroups cannot be co-resident (%d per CU x %d CUs)", P.nwg, per_cu,
-                  device_cu_count());
-        return AMP_E_LAUNCH;
-    }
-    hipLaunchKernelGGL((vamp_persist<NT, KK, NWV, DU, X3>), dim3(P.nwg), dim3(64 * NWV), lds, st, P, dc);
-    e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error("vamp_persist: launch (%d x %d, %zu B LDS): %s", P.nwg, 64 * NWV, lds, hipGetErrorString(e));
-        return AMP_E_LAUNCH;
-    }
-    return AMP_OK;
+    // the bounded barrier spins stay as the backstop of either launch path
+    VampK Pc = P;
+    DecConst dd = dc;
+    void* args[] = {(void*)&Pc, (void*)&dd};
+    return persist_grid_launch("vamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
 template <int NT, int NWV, bool X3>

@@ -63,16 +63,32 @@ def _broadcast_seed() -> int:
 
 class Model(nn.Module):
     def __init__(self, config: Config, detector: str = 'vamp', path: str | None = None, amp=None,
-                 seed: int | None = None, rng: str = 'host') -> None:
+                 seed: int | None = None, rng: str = 'host', group_epochs: bool = False,
+                 shard: str = 'epochs') -> None:
         """rng='host' (default): the reference's numpy / torch-CPU random streams, bit for bit
         (parity mode).  rng='device': channel, messages and noise drawn on the GPU and the SVD
-        on the GPU (throughput mode: same distributions, different streams)."""
+        on the GPU (throughput mode: same distributions, different streams).
+        group_epochs: VAMP detects the epochs of one `res` block (one channel) side by side in
+        one persistent launch (VAMP.forward_epochs; same results, fills the GPU at small B).
+        shard (with torch.distributed): 'epochs' (default) gives each rank whole epochs with its
+        own random stream and merges the metrics once per SNR point; 'trials' (SURVEY §8(e)
+        exact-compat, VAMP) gives every rank the SAME epochs (one seed) and splits each batch's
+        trials over the ranks with the batch scalars all-reduced every iteration (ShardedVAMP),
+        so the sweep equals the single-process sweep."""
         super().__init__()
         self.config = config
         self.detector = detector
         self.rate = config.code_rate
         self.shannon_limit = config.shannon_limit_dB
         self.min_snr = self.shannon_limit
+        if shard not in ('epochs', 'trials'):
+            raise ValueError(f"shard must be 'epochs' or 'trials', got {shard!r}")
+        if shard == 'trials' and detector != 'vamp':
+            raise ValueError("shard='trials' is built for the VAMP detector")
+        self.shard = shard
+        if amp is None and shard == 'trials':
+            from vamp import ShardedVAMP
+            amp = ShardedVAMP(config)
         self.amp = amp if amp is not None else _detector(detector, config)
         self.loss = Loss(config)
         self.rng = rng
@@ -80,6 +96,10 @@ class Model(nn.Module):
         self.data = Data(config, rng=rng)
         self.path = path if path is not None else f'Simulations/{_DIRS[detector]}/{config.name}'
         self.rank, self.world = _dist()
+        # trial sharding: every rank draws the same epochs (rank-independent seeding), the
+        # detector splits each batch; epoch sharding: one stream per rank
+        self._stream_rank = 0 if shard == 'trials' else self.rank
+        self._epoch_world = 1 if shard == 'trials' else self.world
         if seed is None and self.world > 1:
             # unseeded multi-rank sweep: every rank would start torch's and numpy's generators
             # from the same default state and draw the same epochs; rank 0 draws a base seed
@@ -88,13 +108,47 @@ class Model(nn.Module):
         self.seed = seed
         if seed is not None:
             # one independent stream per rank (rank 0 of a 1-process run = the plain seed)
-            np.random.seed((seed + 7919 * self.rank) % 2 ** 32)
-            torch.manual_seed(seed + 7919 * self.rank)
+            np.random.seed((seed + 7919 * self._stream_rank) % 2 ** 32)
+            torch.manual_seed(seed + 7919 * self._stream_rank)
         if self.rank == 0:
             os.makedirs(self.path, exist_ok=True)
+        self.group_cap = 0
+        if group_epochs:
+            if detector != 'vamp' or not hasattr(self.amp, 'forward_epochs'):
+                raise ValueError('group_epochs: side-by-side epochs are built for the VAMP detector')
+            N, n = config.Nt * config.Lin, config.Nr * config.Lout
+            k = min(n, N)
+            cap = 1
+            while self.amp.epochs_eligible(n, k, cap + 1):
+                cap += 1
+            self.group_cap = cap if self.amp.epochs_eligible(n, k, 1) else 0
 
     # one epoch, in the reference's random-call order (vamp_model.py:55-61)
     def _epoch(self, SNR: float, new_channel: bool):
+        x, sym, idx, y = self._inputs(SNR, new_channel)
+        if self.detector == 'vamp':
+            U, s, Vh = self._svd
+            return self.amp(U, s, Vh, y, SNR, x, sym, idx)
+        if self.detector == 'bamp':
+            return self.amp(self._A, y, SNR, x, sym, idx)
+        return self.amp(self._W, self._A, y, SNR, x, sym, idx)
+
+    def _block(self, SNR: float, n: int) -> list:
+        """n epochs of one `res` block (one channel, drawn first) with VAMP's side-by-side
+        launch (VAMP.forward_epochs): every epoch's inputs are drawn in the reference's call
+        order (channel, then message + noise per epoch), then the epochs are detected in chunks
+        that fit one persistent grid.  Results equal n sequential _epoch calls."""
+        inputs = [self._inputs(SNR, i == 0) for i in range(n)]
+        U, s, Vh = self._svd
+        cap = max(1, self.group_cap)
+        out = []
+        for c0 in range(0, n, cap):
+            ch = inputs[c0:c0 + cap]
+            out += self.amp.forward_epochs(U, s, Vh, [v[3] for v in ch], SNR, [v[0] for v in ch],
+                                           [v[1] for v in ch], [v[2] for v in ch])
+        return out
+
+    def _inputs(self, SNR: float, new_channel: bool):
         if new_channel:
             W, A = self.channel.generate_as_sparc()
             self._A = A
@@ -115,12 +169,7 @@ class Model(nn.Module):
             # y = A x + n on the host as the reference's CPU path forms it (vamp_model.py:60)
             A_h = self._A if self._A.device.type == 'cpu' else self._A.cpu()
             y = (A_h @ x.cpu() + self.channel.awgn(SNR).cpu()).to(x.device)
-        if self.detector == 'vamp':
-            U, s, Vh = self._svd
-            return self.amp(U, s, Vh, y, SNR, x, sym, idx)
-        if self.detector == 'bamp':
-            return self.amp(self._A, y, SNR, x, sym, idx)
-        return self.amp(self._W, self._A, y, SNR, x, sym, idx)
+        return x, sym, idx, y
 
     @torch.no_grad()
     def run(self, SNR: float) -> Loss:
@@ -129,8 +178,9 @@ class Model(nn.Module):
         return loss
 
     def _merge(self) -> None:
-        """Sum the per-rank accumulated metrics (one all-reduce per SNR point)."""
-        if self.world == 1:
+        """Sum the per-rank accumulated metrics (one all-reduce per SNR point).  Trial sharding
+        needs none: every rank's Loss already holds the whole batch's counters."""
+        if self.world == 1 or self.shard == 'trials':
             return
         keys = ['T'] + [k for k in self.loss.keys if k in self.loss.loss]
         vals = torch.tensor([float(np.asarray(self.loss.loss.get(k, 0.0), dtype=np.float64)) for k in keys],
@@ -155,7 +205,12 @@ class Model(nn.Module):
                 print(f'EbN0dB={EbN0dB}')
             SNR = 10 ** (SNRdB / 10)
             for i in range(epochs):
-                if (i // res) % self.world != self.rank:      # blocks of `res` epochs share a channel
+                if (i // res) % self._epoch_world != self.rank % self._epoch_world:   # blocks of `res` share a channel
+                    continue
+                if self.group_cap > 1 and res > 1:
+                    if i % res == 0:                          # the whole block at once
+                        for loss in self._block(SNR, min(res, epochs - i)):
+                            self.loss.accumulate(loss)
                     continue
                 loss = self._epoch(SNR, i % res == 0)
                 self.loss.accumulate(loss)
@@ -172,7 +227,7 @@ class Model(nn.Module):
             if self.rank == 0:
                 print(f'FER={fer}, iter={it}')
                 self.loss.export(SNRdB, EbN0dB, self.path)
-            else:
+            elif self.shard == 'epochs':
                 self.loss.loss = {'T': 0}
             if fer < 1e-3:
                 break

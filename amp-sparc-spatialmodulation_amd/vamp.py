@@ -265,6 +265,226 @@ class VAMP(LazyResult, nn.Module):
         self.last = T
         return self.L
 
+    def epochs_eligible(self, n: int, k: int, epochs: int) -> bool:
+        """Whether `epochs` forwards of this config fit ONE persistent launch
+        (amp_vamp_detect_count_epochs): persistent-engine shape, B % 16 == 0 and
+        epochs * B / 16 <= the device's CUs."""
+        if self.config.mode != 'sparc' or epochs < 1 or (epochs > 1 and self.config.B % 16):
+            return False
+        d = self.config.dims()
+        if nat.lib().amp_vamp_select_engine(C.byref(d), k, self.engine) != nat.ENGINE_PERSISTENT:
+            return False
+        return epochs * (-(-self.config.B // 16)) <= torch.cuda.get_device_properties(
+            torch.cuda.current_device()).multi_processor_count
+
+    def forward_epochs(self, U, s, Vh, ys, SNR: float, xs, symbols, indices) -> list:
+        """E epochs that share ONE channel (U, s, Vh) — the epochs of one `res` block of
+        Model.simulate (vamp_model.py:55-61 redraws the channel only when i % res == 0) —
+        detected side by side in one persistent launch (amp_vamp_detect_count_epochs).  Every
+        epoch keeps its own batch-global scalars and early exit (vamp.py:85, 112, 185), so the
+        returned Loss objects (one per epoch, in order) equal E sequential forward() calls.
+        ys / xs: sequences of the epochs' y [B, n, 1] and x [B, N, 1]; symbols / indices:
+        sequences of their label arrays.  One host synchronisation per call."""
+        if self.config.mode != 'sparc':
+            raise NotImplementedError("side-by-side epochs decide in generator_mode='sparc' only")
+        E = len(ys)
+        if not (E == len(xs) == len(symbols) == len(indices)) or E < 1:
+            raise ValueError('forward_epochs: ys, xs, symbols and indices must hold the same number (>= 1) of epochs')
+        dev = ys[0].device
+        with torch.cuda.device(dev):
+            return self._forward_epochs(U, s, Vh, ys, SNR, xs, symbols, indices, E, dev)
+
+    def _forward_epochs(self, U, s, Vh, ys, SNR, xs, symbols, indices, E, dev):
+        from loss import _as_device_labels, _flat_c64
+        cfg = self.config
+        B = cfg.B
+        n, k = U.shape[0], U.shape[1]
+        N = Vh.shape[1]
+        Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
+        sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
+        y = torch.cat([_c64(v, (B, n)) for v in ys]).contiguous()
+        x = torch.cat([_flat_c64(v, B, 'x') for v in xs]).contiguous()
+        sym = torch.cat([_as_device_labels(v, dev).reshape(-1) for v in symbols]).contiguous()
+        idx = torch.cat([_as_device_labels(v, dev).reshape(-1) for v in indices]).contiguous()
+        if sym.numel() != E * B * cfg.L or idx.numel() != E * B * cfg.L:
+            raise ValueError(f'expected {E * B * cfg.L} labels/indices, got {sym.numel()}/{idx.numel()}')
+        d, cst = cfg.dims(), cfg.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_vamp_epochs_workspace_bytes(C.byref(d), k, cfg.N_Layers, E)
+        if wsb == 0:
+            raise ValueError('amp_vamp_epochs_workspace_bytes: invalid dimensions')
+        ws = nat.WORKSPACE.get(dev, 'vamp_epochs', wsb)
+        r = torch.empty(E * B, N, dtype=torch.complex64, device=dev)
+        xm = torch.empty_like(r)
+        var = torch.empty(E * B, N, dtype=torch.float32, device=dev)
+        st_sz, ct_sz = C.sizeof(nat.AmpStatus), C.sizeof(nat.AmpCounts)
+        res, host = self._epochs_slot(dev, E * (st_sz + ct_sz))
+        a = nat.AmpVampArgs()
+        a.U, a.s, a.Vh, a.y = nat.dptr(Uc, name='U'), nat.dptr(sc, torch.float32, 's'), nat.dptr(Vhc, name='Vh'), \
+            nat.dptr(y, name='y')
+        a.k, a.max_iter, a.engine, a.gemm = k, cfg.N_Layers, self.engine, self.gemm
+        a.noise_var, a.sparsity = float(self.E / SNR), float(self.sparsity)
+        a.r, a.xmmse, a.var = nat.dptr(r), nat.dptr(xm), nat.dptr(var)
+        a.status = nat.dptr(res)
+        a.ws, a.ws_bytes = nat.dptr(ws), ws.numel()
+        dec = nat.AmpVampDecideArgs()
+        dec.x, dec.sym, dec.idx = nat.dptr(x, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices')
+        dec.ibits_trunc = self.L._ibits
+        dec.counts = nat.dptr(res) + E * st_sz
+        nat.check(lib.amp_vamp_detect_count_epochs(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), E,
+                                                   nat.stream_ptr(dev)), 'amp_vamp_detect_count_epochs')
+        # the records come back asynchronously: each Loss resolves on first access, and the
+        # previous call's Losses are resolved here, after this call's launches are queued
+        host[:res.numel()].copy_(res, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(dev))
+        for L in self._epochs_prev:
+            L.resolve()
+        out = []
+
+        def finish(L, e):
+            done.synchronize()
+            raw = host.numpy()
+            status = nat.AmpStatus.from_buffer_copy(raw[e * st_sz:(e + 1) * st_sz].tobytes())
+            counts = nat.AmpCounts.from_buffer_copy(raw[E * st_sz + e * ct_sz:E * st_sz + (e + 1) * ct_sz].tobytes())
+            if status.nan_state < 0:
+                raise RuntimeError('amp_vamp_detect_count_epochs: persistent engine grid barrier timed out')
+            L.last_counts, L.last_status = counts, status
+            L.record(L.rates_from_counts(counts), int(status.T))
+
+        for e in range(E):
+            L = Loss(cfg)
+            L._pending = (lambda L=L, e=e: finish(L, e))
+            out.append(L)
+        self._epochs_prev = out
+        self._epochs_keep = (y, x, sym, idx, Uc, Vhc, sc)   # alive until the kernels have read them
+        self.last_epochs = (r.view(E, B, N, 1), xm.view(E, B, N, 1), var.view(E, B, N, 1))
+        return out
+
+    _epochs_prev = ()
+    _epochs_ring = None
+    _epochs_i = 1
+
+    def _epochs_slot(self, device, nbytes):
+        """One of two (device, pinned host) result buffers for forward_epochs, alternating per
+        call, so a call's records stay readable while the next call runs."""
+        if self._epochs_ring is None or self._epochs_ring[0][0].device != device or \
+                self._epochs_ring[0][0].numel() < nbytes:
+            self._epochs_ring = [(torch.zeros(nbytes, dtype=torch.uint8, device=device),
+                                  torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)) for _ in range(2)]
+        self._epochs_i ^= 1
+        d, h = self._epochs_ring[self._epochs_i]
+        d.zero_()
+        return d[:nbytes], h[:nbytes]
+
+
+class ShardedVAMP(VAMP):
+    """SURVEY §8(e) exact-compat mode: ONE batch of config.B trials split over the ranks of
+    torch.distributed, rank r detecting trials [r B / P, (r + 1) B / P).
+
+    ``forward`` keeps VAMP.forward's signature and takes the WHOLE batch's inputs (every rank
+    draws the same epoch from the same seed: channel, messages and noise are replicated with no
+    communication); the rank runs its slice through amp_vamp_run_sharded, whose
+    registered hook all-reduces the batch-global scalars of every iteration (var.mean(),
+    max |xi|, allclose; vamp.py:85, 112, 185) five times per iteration, decides its rows with
+    amp_map_decide_count_rows and merges the error counters with ONE all-reduce.  The returned
+    Loss equals the whole-batch forward's, up to the float64 summation order of var.mean().
+    The hook runs torch.distributed.all_reduce on the device words for RCCL ('nccl') and
+    through host memory for gloo."""
+
+    def __init__(self, config: Config, group=None) -> None:
+        super().__init__(config, engine=nat.ENGINE_LAUNCHES)
+        self.group = group
+        self._ws = None
+        self._hook_error = None
+        self._hook = nat.ALLREDUCE_FN(self._allreduce)     # kept alive with the detector
+
+    def _allreduce(self, buf, count, op, stream, ctx) -> int:
+        """amp_allreduce_fn: `count` float64 words at device address `buf` (inside this
+        detector's workspace), in place, ordered on the current stream."""
+        try:
+            dist = torch.distributed
+            ws = self._ws
+            off = int(buf) - ws.data_ptr()
+            if off < 0 or off + 8 * count > ws.numel():
+                raise ValueError(f'hook buffer outside the workspace (offset {off})')
+            view = ws[off:off + 8 * count].view(torch.float64)
+            rop = dist.ReduceOp.SUM if op == nat.ALLREDUCE_SUM else dist.ReduceOp.MAX
+            if view.device.type == 'cuda' and dist.get_backend(self.group) == 'nccl':
+                dist.all_reduce(view, op=rop, group=self.group)
+            else:
+                h = view.cpu()
+                dist.all_reduce(h, op=rop, group=self.group)
+                view.copy_(h)
+            return 0
+        except Exception as e:   # noqa: BLE001 — surfaced by the C driver as AMP_E_LAUNCH
+            self._hook_error = e
+            return 1
+
+    def shard(self):
+        dist = torch.distributed
+        rank, world = (dist.get_rank(self.group), dist.get_world_size(self.group)) if dist.is_initialized() else (0, 1)
+        B = self.config.B
+        return rank * B // world, (rank + 1) * B // world
+
+    def _forward(self, U, s, Vh, y, SNR, x, symbols, indices) -> Loss:
+        from loss import _as_device_labels, _flat_c64, allreduce_counts, counts_to_vector, vector_to_counts
+        cfg = self.config
+        B, L = cfg.B, cfg.L
+        b0, b1 = self.shard()
+        Bl = b1 - b0
+        n, k = U.shape[0], U.shape[1]
+        N = Vh.shape[1]
+        dev = y.device
+        Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
+        sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
+        yl = _c64(y, (B, n))[b0:b1].contiguous()
+        xl = _flat_c64(x, B, 'x')[b0:b1].contiguous()
+        syml = _as_device_labels(symbols, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
+        idxl = _as_device_labels(indices, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
+        d, cst = cfg.dims(batch=Bl), cfg.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_vamp_workspace_bytes(C.byref(d), k, cfg.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_vamp_workspace_bytes: invalid dimensions')
+        self._ws = nat.WORKSPACE.get(dev, 'vamp_sharded', wsb)
+        r = torch.empty(Bl, N, dtype=torch.complex64, device=dev)
+        xm = torch.empty_like(r)
+        var = torch.empty(Bl, N, dtype=torch.float32, device=dev)
+        res = torch.zeros(256, dtype=torch.uint8, device=dev)      # amp_status @0, amp_counts @64
+        a = nat.AmpVampArgs()
+        a.U, a.s, a.Vh, a.y = nat.dptr(Uc, name='U'), nat.dptr(sc, torch.float32, 's'), nat.dptr(Vhc, name='Vh'), \
+            nat.dptr(yl, name='y')
+        a.k, a.max_iter, a.engine, a.gemm = k, cfg.N_Layers, nat.ENGINE_LAUNCHES, nat.GEMM_AUTO
+        a.noise_var, a.sparsity = float(self.E / SNR), float(self.sparsity)
+        a.r, a.xmmse, a.var = nat.dptr(r), nat.dptr(xm), nat.dptr(var)
+        a.status = nat.dptr(res)
+        a.ws, a.ws_bytes = nat.dptr(self._ws), self._ws.numel()
+        st = nat.stream_ptr(dev)
+        self._hook_error = None
+        nat.check(lib.amp_set_allreduce_hook(C.cast(self._hook, C.c_void_p), None), 'amp_set_allreduce_hook')
+        rc = lib.amp_vamp_run_sharded(C.byref(d), C.byref(cst), C.byref(a), B, st)
+        if self._hook_error is not None:
+            raise RuntimeError('amp_vamp_run_sharded: all-reduce hook failed') from self._hook_error
+        nat.check(rc, 'amp_vamp_run_sharded')
+        # decision on T.r (vamp.py:187) over this slice, flat indices of the whole batch
+        dwsb = lib.amp_map_decide_workspace_bytes(C.byref(d))
+        dws = nat.WORKSPACE.get(dev, 'decide_sharded', dwsb)
+        nat.check(lib.amp_map_decide_count_rows(C.byref(d), C.byref(cst), nat.dptr(r), nat.dptr(xm), nat.dptr(xl),
+                                                nat.dptr(syml), nat.dptr(idxl), self.L._ibits, b0,
+                                                nat.dptr(res) + 64, None, nat.dptr(dws), dwsb, st),
+                  'amp_map_decide_count_rows')
+        raw = res.cpu().numpy().tobytes()
+        status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
+        counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
+        merged = vector_to_counts(allreduce_counts(counts_to_vector(counts)))   # the ONE counter all-reduce
+        self.L.resolve()
+        self.L.dump()
+        self.L.last_counts, self.L.last_status = merged, status
+        self.L.record(self.L.rates_from_counts(merged), int(status.T))
+        self.last_shard = (r.view(Bl, N, 1), xm.view(Bl, N, 1), var.view(Bl, N, 1))
+        return self.L
+
 
 def read_result(res: torch.Tensor):
     """(amp_status, amp_counts) from the 256-byte result buffer (status @0, counts @64)."""

@@ -155,6 +155,34 @@ typedef struct amp_vamp_decide_args {
 } amp_vamp_decide_args;
 int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                           const amp_vamp_decide_args* dec, void* stream);
+/* `epochs` independent forwards of d->B trials each that share ONE channel (U, s, Vh) — the
+ * epochs of one `res` block of Model.simulate (vamp_model.py:55-61: the channel is redrawn only
+ * when i % res == 0) — side by side in one persistent launch.  Each epoch keeps its own
+ * batch-global scalars (mean var, max|xi|, allclose; vamp.py:85, 112, 185) and early exit, so
+ * the results equal `epochs` sequential amp_vamp_detect_count calls.  y, r, xmmse, var, x, sym,
+ * idx hold the epochs' rows back to back ([epochs * B] rows); status -> amp_status[epochs],
+ * dec->counts -> amp_counts[epochs]; workspace: amp_vamp_epochs_workspace_bytes.  Needs the
+ * persistent engine with B % 16 == 0 and epochs * B / 16 <= the device's CUs. */
+/* ---- Trial sharding across ranks (SURVEY §8(e) exact-compat mode) ----
+ * One batch of B_global trials split over ranks (rank r holds a contiguous slice of d->B rows);
+ * every per-iteration batch-global value of VAMP.forward (var.mean() vamp.py:85, the float64
+ * max|xi| shift vamp.py:112, torch.allclose vamp.py:185, and the rare path's exact values) is
+ * all-reduced through a caller-registered hook between launches, so each rank follows the
+ * trajectory of the whole-batch forward.  The hook all-reduces `count` float64 words at the
+ * device pointer `buf` in place, ordered on `stream` (e.g. an RCCL ncclAllReduce on that stream,
+ * or torch.distributed.all_reduce); it returns 0 on success.  It is called 5 times per
+ * iteration on every rank (no data-dependent calls, no host synchronisation inside). */
+enum { AMP_ALLREDUCE_SUM = 0, AMP_ALLREDUCE_MAX = 1 };
+typedef int (*amp_allreduce_fn)(void* buf, int64_t count, int32_t op, void* stream, void* ctx);
+int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx);
+/* amp_vamp_run on this rank's slice (launch engine) with the batch scalars all-reduced; workspace
+ * as amp_vamp_workspace_bytes(d, ...) for the slice.  Decide with amp_map_decide_count_rows. */
+int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t B_global,
+                         void* stream);
+
+size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs);
+int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                 const amp_vamp_decide_args* dec, int32_t epochs, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
  * launches, in milliseconds.  LAUNCHES engine: ms_out[4] = mean GEMM1 / GEMM2+denoiser /
  * reduction kernel time per executed iteration and the whole forward.  PERSISTENT engine
@@ -254,6 +282,14 @@ int amp_map_decide_count(const amp_dims* d, const amp_constellation* c, const vo
                          const void* xmmse, const void* x, const void* sym, const void* idx,
                          int32_t ibits_trunc, void* counts, void* decisions, void* ws, size_t ws_bytes,
                          void* stream);
+/* The same over rows [row0, row0 + d->B) of a larger batch (a trial-sharded rank's slice): the
+ * flat indices it compares (loss.py:105-169) are those of the whole batch, so the chosen entry's
+ * flat index is formed at section (row0 + b) * L + l; sym / idx hold this slice's labels.  The
+ * ranks' counters sum to the whole batch's. */
+int amp_map_decide_count_rows(const amp_dims* d, const amp_constellation* c, const void* xmap,
+                              const void* xmmse, const void* x, const void* sym, const void* idx,
+                              int32_t ibits_trunc, int64_t row0, void* counts, void* decisions, void* ws,
+                              size_t ws_bytes, void* stream);
 size_t amp_map_decide_workspace_bytes(const amp_dims* d);
 /* Same counters with Loss.random_decision (loss.py:252-280, generator_mode='random'): per
  * channel use the Na largest |x_m| (NaN largest; exact ties by larger index), each decided to

@@ -165,12 +165,13 @@ def _logits(r: np.ndarray, tau, cfg: OracleConfig, B: int) -> np.ndarray:
     return (u.astype(np.complex128)[..., None] * np.conj(sym)[None, None, None, :]).real
 
 
-def block_denoise(r: np.ndarray, tau, cfg: OracleConfig):
+def block_denoise(r: np.ndarray, tau, cfg: OracleConfig, G=None):
     """Posterior mean and variance of the section-sparse prior.
 
     VAMP ``segmented_denoiser`` (vamp.py:96-119): ``tau`` is the 0-dim sigma2.
     BAMP ``segmented_denoiser`` (bamp.py:66-77): pass ``tau = cov/2`` (per element).
-    Float64 with the batch-global ``max |xi|`` shift (vamp.py:112).
+    Float64 with the batch-global ``max |xi|`` shift (vamp.py:112); ``G`` overrides the shift
+    (a trial-sharded batch: the max over every rank's slice).
     Returns (xmmse complex64 [B,N], var float32 [B,N]).
     """
     B = r.shape[0]
@@ -179,7 +180,7 @@ def block_denoise(r: np.ndarray, tau, cfg: OracleConfig):
     sym = cfg.symbols
     xi = _logits(r, tau, cfg, B)
     with np.errstate(under='ignore', invalid='ignore', divide='ignore', over='ignore'):
-        eta = np.exp(xi - np.abs(xi).max())
+        eta = np.exp(xi - (np.abs(xi).max() if G is None else G))
         zm = eta.sum(axis=-1)                          # [B,L,M]
         z = zm.sum(axis=2, keepdims=True)              # [B,L,1]
         xm = (sym * eta).sum(axis=-1) / z              # vamp.py:114
@@ -259,6 +260,72 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
             trace.append(dict(r=r.copy(), xmmse=xm.copy(), var=var.copy(), alpha=alpha,
                               sigma2=sigma2, dxdr=dxdr, sigma2_tilde=s2t, r_tilde=rt.copy()))
         if allclose_f32(var, prev):                               # vamp.py:185
+            break
+    return dict(r=r, xmmse=xm, var=var, T=t + 1)
+
+
+def vamp_detect_sharded(U, s, Vh, y_local, SNR: float, cfg: OracleConfig, B_global: int, allreduce):
+    """vamp_detect on ONE rank's slice of a trial-sharded batch (SURVEY §8(e) exact-compat
+    mode; the build's amp_vamp_run_sharded): the batch-global values of vamp.py:85
+    (var.mean()), vamp.py:112 (max |xi|) and vamp.py:185 (allclose) come from
+    ``allreduce(np.float64 array, 'sum' | 'max')`` over the ranks, so every rank follows the
+    whole-batch trajectory (up to the float64 summation order of the mean).  A NaN max |xi| is
+    sent as +inf: exp(xi - inf) makes every section 0/0 = NaN, as the NaN shift does."""
+    U = np.asarray(U, C64); Vh = np.asarray(Vh, C64); y = np.asarray(y_local, C64)
+    s = np.asarray(s, F32)
+    B = y.shape[0]
+    E = cfg.Na / cfg.Nr
+    p = cfg.Na / cfg.Nt
+    noise_var = E / SNR
+    Uh = np.conj(U).T
+    Vt = np.conj(Vh)
+    s2 = (s * s).astype(F32)
+    ytil = (y @ ((s[:, None] * Uh).astype(C64)).T).astype(C64)
+    N = Vh.shape[1]
+    r = np.zeros((B, N), C64)
+    var = np.ones((B, N), F32)
+    rt = np.full((B, N), F32(p), dtype=C64)
+    s2t = p ** 2 * (1 - p) + (1 - p) ** 2 * p
+    eta = s.shape[0] / N
+    xm = None
+    t = 0
+    for t in range(cfg.N_Layers):
+        prev = var
+        first = isinstance(s2t, float)
+        vr = F32(noise_var / s2t) if first else F32(_recip(s2t) * F32(noise_var))
+        q = (rt @ Vh.T).astype(C64)
+        scale = _recip(s2 + vr)
+        xt = (scale * (ytil + vr * q)).astype(C64)
+        varL = F32(F32(np.sum(scale, dtype=np.float64) / scale.size) * F32(noise_var))
+        xt = ((xt - q) @ Vt + rt).astype(C64)
+        if first:
+            xtv = F32(F32(eta) * varL + F32((1 - eta) * s2t))
+            alpha = F32(xtv / F32(s2t))
+            s2t32 = F32(s2t)
+        else:
+            xtv = F32(F32(eta) * varL + F32(F32(1 - eta) * s2t))
+            alpha = F32(xtv / s2t)
+            s2t32 = s2t
+        alpha = _clamp(alpha, VAR_RATIO_MIN, VAR_RATIO_MAX)
+        r = _div_real(xt - alpha * rt, F32(1) - alpha)
+        sigma2 = _clamp(F32(F32(alpha / (F32(1) - alpha)) * s2t32), VAR_MIN, VAR_MAX)
+        with np.errstate(invalid='ignore'):
+            g = np.abs(_logits(r, sigma2, cfg, B)).max()
+        g = np.float64(np.inf) if not np.isfinite(g) else g
+        G = allreduce(np.array([g]), 'max')[0]
+        xm, var = block_denoise(r, sigma2, cfg, G=G)
+        # torch.allclose over the whole batch (vamp.py:185): the count of not-close elements
+        with np.errstate(invalid='ignore', over='ignore'):
+            nxt, prv = var.astype(F32), prev.astype(F32)
+            actual = np.abs(nxt - prv)
+            close = (nxt == prv) | (np.isfinite(actual) & (actual <= ALLCLOSE_ATOL + np.abs(ALLCLOSE_RTOL * prv)))
+        tot = allreduce(np.array([np.sum(var, dtype=np.float64), float(np.sum(~close))]), 'sum')
+        mean_var = F32(tot[0] / (B_global * N))
+        dxdr = _clamp(F32(mean_var / sigma2), VAR_RATIO_MIN, VAR_RATIO_MAX)
+        ns = _recip(F32(1) - dxdr)
+        rt = ((xm - dxdr * r) * ns).astype(C64)
+        s2t = _clamp(F32(F32(sigma2 * dxdr) * ns), VAR_MIN, VAR_MAX)
+        if tot[1] == 0:
             break
     return dict(r=r, xmmse=xm, var=var, T=t + 1)
 
@@ -614,7 +681,7 @@ def shrink_sw_ook(r, cov, B, L, M):
     return x.reshape(B, L * M).astype(C64), var.reshape(B, L * M)
 
 
-__all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect', 'vamp2_detect',
+__all__ = ['OracleConfig', 'constellation', 'block_denoise', 'scamp_denoise', 'vamp_detect', 'vamp_detect_sharded', 'vamp2_detect',
            'vamp2_denoise',
            'bamp_detect', 'scamp_detect', 'map_decision', 'error_rates', 'loss_dict', 'allclose_f32',
            'LOSS_KEYS', 'VAR_RATIO_MIN', 'VAR_RATIO_MAX', 'VAR_MIN', 'VAR_MAX',

@@ -1,0 +1,120 @@
+"""GPU: side-by-side epochs (amp_vamp_detect_count_epochs, VAMP.forward_epochs).
+
+E epochs that share one channel (one `res` block of Model.simulate, vamp_model.py:55-61) run
+in ONE persistent launch, each with its own batch-global scalars and early exit.  The bar is
+bit-identity with E sequential forwards: same T, same counters and the same r / xmmse / var
+bits (the per-epoch granule sweep reduces in the same fixed order as a one-epoch launch).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(Nt, Na, Nr, B, alphabet, device='cuda', iterations=20):
+    from config import Config
+    return Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iterations, alphabet=alphabet,
+                  channel_profile='uniform', channel_truncation='tail', device=device)
+
+
+def _epochs(cfg, E, ebn0, seed, scales=None):
+    """One channel and E epochs of messages + noise in the reference's call order (host replica)."""
+    from channel import Channel
+    from data import Data
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    c = _cfg(cfg.Nt, cfg.Na, cfg.Nr, cfg.B, cfg.alphabet, device='cpu', iterations=cfg.N_Layers)
+    ch, da = Channel(c), Data(c)
+    _, A = ch.generate_as_sparc()
+    U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+    SNR = c.snr(ebn0)
+    eps = []
+    for e in range(E):
+        x, sym, idx = da.generate_message()
+        y = A @ x + ch.awgn(SNR)
+        if scales is not None:
+            y = y * scales[e]
+        eps.append((x, sym, idx, y))
+    return (U, s, Vh), SNR, eps
+
+
+def _run_both(cfg, chan, SNR, eps, device):
+    from vamp import VAMP
+    mv = lambda t: t.to(device).contiguous()  # noqa: E731
+    U, s, Vh = (mv(t) for t in chan)
+    det = VAMP(cfg)
+    seq = []
+    for x, sym, idx, y in eps:
+        L = det(U, s, Vh, mv(y), SNR, mv(x), sym, idx)
+        seq.append((dict(L.loss), L.last_status, det.last.r.clone(), det.last.xmmse.clone(), det.last.var.clone()))
+    grp = det.forward_epochs(U, s, Vh, [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
+                             [e[1] for e in eps], [e[2] for e in eps])
+    return det, seq, grp
+
+
+@pytest.mark.parametrize('alphabet,ebn0', [('16QAM', 8.0), ('16QAM', 20.0), ('QPSK', 4.0), ('QPSK', 12.0)])
+def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0):
+    cfg = _cfg(64, 4, 128, 1024, alphabet)
+    chan, SNR, eps = _epochs(cfg, 4, ebn0, seed=3)
+    det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
+    r, xm, var = det.last_epochs
+    assert len(grp) == 4
+    for e, (ls, st, r0, x0, v0) in enumerate(seq):
+        lg = grp[e].loss
+        assert int(lg['T']) == int(ls['T']), (e, lg['T'], ls['T'])
+        assert grp[e].last_status.nan_state == st.nan_state
+        assert lg.keys() == ls.keys()
+        for k in ls:
+            assert np.array_equal(np.asarray(lg[k]), np.asarray(ls[k]), equal_nan=True), (e, k)
+        assert torch.equal(r[e].view(torch.int32), r0.view(torch.int32)), e
+        assert torch.equal(xm[e].view(torch.int32), x0.view(torch.int32)), e
+        assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), e
+
+
+def test_epochs_independent_rare_path(device):
+    """One epoch driven into the exact float64 rare path (its y scaled up: logits beyond the
+    float64 range of the global shift) while the others are not: the per-epoch barrier counters
+    keep the groups apart and every epoch still equals its sequential forward."""
+    cfg = _cfg(64, 4, 128, 1024, '16QAM')
+    chan, SNR, eps = _epochs(cfg, 3, 14.0, seed=5, scales=[1.0, 40.0, 1.0])
+    det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
+    r, xm, var = det.last_epochs
+    for e, (ls, st, r0, x0, v0) in enumerate(seq):
+        assert int(grp[e].loss['T']) == int(ls['T']), e
+        assert grp[e].last_status.nan_state == st.nan_state, e
+        assert float(grp[e].loss['ser']) == float(ls['ser']), e
+        assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), e
+
+
+def test_epochs_cfg4_two(device):
+    """Two cfg4 epochs would need 512 workgroups > 256 CUs: refused (AMP_E_ARG), no fallback."""
+    import amp_native as nat
+    cfg = _cfg(256, 8, 512, 4096, '16QAM')
+    from vamp import VAMP
+    det = VAMP(cfg)
+    assert not det.epochs_eligible(512, 256, 2)
+    assert det.epochs_eligible(512, 256, 1)
+    z = torch.zeros(4096, 256, dtype=torch.complex64, device=device)
+    with pytest.raises(nat.AmpError):
+        det.forward_epochs(torch.zeros(512, 256, dtype=torch.complex64, device=device),
+                           torch.ones(256, device=device), torch.zeros(256, 256, dtype=torch.complex64, device=device),
+                           [torch.zeros(4096, 512, dtype=torch.complex64, device=device)] * 2, 10.0, [z, z],
+                           [np.zeros(4096 * 8, np.int64)] * 2, [np.zeros(4096 * 8, np.int64)] * 2)
+
+
+def test_simulate_group_epochs_identical(device, tmp_path):
+    """Model.simulate(res=4) with group_epochs=True writes the same points as the per-epoch loop."""
+    from model import Model
+    cfg = _cfg(64, 4, 128, 1024, 'QPSK')
+    outs = []
+    for grouped in (False, True):
+        m = Model(cfg, 'vamp', path=str(tmp_path / f'g{int(grouped)}'), seed=11, group_epochs=grouped)
+        if grouped:
+            assert m.group_cap >= 4
+        outs.append(m.simulate(epochs=8, start=2.0, final=4.0, step=2.0, res=4))
+    assert len(outs[0]) == len(outs[1])
+    for a, b in zip(*outs):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k

@@ -1,0 +1,152 @@
+"""Trial sharding across ranks (SURVEY §8(e) exact-compat mode) on the CPU, gloo, world size 2-3.
+
+* The decomposition the build's amp_vamp_run_sharded implements, restated in the oracle
+  (vamp_detect_sharded): each rank holds a slice of ONE batch and all-reduces the batch-global
+  values of every iteration (max |xi| for vamp.py:112, sum var and the not-close count for
+  vamp.py:85 / 185).  Every rank must follow the whole-batch trajectory: same T, r equal to the
+  whole-batch oracle's rows, and the merged Loss dict equal to the whole-batch one.
+* The host side of ShardedVAMP's all-reduce hook (amp_allreduce_fn) on gloo: the float64 words
+  at an address inside the workspace are reduced in place (SUM / MAX).
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import golden_io as gio
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _case(name):
+    if name.startswith('g1:'):
+        c = gio.g1_cases()[name[3:]]
+        return dict(Nt=int(c.Nt), Na=int(c.Na), Nr=int(c.Nr), B=int(c.B), alphabet=str(c.alphabet),
+                    iters=int(c.iters), U=c.U, s=c.s, Vh=c.Vh, y=c.y, SNR=float(c.SNR), x=c.x, sym=c.sym, idx=c.idx)
+    # synthetic cfg2-shaped case (N = 64, n = 128, 16-QAM / QPSK) from the host replica
+    from channel import Channel
+    from config import Config
+    from data import Data
+    alph, ebn0, B = name.split(':')[1:]
+    cfg = Config(64, 4, 128, 1, 1, batch=int(B), generator_mode='sparc', iterations=20, alphabet=alph,
+                 channel_profile='uniform', channel_truncation='tail', device='cpu')
+    np.random.seed(7)
+    torch.manual_seed(7)
+    ch, da = Channel(cfg), Data(cfg)
+    _, A = ch.generate_as_sparc()
+    U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+    x, sym, idx = da.generate_message()
+    SNR = cfg.snr(float(ebn0))
+    y = A @ x + ch.awgn(SNR)
+    return dict(Nt=64, Na=4, Nr=128, B=int(B), alphabet=alph, iters=20, U=U.numpy(), s=s.numpy(), Vh=Vh.numpy(),
+                y=y.numpy()[..., 0], SNR=SNR, x=x.numpy()[..., 0], sym=np.asarray(sym), idx=np.asarray(idx))
+
+
+def _worker(rank, world, port, out, names):
+    torch.distributed.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                                         world_size=world)
+    try:
+        from oracle import OracleConfig, vamp_detect_sharded
+
+        def allreduce(v, op):
+            t = torch.as_tensor(np.asarray(v, dtype=np.float64))
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM if op == 'sum'
+                                         else torch.distributed.ReduceOp.MAX)
+            return t.numpy()
+
+        res = {}
+        for name in names:
+            c = _case(name)
+            B = c['B']
+            b0, b1 = rank * B // world, (rank + 1) * B // world
+            ocfg = OracleConfig(c['Nt'], c['Na'], c['Nr'], B=B, alphabet=c['alphabet'], iterations=c['iters'])
+            o = vamp_detect_sharded(c['U'], c['s'], c['Vh'], np.asarray(c['y']).reshape(B, -1)[b0:b1], c['SNR'],
+                                    ocfg, B, allreduce)
+            np.save(os.path.join(out, f'{name.replace(":", "_")}_r{rank}.npy'), o['r'])
+            res[name] = int(o['T'])
+        with open(os.path.join(out, f'T{rank}.json'), 'w') as f:
+            json.dump(res, f)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+NAMES = ['g1:vamp_QPSK_6_0', 'g1:vamp_16QAM_20_0', 'g1:vamp_16QAM_30_1', 'g1:vamp_QPSK_0_1', 'syn:QPSK:4:96', 'syn:16QAM:8:96',
+         'syn:16QAM:16:96']
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_oracle_trial_shard_equals_whole_batch(tmp_path, world):
+    from oracle import OracleConfig, loss_dict, vamp_detect
+    names = [n for n in NAMES if not n.startswith('g1:') or n[3:] in gio.g1_cases()]
+    assert len(names) >= 4
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), names), nprocs=world, join=True)
+    Ts = [json.load(open(tmp_path / f'T{r}.json')) for r in range(world)]
+    for name in names:
+        c = _case(name)
+        B = c['B']
+        ocfg = OracleConfig(c['Nt'], c['Na'], c['Nr'], B=B, alphabet=c['alphabet'], iterations=c['iters'])
+        whole = vamp_detect(c['U'], c['s'], c['Vh'], np.asarray(c['y']).reshape(B, -1), c['SNR'], ocfg)
+        for r in range(world):
+            assert Ts[r][name] == whole['T'], (name, r, Ts[r][name], whole['T'])
+        rs = np.concatenate([np.load(tmp_path / f'{name.replace(":", "_")}_r{r}.npy') for r in range(world)])
+        fin = np.isfinite(whole['r'])
+        assert np.array_equal(np.isfinite(rs), fin), name
+        # r: equal on the small golden cases; on the cfg2-shaped ones the slices' BLAS GEMMs round
+        # differently from the whole batch's, and at 16-QAM / 16 dB (no convergence within 20
+        # iterations) that rounding moves most of r by > 1e-3 while T and the metrics agree: the
+        # same sensitivity the reference shows against any other GEMM order
+        if name.startswith('g1:'):
+            err = np.max(np.abs(rs[fin] - whole['r'][fin])) if fin.any() else 0.0
+            assert err <= 1e-6, (name, err)
+        xm = np.asarray(c['x']).reshape(B, -1)
+        a = loss_dict(rs, whole['xmmse'], xm, c['sym'], c['idx'], whole['T'], ocfg)
+        b = loss_dict(whole['r'], whole['xmmse'], xm, c['sym'], c['idx'], whole['T'], ocfg)
+        for k in ('ver', 'ser', 'fer', 'ier'):
+            assert abs(float(a[k]) - float(b[k])) <= 1e-3, (name, k, a[k], b[k])
+
+
+def _hook_worker(rank, world, port, out):
+    torch.distributed.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                                         world_size=world)
+    try:
+        import amp_native as nat
+        from config import Config
+        from vamp import ShardedVAMP
+        cfg = Config(16, 2, 32, 1, 1, batch=8, generator_mode='sparc', iterations=5, alphabet='QPSK',
+                     channel_profile='uniform', channel_truncation='tail', device='cpu')
+        det = ShardedVAMP(cfg)
+        ws = torch.zeros(256, dtype=torch.uint8)
+        det._ws = ws
+        w = ws[64:96].view(torch.float64)
+        w[:] = torch.tensor([1.0 + rank, -2.0 * rank, float(rank), 7.0], dtype=torch.float64)
+        # through the ctypes function pointer the C driver calls
+        fn = nat.ALLREDUCE_FN(det._allreduce)
+        rc1 = fn(ws.data_ptr() + 64, 2, nat.ALLREDUCE_SUM, None, None)
+        rc2 = fn(ws.data_ptr() + 80, 2, nat.ALLREDUCE_MAX, None, None)
+        rc3 = fn(ws.data_ptr() + 250, 2, nat.ALLREDUCE_SUM, None, None)    # outside the workspace: error
+        b0, b1 = det.shard()
+        with open(os.path.join(out, f'h{rank}.json'), 'w') as f:
+            json.dump({'w': w.tolist(), 'rc': [rc1, rc2, rc3], 'slice': [b0, b1],
+                       'err': repr(det._hook_error)}, f)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_sharded_hook_gloo(tmp_path):
+    world = 2
+    mp.spawn(_hook_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [json.load(open(tmp_path / f'h{r}.json')) for r in range(world)]
+    for r, o in enumerate(outs):
+        assert o['rc'][:2] == [0, 0] and o['rc'][2] == 1 and 'outside the workspace' in o['err']
+        assert o['w'] == [1.0 + 2.0, 0.0 - 2.0, 1.0, 7.0]       # SUM of words 0-1, MAX of words 2-3
+        assert o['slice'] == [r * 8 // world, (r + 1) * 8 // world]

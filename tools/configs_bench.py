@@ -37,7 +37,10 @@ CFGS = {
     'cfg3-launches': ('scamp', 128, 8, 256, 4096, '16QAM', 20, 8.0),   # the launch engine, for comparison
     'cfg3-qpsk': ('scamp', 128, 8, 256, 4096, 'QPSK', 20, 2.0),
     'cfg4': ('vamp', 256, 8, 512, 4096, '16QAM', 20, 8.0),
+    # cfg2 with the 4 epochs of one res = 4 block side by side (VAMP.forward_epochs: 256 workgroups)
+    'cfg2-epochs4': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
 }
+EPOCHS = {'cfg2-epochs4': 4}
 
 
 def main(steps=50, warmup=30, only=None):
@@ -56,6 +59,35 @@ def main(steps=50, warmup=30, only=None):
         y = A @ x + ch.awgn(SNR)
         cfg.device = 'cuda'
         mv = lambda t: t.to(dev).contiguous()  # noqa: E731
+        E = EPOCHS.get(name, 1)
+        if E > 1:
+            eps = [(x, sym, idx, y)]
+            for _ in range(E - 1):
+                xe, se, ie = da.generate_message()
+                eps.append((xe, se, ie, A @ xe + ch.awgn(SNR)))
+            U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+            det = VAMP(cfg)
+            ea = (mv(U), mv(s), mv(Vh), [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
+                  [e[1] for e in eps], [e[2] for e in eps])
+            flop = 16.0 * Nt * min(Nt, Nr)
+            for _ in range(warmup):
+                Ls = det.forward_epochs(*ea)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                Ls = det.forward_epochs(*ea)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+            Ts = [int(L.loss['T']) for L in Ls]
+            tf = B * sum(Ts) * flop / (ms * 1e-3) / 1e12
+            print(json.dumps({'config': name, 'algo': algo, 'engine': 'persistent (side-by-side epochs)',
+                              'epochs_per_launch': E, 'Nt': Nt, 'Nr': Nr, 'Na': Na, 'alphabet': alph, 'B': B,
+                              'EbN0': ebn0, 'T': Ts, 'ser': [float(L.loss['ser']) for L in Ls],
+                              'ms_per_launch': round(ms, 4), 'ms_per_epoch': round(ms / E, 4),
+                              'symbol_vectors_per_s': E * B / (ms * 1e-3),
+                              'trial_iterations_per_s': B * sum(Ts) / (ms * 1e-3), 'achieved_TFLOPs': round(tf, 2),
+                              'mfma_frac_incl_decision': round(tf / PEAK_TF, 4)}), flush=True)
+            continue
         if algo == 'vamp':
             U, s, Vh = torch.linalg.svd(A, full_matrices=False)
             det, args = VAMP(cfg), (mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
