@@ -138,13 +138,37 @@ __device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1
 // Batch scalars of iteration t (vamp.py:66-82) from sigma2_tilde; t == 0 uses the
 // Tracker's Python-float sigma2_tilde (vamp.py:26).  Called by one workgroup.
 // ---------------------------------------------------------------------------
-__device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it) {
+// This lane's s^2 (vamp.py:17) at i = lane + 64 j, held in registers by the persistent engine for
+// the whole forward (k <= 256), so the per-iteration LMMSE sum reads no memory.
+struct S2Lane {
+    float v[4];
+};
+__device__ inline S2Lane s2_lane(const VampK& P) {
+    S2Lane a;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = lane + 64 * j;
+        a.v[j] = i < P.k ? P.s[i] * P.s[i] : 0.f;
+    }
+    return a;
+}
+
+__device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t64, float s2t, float* lds, VampIter& it,
+                                          const S2Lane* sl = nullptr) {
     const float vr = first ? (float)(P.noise_var / s2t64) : (1.0f / s2t) * (float)P.noise_var;   // vamp.py:66
     // every wave sums all k terms in the same order (no LDS round trip, no barrier): the
     // workgroup's waves hold bit-identical scalars
     (void)lds;
     double ss = 0.0;
-    for (int i = threadIdx.x & 63; i < P.k; i += 64) ss += (double)(1.0f / (P.s[i] * P.s[i] + vr));  // vamp.py:17, 68
+    if (sl) {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (lane + 64 * j < P.k) ss += (double)(1.0f / (sl->v[j] + vr));                        // vamp.py:17, 68
+    } else {
+        for (int i = threadIdx.x & 63; i < P.k; i += 64) ss += (double)(1.0f / (P.s[i] * P.s[i] + vr));  // vamp.py:17, 68
+    }
     ss = group_sum(ss, 64);
     const float varL = (float)(ss / (double)P.k) * (float)P.noise_var;                         // vamp.py:71
     const double eta = (double)P.k / (double)P.N;                                              // vamp.py:28
@@ -168,14 +192,14 @@ __device__ inline void vamp_lmmse_scalars(const VampK& P, bool first, double s2t
 
 // The record that drives iteration 0 (vamp.py:22-26, 66-82 with the Tracker's Python-float
 // sigma2_tilde).  Called uniformly by every thread of one workgroup.
-__device__ inline VampIter vamp_first_iter(const VampK& P, float* lds) {
+__device__ inline VampIter vamp_first_iter(const VampK& P, float* lds, const S2Lane* sl = nullptr) {
     VampIter it;
     it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0; it.G = 0.0;
     it.pad1[0] = it.pad1[1] = it.pad1[2] = 0.f;
     it.dxdr_prev = 0.f;   // r~ = (xmmse - 0 * r) * 1 = sparsity at t = 0 (vamp.py:25)
     it.ns_prev = 1.f;
     const double p = P.sparsity;
-    vamp_lmmse_scalars(P, true, p * p * (1 - p) + (1 - p) * (1 - p) * p, 0.f, lds, it);   // vamp.py:26
+    vamp_lmmse_scalars(P, true, p * p * (1 - p) + (1 - p) * (1 - p) * p, 0.f, lds, it, sl);   // vamp.py:26
     return it;
 }
 
@@ -183,7 +207,7 @@ __device__ inline VampIter vamp_first_iter(const VampK& P, float* lds) {
 // record when allclose held (vamp.py:185-186), else the scalars of vamp.py:85-94 and 66-82.
 // Called uniformly by every thread of one workgroup (vamp_lmmse_scalars reduces over k).
 __device__ inline VampIter vamp_advance(const VampK& P, const VampIter& cur, const PartAcc& pa, int fixed, int t,
-                                        float* lds) {
+                                        float* lds, const S2Lane* sl = nullptr) {
     VampIter nx;
     nx.stopped = 0; nx.T = 0; nx.fixed = fixed; nx.fixed_all = (fixed < 0) ? 1 : 0; nx.G = pa.maxabs;
     nx.pad1[0] = nx.pad1[1] = nx.pad1[2] = 0.f;
@@ -200,7 +224,7 @@ __device__ inline VampIter vamp_advance(const VampK& P, const VampIter& cur, con
         const float s2t = clampf_t((cur.sigma2 * dxdr) * ns, AMP_VAR_MIN, AMP_VAR_MAX);              // vamp.py:92-94
         nx.dxdr_prev = dxdr;
         nx.ns_prev = ns;
-        vamp_lmmse_scalars(P, false, 0.0, s2t, lds, nx);
+        vamp_lmmse_scalars(P, false, 0.0, s2t, lds, nx, sl);
     }
     return nx;
 }
@@ -249,6 +273,7 @@ struct PDenoisePolicy {
 constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs = 1);
+int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu);
 bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);

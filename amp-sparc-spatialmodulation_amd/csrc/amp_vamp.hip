@@ -747,6 +747,11 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
     return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 
+int amp_vamp_max_epochs(const amp_dims* d, int32_t k) {
+    if (!d || k <= 0 || d->B <= 0) return 0;
+    return vamp_persist_max_epochs(d, k, device_cu_count());
+}
+
 size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs) {
     if (!d || k <= 0 || max_iter <= 0 || epochs < 1 || (long)d->B * epochs > (1L << 30)) return 0;
     amp_dims de = *d;
@@ -761,7 +766,8 @@ int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, 
     const int ncu = device_cu_count();
     AMP_REQUIRE(a && a->engine != AMP_ENGINE_LAUNCHES && vamp_persist_eligible(d, a->k, ncu, epochs),
                 "amp_vamp_detect_count_epochs: needs the persistent engine (k == N in {64, 128, 256}, M <= 64, "
-                "B %% 16 == 0 when epochs > 1, epochs * ceil(B/16) = %d <= %d CUs)", epochs * cdiv(d->B, PBM), ncu);
+                "B %% 16 == 0 when epochs > 1, epochs <= amp_vamp_max_epochs = %d)",
+                vamp_persist_max_epochs(d, a ? a->k : 0, ncu));
     amp_dims de = *d;
     de.B = d->B * epochs;
     VampK P;

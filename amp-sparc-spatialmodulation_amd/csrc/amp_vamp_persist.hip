@@ -64,9 +64,25 @@ bool vamp_persist_x3_fits(int N, int k, int L) {
     return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
 }
 
+// One persistent workgroup per CU.  Round 2 tried two per CU at N = 64 (launch bounds for 256
+// VGPRs, 2 x 256 workgroups for 8 cfg2 epochs): the launch ran, but the results of co-resident
+// epochs were not reproducible run to run (every r element of most epochs off in the last bits,
+// tools/epochs_diag.py), so the engine stays at one workgroup per CU.
+static int persist_wg_cap(int) { return 1; }
+
+int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu) {
+    if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return 0;
+    if ((size_t)playout(d->N, k, d->L).total * 4 + 2048 > 160 * 1024) return 0;
+    const int wpe = cdiv(d->B, PBM);
+    if (wpe > ncu) return 0;
+    if (d->B % PBM != 0) return 1;
+    return std::max(1, persist_wg_cap(d->N) * ncu / wpe);
+}
+
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
-    if (epochs < 1 || (epochs > 1 && d->B % PBM != 0) || (long)epochs * cdiv(d->B, PBM) > ncu) return false;
+    if (epochs < 1 || (epochs > 1 && d->B % PBM != 0)) return false;
+    if (cdiv(d->B, PBM) > ncu || (long)epochs * cdiv(d->B, PBM) > (long)persist_wg_cap(d->N) * ncu) return false;
     return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
 }
 

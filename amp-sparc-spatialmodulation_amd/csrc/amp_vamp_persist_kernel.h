@@ -247,7 +247,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
             }
         }
     }
-    VampIter cur = vamp_first_iter(P, scr);   // vamp.py:26, 66-82 at t = 0
+    const S2Lane s2l = s2_lane(P);            // s^2 in registers for the per-iteration LMMSE sum
+    VampIter cur = vamp_first_iter(P, scr, &s2l);   // vamp.py:26, 66-82 at t = 0
     // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
     {
         const float p = (float)P.sparsity;
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
             g.maxabs = G;
             fixed = (int)c;
         }
-        nx = vamp_advance(P, cur, g, fixed, t, scr);
+        nx = vamp_advance(P, cur, g, fixed, t, scr, &s2l);
         stamp(t, 7);
         if (nx.stopped || t + 1 == P.max_iter) break;
         cur = nx;

@@ -117,11 +117,7 @@ class Model(nn.Module):
             if detector != 'vamp' or not hasattr(self.amp, 'forward_epochs'):
                 raise ValueError('group_epochs: side-by-side epochs are built for the VAMP detector')
             N, n = config.Nt * config.Lin, config.Nr * config.Lout
-            k = min(n, N)
-            cap = 1
-            while self.amp.epochs_eligible(n, k, cap + 1):
-                cap += 1
-            self.group_cap = cap if self.amp.epochs_eligible(n, k, 1) else 0
+            self.group_cap = self.amp.max_epochs(min(n, N))
 
     # one epoch, in the reference's random-call order (vamp_model.py:55-61)
     def _epoch(self, SNR: float, new_channel: bool):

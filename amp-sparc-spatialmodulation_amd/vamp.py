@@ -265,17 +265,20 @@ class VAMP(LazyResult, nn.Module):
         self.last = T
         return self.L
 
-    def epochs_eligible(self, n: int, k: int, epochs: int) -> bool:
-        """Whether `epochs` forwards of this config fit ONE persistent launch
-        (amp_vamp_detect_count_epochs): persistent-engine shape, B % 16 == 0 and
-        epochs * B / 16 <= the device's CUs."""
-        if self.config.mode != 'sparc' or epochs < 1 or (epochs > 1 and self.config.B % 16):
-            return False
+    def max_epochs(self, k: int) -> int:
+        """The most epochs of this config ONE persistent launch holds (amp_vamp_max_epochs:
+        one workgroup of 16 trials per CU, two at N = 64; 0 when not persistent-eligible)."""
+        if self.config.mode != 'sparc':
+            return 0
         d = self.config.dims()
         if nat.lib().amp_vamp_select_engine(C.byref(d), k, self.engine) != nat.ENGINE_PERSISTENT:
-            return False
-        return epochs * (-(-self.config.B // 16)) <= torch.cuda.get_device_properties(
-            torch.cuda.current_device()).multi_processor_count
+            return 0
+        return int(nat.lib().amp_vamp_max_epochs(C.byref(d), k))
+
+    def epochs_eligible(self, n: int, k: int, epochs: int) -> bool:
+        """Whether `epochs` forwards of this config fit ONE persistent launch
+        (amp_vamp_detect_count_epochs)."""
+        return 1 <= epochs <= self.max_epochs(k)
 
     def forward_epochs(self, U, s, Vh, ys, SNR: float, xs, symbols, indices) -> list:
         """E epochs that share ONE channel (U, s, Vh) — the epochs of one `res` block of

@@ -162,7 +162,8 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
  * the results equal `epochs` sequential amp_vamp_detect_count calls.  y, r, xmmse, var, x, sym,
  * idx hold the epochs' rows back to back ([epochs * B] rows); status -> amp_status[epochs],
  * dec->counts -> amp_counts[epochs]; workspace: amp_vamp_epochs_workspace_bytes.  Needs the
- * persistent engine with B % 16 == 0 and epochs * B / 16 <= the device's CUs. */
+ * persistent engine with B % 16 == 0 and epochs <= amp_vamp_max_epochs (one workgroup of 16
+ * trials per CU). */
 /* ---- Trial sharding across ranks (SURVEY §8(e) exact-compat mode) ----
  * One batch of B_global trials split over ranks (rank r holds a contiguous slice of d->B rows);
  * every per-iteration batch-global value of VAMP.forward (var.mean() vamp.py:85, the float64
@@ -181,6 +182,8 @@ int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
                          void* stream);
 
 size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs);
+/* The most epochs of d->B trials one launch holds on this device (0: not persistent-eligible). */
+int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                  const amp_vamp_decide_args* dec, int32_t epochs, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the

@@ -53,13 +53,16 @@ def _run_both(cfg, chan, SNR, eps, device):
     return det, seq, grp
 
 
-@pytest.mark.parametrize('alphabet,ebn0', [('16QAM', 8.0), ('16QAM', 20.0), ('QPSK', 4.0), ('QPSK', 12.0)])
-def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0):
+@pytest.mark.parametrize('alphabet,ebn0,E', [('16QAM', 8.0, 4), ('16QAM', 20.0, 4), ('QPSK', 4.0, 4),
+                                             ('QPSK', 12.0, 4), ('QPSK', 6.0, 4), ('16QAM', 14.0, 2)])
+def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0, E):
     cfg = _cfg(64, 4, 128, 1024, alphabet)
-    chan, SNR, eps = _epochs(cfg, 4, ebn0, seed=3)
+    chan, SNR, eps = _epochs(cfg, E, ebn0, seed=3)
     det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
+    # one workgroup of 16 trials per CU: 4 epochs of 64 workgroups on 256 CUs
+    assert det.max_epochs(64) == torch.cuda.get_device_properties(0).multi_processor_count // 64
     r, xm, var = det.last_epochs
-    assert len(grp) == 4
+    assert len(grp) == E
     for e, (ls, st, r0, x0, v0) in enumerate(seq):
         lg = grp[e].loss
         assert int(lg['T']) == int(ls['T']), (e, lg['T'], ls['T'])
@@ -94,7 +97,7 @@ def test_epochs_cfg4_two(device):
     from vamp import VAMP
     det = VAMP(cfg)
     assert not det.epochs_eligible(512, 256, 2)
-    assert det.epochs_eligible(512, 256, 1)
+    assert det.epochs_eligible(512, 256, 1) and det.max_epochs(256) == 1
     z = torch.zeros(4096, 256, dtype=torch.complex64, device=device)
     with pytest.raises(nat.AmpError):
         det.forward_epochs(torch.zeros(512, 256, dtype=torch.complex64, device=device),

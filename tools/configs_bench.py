@@ -59,12 +59,14 @@ def main(steps=50, warmup=30, only=None):
         y = A @ x + ch.awgn(SNR)
         cfg.device = 'cuda'
         mv = lambda t: t.to(dev).contiguous()  # noqa: E731
+        lab = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int64)).to(dev)  # noqa: E731  (resident in HBM)
+        sym, idx = lab(sym), lab(idx)
         E = EPOCHS.get(name, 1)
         if E > 1:
             eps = [(x, sym, idx, y)]
             for _ in range(E - 1):
                 xe, se, ie = da.generate_message()
-                eps.append((xe, se, ie, A @ xe + ch.awgn(SNR)))
+                eps.append((xe, lab(se), lab(ie), A @ xe + ch.awgn(SNR)))
             U, s, Vh = torch.linalg.svd(A, full_matrices=False)
             det = VAMP(cfg)
             ea = (mv(U), mv(s), mv(Vh), [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
