@@ -180,7 +180,8 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
         f32x4 cr1[NC1], ci1[NC1];
         if constexpr (X3) {
             for (int e = tid; e < SPB * (N >> 3); e += PWG) {   // x rows -> bf16 planes, 8 per item
-                const int row = e / (N >> 3), j0 = 8 * (e - row * (N >> 3));
+                // consecutive items walk the 16 rows (stride 2N + 4 floats): conflict-free reads
+                const int row = e % SPB, j0 = 8 * (e / SPB);
                 float re[8], im[8];
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {

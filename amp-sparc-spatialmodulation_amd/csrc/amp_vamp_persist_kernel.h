@@ -281,7 +281,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
         // 1. A <- r~ (vamp.py:91; t = 0: dxdr 0, normScalar 1)
         if constexpr (X3) {
             for (int e = tid; e < PBM * (N >> 3); e += PWG) {   // 8 complex values per item
-                const int row = e / (N >> 3), j0 = 8 * (e - row * (N >> 3));
+                // consecutive items walk the 16 rows (row stride 2N + 4 floats): each group of 16
+                // lanes reads 16 different bank quads (item-major rows put 4 lanes on each)
+                const int row = e % PBM, j0 = 8 * (e / PBM);
                 float re[8], im[8];
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
