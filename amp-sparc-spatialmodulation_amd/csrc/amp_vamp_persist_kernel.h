@@ -12,6 +12,9 @@
 namespace amp {
 
 constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iteration)
+#ifndef AMP_X3_DU
+#define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
+#endif
 
 // LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the 16-row ds_read_b128 and the
 // accumulator stores conflict-free (row r and r+4 land 16 banks apart).
@@ -555,7 +558,7 @@ static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st)
     case 16:
         // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8;
         // f32 engine only: 4 and 8 spill beside the bf16x3 GEMM's registers)
-        if constexpr (X3) return persist_launch_t<NT, 16, NWV, 2, X3>(P, dc, st);
+        if constexpr (X3) return persist_launch_t<NT, 16, NWV, AMP_X3_DU, X3>(P, dc, st);
         switch (den_u()) {
         case 4: return persist_launch_t<NT, 16, NWV, 4, X3>(P, dc, st);
         case 8: return persist_launch_t<NT, 16, NWV, 8, X3>(P, dc, st);

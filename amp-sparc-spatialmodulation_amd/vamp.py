@@ -286,8 +286,9 @@ class VAMP(LazyResult, nn.Module):
         detected side by side in one persistent launch (amp_vamp_detect_count_epochs).  Every
         epoch keeps its own batch-global scalars and early exit (vamp.py:85, 112, 185), so the
         returned Loss objects (one per epoch, in order) equal E sequential forward() calls.
-        ys / xs: sequences of the epochs' y [B, n, 1] and x [B, N, 1]; symbols / indices:
-        sequences of their label arrays.  One host synchronisation per call."""
+        ys / xs: sequences of the epochs' y [B, n, 1] and x [B, N, 1], or stacked [E, B, ...]
+        tensors (used without a copy); symbols / indices: sequences of their label arrays or
+        stacked label tensors.  The Losses resolve lazily (no host stall inside the call)."""
         if self.config.mode != 'sparc':
             raise NotImplementedError("side-by-side epochs decide in generator_mode='sparc' only")
         E = len(ys)
@@ -305,10 +306,12 @@ class VAMP(LazyResult, nn.Module):
         N = Vh.shape[1]
         Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
         sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
-        y = torch.cat([_c64(v, (B, n)) for v in ys]).contiguous()
-        x = torch.cat([_flat_c64(v, B, 'x') for v in xs]).contiguous()
-        sym = torch.cat([_as_device_labels(v, dev).reshape(-1) for v in symbols]).contiguous()
-        idx = torch.cat([_as_device_labels(v, dev).reshape(-1) for v in indices]).contiguous()
+        # a stacked [E, B, ...] tensor is used as it lies (no copy); a sequence is concatenated
+        stack = lambda v, f: (f(v, E) if isinstance(v, torch.Tensor) else torch.cat([f(u, 1) for u in v]))  # noqa: E731
+        y = stack(ys, lambda v, e: _c64(v, (e * B, n))).contiguous()
+        x = stack(xs, lambda v, e: _flat_c64(v, e * B, 'x')).contiguous()
+        sym = stack(symbols, lambda v, e: _as_device_labels(v, dev).reshape(-1)).contiguous()
+        idx = stack(indices, lambda v, e: _as_device_labels(v, dev).reshape(-1)).contiguous()
         if sym.numel() != E * B * cfg.L or idx.numel() != E * B * cfg.L:
             raise ValueError(f'expected {E * B * cfg.L} labels/indices, got {sym.numel()}/{idx.numel()}')
         d, cst = cfg.dims(), cfg.constellation()

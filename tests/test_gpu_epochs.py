@@ -73,6 +73,18 @@ def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0, E):
         assert torch.equal(r[e].view(torch.int32), r0.view(torch.int32)), e
         assert torch.equal(xm[e].view(torch.int32), x0.view(torch.int32)), e
         assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), e
+    # the same epochs as stacked [E, B, ...] tensors (used without a copy)
+    mv = lambda t: t.to(device).contiguous()  # noqa: E731
+    U, s, Vh = (mv(t) for t in chan)
+    ys = torch.stack([mv(e[3]) for e in eps])
+    xs = torch.stack([mv(e[0]) for e in eps])
+    syms = torch.stack([torch.as_tensor(np.asarray(e[1], np.int64)) for e in eps]).to(device)
+    idxs = torch.stack([torch.as_tensor(np.asarray(e[2], np.int64)) for e in eps]).to(device)
+    grp2 = det.forward_epochs(U, s, Vh, ys, SNR, xs, syms, idxs)
+    r2 = det.last_epochs[0]
+    for e in range(E):
+        assert int(grp2[e].loss['T']) == int(grp[e].loss['T']) and float(grp2[e].loss['ser']) == float(grp[e].loss['ser'])
+        assert torch.equal(r2[e].view(torch.int32), r[e].view(torch.int32)), e
 
 
 def test_epochs_independent_rare_path(device):
