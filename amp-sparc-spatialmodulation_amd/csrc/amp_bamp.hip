@@ -47,6 +47,9 @@ struct BampK {
     Partial* parts;        // [max_iter][nblk]
     BampIter* iters;       // [max_iter + 1]
     amp_status* status;
+    // block-banded H (Lin > 1 or Lout > 1): per column tile of Wabs2 / WH / Wabs2T / WHH the
+    // reduction range holding its nonzero blocks (weight_kband), else null (whole range)
+    const int* band[4];
     Const c;
     int elementwise;                       // random_denoiser (bamp.py:79-88) instead of the block one
     float P0, Ps;
@@ -83,6 +86,7 @@ __device__ __forceinline__ void bamp_bayes_elem(const BampK& P, const Const64& c
 
 struct BampWs {
     float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
+    int* band[4];
     float *secmax, *secabs;
     Partial* parts;
     BampIter* iters;
@@ -118,11 +122,19 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.secabs = cv.take<float>((size_t)d->B * d->L);
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk);
     w.iters = cv.take<BampIter>((size_t)max_iter + 1);
+    w.band[0] = cv.take<int>((size_t)2 * (P.ncpA1 / 128));
+    w.band[1] = cv.take<int>((size_t)2 * (P.ncpA2 / 128));
+    w.band[2] = cv.take<int>((size_t)2 * (P.ncpB1 / 128));
+    w.band[3] = cv.take<int>((size_t)2 * (P.ncpB2 / P.bn));
     w.bytes = cv.off;
     return w;
 }
 
 __device__ __forceinline__ float* bvar(const BampK& P, int t) { return (t & 1) ? P.var1 : P.var0; }
+// reduction range of column tile cb of GEMM weight w (0..3: Wabs2, WH, Wabs2T, WHH); whole range
+// when the channel is not block-banded
+__device__ __forceinline__ int bkb(const BampK& P, int w, int cb) { return P.band[w] ? P.band[w][2 * cb] : 0; }
+__device__ __forceinline__ int bke(const BampK& P, int w, int cb) { return P.band[w] ? P.band[w][2 * cb + 1] : -1; }
 
 // v = |H|^2 var (bamp.py:59)
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
@@ -130,7 +142,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     if (P.iters[t].stopped) return;
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds);
+    gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds, bkb(P, 0, tile.cb),
+                   bke(P, 0, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -146,7 +159,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds);
+    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds, bkb(P, 1, tile.cb),
+                   bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
         const int rho = e >> 6, cp = e & 63;           // complex column pair
@@ -173,7 +187,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     if (P.iters[t].stopped) return;
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds);
+    gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds, bkb(P, 2, tile.cb),
+                   bke(P, 2, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -223,7 +238,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds);
+    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds, bkb(P, 3, tile.cb),
+                  bke(P, 3, tile.cb));
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
         const int rho = e / BN, cc = e % BN;
@@ -439,6 +455,12 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.var0 = (float*)a->var; P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    {
+        // block-banded H: the ranges are formed by the prepare launch sequence (AMP_BAND_GEMM=0: off)
+        const char* e = getenv("AMP_BAND_GEMM");
+        const bool band = (d->Lin > 1 || d->Lout > 1) && !(e && e[0] == '0');
+        for (int i = 0; i < 4; ++i) P.band[i] = band ? w.band[i] : nullptr;
+    }
     AMP_REQUIRE(a->denoiser == 0 || a->denoiser == 1, "amp_bamp_run: denoiser %d", a->denoiser);
     P.elementwise = a->denoiser;
     P.P0 = a->P0;
@@ -456,6 +478,13 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
     if ((rc = build_cweight(H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WH, P.kapA2, P.ncpA2, st))) return rc;
     if ((rc = build_abs2_weight(H, 1, P.N, P.N, P.n, (float*)P.Wabs2T, P.kapB1, P.ncpB1, st))) return rc;
     if ((rc = build_cweight(H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.kapB2, P.ncpB2, st))) return rc;
+    if (P.band[0]) {
+        const float* wts[4] = {P.Wabs2, P.WH, P.Wabs2T, P.WHH};
+        const int kaps[4] = {P.kapA1, P.kapA2, P.kapB1, P.kapB2}, ncps[4] = {P.ncpA1, P.ncpA2, P.ncpB1, P.ncpB2};
+        const int bns[4] = {128, 128, 128, P.bn};
+        for (int i = 0; i < 4; ++i)
+            if ((rc = weight_kband(wts[i], kaps[i], ncps[i], bns[i], const_cast<int*>(P.band[i]), st))) return rc;
+    }
     const size_t tot = std::max((size_t)P.B * P.N, (size_t)P.B * P.n);
     const int g = (int)std::min<size_t>((tot + 255) / 256, 2048);
     hipLaunchKernelGGL(bamp_init_kernel, dim3(g), dim3(256), 0, st, P);

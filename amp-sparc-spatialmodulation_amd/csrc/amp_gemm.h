@@ -106,10 +106,13 @@ struct ALoadPlain {
 
 // Computes the C tile of rows [row0, row0+32) x cols [col0, col0+BN) into `lds` (as the C
 // tile, row stride GemmCfg<BN>::LDC).  `wp` is the MFMA-packed [Ncp][kap] weight,
-// kap % GBK == 0, col0 % BN == 0, col0 + BN <= Ncp.
+// kap % GBK == 0, col0 % BN == 0, col0 + BN <= Ncp.  [kb, ke): the reduction range that holds
+// every nonzero weight of this column tile (multiples of GBK; weight_kband), default all of it:
+// a block-banded operator (the ISI / spatially coupled channel, channel.py:75-95) skips its
+// all-zero blocks.
 template <int BN, class AL>
 __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict__ wp, int kap, int row0,
-                                          int col0, float* lds) {
+                                          int col0, float* lds, int kb = 0, int ke = -1) {
     using C = GemmCfg<BN>;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
@@ -126,8 +129,9 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
     for (int j = 0; j < C::NACC; ++j)
         wcol[j] = reinterpret_cast<const float4*>(wp) + ((size_t)((col0 >> 5) + wave * C::NACC + j) * G) * 64 + lane;
 
-    for (int kc0 = 0; kc0 < kap; kc0 += GKC) {
-        const int kc = min(GKC, kap - kc0);
+    if (ke < 0) ke = kap;
+    for (int kc0 = kb; kc0 < ke; kc0 += GKC) {
+        const int kc = min(GKC, ke - kc0);
         const int q4 = kc >> 2;   // float4 per A row in this chunk
         const int g0 = kc0 >> 3, gc = kc >> 3;   // gc % GRING == 0 (kap % 64 == 0)
         // W ring first: its latency overlaps the A staging
@@ -136,7 +140,7 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         for (int d = 0; d < GRING; ++d)
 #pragma unroll
             for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)(g0 + d) * 64];
-        if (kc0 > 0) __syncthreads();   // every wave is done with the previous chunk
+        if (kc0 > kb) __syncthreads();   // every wave is done with the previous chunk
         // stage A[row0 .. row0+32) x [kc0, kc0+kc) (the loader forms fused prologues): all loads
         // of a half-batch in flight before its LDS stores
         constexpr int PER = GBM * (GKC / 4) / AMP_WG;   // float4 per thread for a full chunk

@@ -189,6 +189,10 @@ struct CWeightJob {
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st);
+// For each BN-column tile of an MFMA-packed [ncp][kap] weight: the reduction range [kb, ke)
+// (multiples of GBK) that holds all its nonzero entries -> band[2 c], band[2 c + 1] (kb = ke when
+// the tile is all zero).  One pass over the weight (amp_weights.hip).
+int weight_kband(const float* wp, int kap, int ncp, int BN, int* band, hipStream_t st);
 template <int BN>
 int set_lds_attr(const void* fn);
 int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,

@@ -58,6 +58,10 @@ struct ScampK {
     int x3;                // persistent GEMMs on the bf16x3 engine (Wx1 / Wx2)
     const void* Wx1;       // A    X3-packed (x3_index, O = n, J = N)
     const void* Wx2;       // A^H  X3-packed (O = N, J = n)
+    // launch engine, block-banded A (Lin > 1 or Lout > 1: the ISI / coupled channel): per column
+    // tile of WA (128 wide) / WAH (bn wide) the reduction range holding its nonzero blocks
+    const int* bandA;
+    const int* bandB;
     Const c;
 };
 
@@ -71,6 +75,7 @@ struct ScampWs {
     unsigned* pbar;
     Partial* pparts;
     double* pxch;
+    int *bandA, *bandB;
     size_t bytes;
 };
 
@@ -114,6 +119,8 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(64);
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);
+    w.bandA = cv.take<int>((size_t)2 * (P.ncpA / 128));
+    w.bandB = cv.take<int>((size_t)2 * (P.ncpB / P.bn));
     w.bytes = cv.off;
     return w;
 }

@@ -24,7 +24,8 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds);
+    const int kb = P.bandA ? P.bandA[2 * tile.cb] : 0, ke = P.bandA ? P.bandA[2 * tile.cb + 1] : -1;
+    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
     using C = GemmCfg<128>;
     const float* psi = spsi(P, t + 1);               // psi of iteration t-1 (ones at t = 0)
     const float* phi_old = sphi(P, t + 1);           // +inf at t = 0 (scamp.py:19)
@@ -85,7 +86,8 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds);
+    const int kb = P.bandB ? P.bandB[2 * tile.cb] : 0, ke = P.bandB ? P.bandB[2 * tile.cb + 1] : -1;
+    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     const int lc0 = (col0 / 2) / P.Nt, nlc = max(1, (ncols / 2) / P.Nt);   // coupling blocks in this tile
     float* tau_t = lds + C::CTILE_FLOATS;                                    // [32][Lin]
@@ -435,6 +437,17 @@ static bool scamp_gemm_f32_requested() {
     return v;
 }
 
+// Block-banded A (Lin > 1 or Lout > 1): the GEMMs skip the reduction blocks of each column tile
+// that hold only zeros (weight_kband over the packed weights, once per forward).  Off with
+// AMP_BAND_GEMM=0 (A/B runs).
+static bool band_gemm_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("AMP_BAND_GEMM");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, ScampK& P,
                        Const64& c64) {
     int rc = check_dims(d, c);
@@ -453,6 +466,11 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.sigma2 = (float)a->noise_var;
     P.W = (const float*)a->W;
     P.WA = w.WA; P.WAH = w.WAH;
+    // block-banded A: the ranges are formed by the prepare launch sequence (every later call of
+    // the layer-level API reads them from the workspace)
+    const bool band = (d->Lin > 1 || d->Lout > 1) && band_gemm_enabled();
+    P.bandA = band ? w.bandA : nullptr;
+    P.bandB = band ? w.bandB : nullptr;
     P.y = (const float*)a->y; P.z = w.z; P.s = w.s; P.phi = w.phi; P.tau = w.tau;
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
@@ -496,6 +514,10 @@ static int scamp_prepare_impl(const ScampK& P, const amp_scamp_args* a, hipStrea
     const float2* A = (const float2*)a->A;
     if ((rc = build_cweight(A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.kapA, P.ncpA, st))) return rc;
     if ((rc = build_cweight(A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WAH, P.kapB, P.ncpB, st))) return rc;
+    if (P.bandA) {
+        if ((rc = weight_kband(P.WA, P.kapA, P.ncpA, 128, const_cast<int*>(P.bandA), st))) return rc;
+        if ((rc = weight_kband(P.WAH, P.kapB, P.ncpB, P.bn, const_cast<int*>(P.bandB), st))) return rc;
+    }
     const size_t tot = std::max(std::max((size_t)P.B * P.N, (size_t)P.B * P.n), (size_t)P.B * P.Lout);
     hipLaunchKernelGGL(scamp_init_kernel, dim3((int)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("scamp_init");

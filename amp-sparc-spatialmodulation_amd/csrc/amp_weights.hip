@@ -225,6 +225,44 @@ __global__ __launch_bounds__(AMP_WG) void gemm_store_kernel(const float* __restr
     }
 }
 
+// One workgroup per BN-column tile; each wave takes (column group, reduction group) blocks of the
+// packed layout (64 float4 = one lane each, wcol in gemm_tile) and keeps the first / last group
+// holding a nonzero value (NaN / inf count as nonzero: they must reach the product).
+__global__ __launch_bounds__(256) void weight_kband_kernel(const float4* __restrict__ wp, int G, int cgs,
+                                                           int* __restrict__ band) {
+    __shared__ int s_lo, s_hi;
+    if (threadIdx.x == 0) { s_lo = G; s_hi = -1; }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int cg0 = blockIdx.x * cgs;
+    int lo = G, hi = -1;
+    for (int b = wave; b < cgs * G; b += blockDim.x >> 6) {   // wave-uniform
+        const int cg = cg0 + b / G, g = b % G;
+        const float4 v = wp[((size_t)cg * G + g) * 64 + lane];
+        const bool nz = (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f) | (v.x != v.x) | (v.y != v.y) |
+                        (v.z != v.z) | (v.w != v.w);
+        if (__any(nz)) { lo = min(lo, g); hi = max(hi, g); }
+    }
+    if (lane == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int gpk = GBK / 8;                           // reduction groups per GBK
+        const int kb = s_hi < 0 ? 0 : (s_lo / gpk) * GBK;
+        const int ke = s_hi < 0 ? 0 : ((s_hi + gpk) / gpk) * GBK;
+        band[2 * blockIdx.x] = kb;
+        band[2 * blockIdx.x + 1] = ke;
+    }
+}
+
+int weight_kband(const float* wp, int kap, int ncp, int BN, int* band, hipStream_t st) {
+    AMP_REQUIRE(kap % GBK == 0 && ncp % BN == 0 && BN % 32 == 0, "weight_kband: kap %d / ncp %d / BN %d", kap, ncp,
+                BN);
+    hipLaunchKernelGGL(weight_kband_kernel, dim3(ncp / BN), dim3(256), 0, st, (const float4*)wp, kap / 8, BN / 32,
+                       band);
+    AMP_LAUNCH_CHECK("weight_kband");
+    return AMP_OK;
+}
+
 int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,
                int nc, hipStream_t st) {
     static bool attr = false;
