@@ -69,8 +69,10 @@ def main(steps=50, warmup=30, only=None):
                 eps.append((xe, lab(se), lab(ie), A @ xe + ch.awgn(SNR)))
             U, s, Vh = torch.linalg.svd(A, full_matrices=False)
             det = VAMP(cfg)
-            ea = (mv(U), mv(s), mv(Vh), [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
-                  [e[1] for e in eps], [e[2] for e in eps])
+            # the epochs' inputs stacked [E, B, ...] in HBM (forward_epochs uses them without a copy)
+            ea = (mv(U), mv(s), mv(Vh), torch.stack([mv(e[3]) for e in eps]), SNR,
+                  torch.stack([mv(e[0]) for e in eps]), torch.stack([e[1] for e in eps]),
+                  torch.stack([e[2] for e in eps]))
             flop = 16.0 * Nt * min(Nt, Nr)
             for _ in range(warmup):
                 Ls = det.forward_epochs(*ea)
