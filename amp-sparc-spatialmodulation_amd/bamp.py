@@ -19,7 +19,7 @@ from torch import nn
 import amp_native as nat
 from config import Config
 from loss import Loss
-from vamp import LazyResult, _c64, block_denoise
+from vamp import LazyResult, ShardHook, _c64, block_denoise
 
 
 class _Buffers:
@@ -185,3 +185,58 @@ class BAMP(LazyResult, nn.Module):
         self._keep = T
         self.last = T
         return self.L
+
+
+class ShardedBAMP(ShardHook, BAMP):
+    """SURVEY §8(e) exact-compat mode for BAMP: ONE batch split over the ranks of
+    torch.distributed (rank r detects trials [r B / P, (r + 1) B / P)).  ``forward`` keeps
+    BAMP.forward's signature and takes the whole batch's inputs (replicated from one seed); the
+    rank runs its slice through amp_bamp_run_sharded, whose hook all-reduces the batch-global
+    values of every iteration (max |xi| of the denoiser's shift, bamp.py:70; the allclose count,
+    bamp.py:140; the rare path's exact values), decides its rows on xmap (bamp.py:142) and merges
+    the counters with ONE all-reduce: the returned Loss equals the whole-batch forward's."""
+
+    def __init__(self, config: Config, group=None) -> None:
+        super().__init__(config)
+        self._shard_init(group)
+
+    def forward(self, H: torch.Tensor, y: torch.Tensor, SNR: float, x: torch.Tensor, symbols, indices) -> Loss:
+        if self.config.mode == 'random':
+            raise NotImplementedError("trial sharding needs the batch (generator_mode 'random' runs at B = 1)")
+        with torch.cuda.device(y.device):
+            return self._forward_sharded(H, y, SNR, x, symbols, indices)
+
+    def _forward_sharded(self, H, y, SNR, x, symbols, indices) -> Loss:
+        cfg = self.config
+        B = cfg.B
+        b0, b1 = self.shard()
+        Bl = b1 - b0
+        n, N = H.shape[-2], H.shape[-1]
+        dev = y.device
+        Hc = _c64(H, (n, N))
+        yl = _c64(y, (B, n))[b0:b1].contiguous()
+        d, cst = cfg.dims(batch=Bl), cfg.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_bamp_workspace_bytes(C.byref(d), cfg.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_bamp_workspace_bytes: invalid dimensions')
+        self._ws = nat.WORKSPACE.get(dev, 'bamp_sharded', wsb)
+        xmap = torch.empty(Bl, N, dtype=torch.complex64, device=dev)
+        xm = torch.empty_like(xmap)
+        var = torch.empty(Bl, N, dtype=torch.float32, device=dev)
+        res = torch.zeros(256, dtype=torch.uint8, device=dev)      # amp_status @0, amp_counts @64
+        a = nat.AmpBampArgs()
+        a.H, a.y = nat.dptr(Hc, name='H'), nat.dptr(yl, name='y')
+        a.max_iter = cfg.N_Layers
+        a.denoiser = 0
+        a.noise_var = float(self.E / SNR)                                  # bamp.py:124
+        a.P0, a.Ps = float(np.float32(cfg.P0)), float(np.float32(cfg.Ps))
+        a.xmap, a.xmmse, a.var = nat.dptr(xmap), nat.dptr(xm), nat.dptr(var)
+        a.status = nat.dptr(res)
+        a.ws, a.ws_bytes = nat.dptr(self._ws), self._ws.numel()
+        st = nat.stream_ptr(dev)
+        self._run_hooked(lib.amp_bamp_run_sharded, 'amp_bamp_run_sharded', C.byref(d), C.byref(cst), C.byref(a), B,
+                         st)
+        L = self._decide_merge(d, cst, xmap, xm, x, symbols, indices, b0, b1, res, st)
+        self.last_shard = (xmap.view(Bl, N, 1), xm.view(Bl, N, 1), var.view(Bl, N, 1))
+        return L

@@ -50,6 +50,7 @@ struct BampK {
     // block-banded H (Lin > 1 or Lout > 1): per column tile of Wabs2 / WH / Wabs2T / WHH the
     // reduction range holding its nonzero blocks (weight_kband), else null (whole range)
     const int* band[4];
+    XState* xs;            // trial-sharded exchange words (amp_bamp_run_sharded)
     Const c;
     int elementwise;                       // random_denoiser (bamp.py:79-88) instead of the block one
     float P0, Ps;
@@ -87,6 +88,7 @@ __device__ __forceinline__ void bamp_bayes_elem(const BampK& P, const Const64& c
 struct BampWs {
     float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
     int* band[4];
+    XState* xs;
     float *secmax, *secabs;
     Partial* parts;
     BampIter* iters;
@@ -126,6 +128,7 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.band[1] = cv.take<int>((size_t)2 * (P.ncpA2 / 128));
     w.band[2] = cv.take<int>((size_t)2 * (P.ncpB1 / 128));
     w.band[3] = cv.take<int>((size_t)2 * (P.ncpB2 / P.bn));
+    w.xs = cv.take<XState>(1);
     w.bytes = cv.off;
     return w;
 }
@@ -346,6 +349,149 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
 }
 
 // Tracker (bamp.py:13-25): xmmse = 0, var(prev) = 1, z = y, u = 0 + sigma2 -> 1/u.
+// ---- trial-sharded iteration (amp_bamp_run_sharded; SURVEY §8(e) exact-compat) ----
+// bamp_r split at its batch-global values, as the VAMP stages (amp_vamp.hip vamp_xr*): the
+// not-close count (bamp.py:140) and max|xi| / min section max (bamp.py:70) after xr1, the rare
+// path's exact max|xi| after xr2 and its recomputed sections' deltas after xr3.
+__device__ inline void bamp_record(const BampK& P, int t, bool stop, int fixed) {
+    BampIter nx;
+    nx.stopped = stop ? 1 : 0;
+    nx.T = t + 1;
+    nx.fixed = fixed;
+    nx.fixed_all = (fixed < 0) ? 1 : 0;
+    P.iters[t + 1] = nx;
+    if (nx.stopped || t + 1 == P.max_iter) {
+        amp_status s;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+        *P.status = s;
+    }
+}
+
+__global__ __launch_bounds__(BRWG) void bamp_xr1(BampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    XState* xs = P.xs;
+    if (P.iters[t].stopped) {
+        if (threadIdx.x == 0) { xs->sum[0] = xs->sum[1] = 0.0; xs->mx[0] = xs->mx[1] = 0.0; }
+        return;
+    }
+    const PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
+    if (threadIdx.x == 0) {
+        xs->sum[0] = 0.0;
+        xs->sum[1] = (double)pa.notclose;
+        xs->mx[0] = (pa.maxabs <= 1.7976931348623157e308) ? pa.maxabs : INFINITY;   // NaN / inf wins
+        xs->mx[1] = (pa.minsecmax == pa.minsecmax) ? -pa.minsecmax : INFINITY;
+    }
+}
+
+__device__ inline PartAcc bamp_xs_global(const XState& x) {
+    PartAcc pa;
+    pa.sumvar = 0.0;
+    pa.notclose = (uint32_t)x.sum[1];
+    pa.maxabs = x.mx[0];
+    pa.minsecmax = -x.mx[1];
+    return pa;
+}
+
+__global__ __launch_bounds__(BRWG) void bamp_xr2(BampK P, Const64 c64, int t) {
+    __shared__ double s_d[BRWG / 64];
+    XState* xs = P.xs;
+    const BampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) { P.iters[t + 1] = cur; xs->mode = 0; xs->gmax[0] = 0.0; }
+        return;
+    }
+    PartAcc pa = bamp_xs_global(*xs);
+    if (!part_allnan(pa) && part_danger(pa)) {
+        const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+        const float* cov = P.cov;
+        const int M = P.M;
+        const double G32 = pa.maxabs, slack = logit_slack(G32);
+        double gm = 0.0;
+        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
+            if (!((double)P.secabs[sct] >= G32 - slack)) continue;
+            const size_t o0 = (size_t)sct * M;
+            gm = fmax(gm, section_absmax_f64([=](int m, float& rr, float& ri, float& it) {
+                const float2 v = xp2[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (cov[o0 + m] * 0.5f);
+            }, M, c64));
+        }
+        gm = group_max(gm, 64);
+        if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double G = 0.0;
+            for (int w = 0; w < BRWG / 64; ++w) G = fmax(G, s_d[w]);
+            xs->gmax[0] = G;
+            xs->mode = 2;
+        }
+        return;
+    }
+    int fixed = 0;
+    if (part_allnan(pa)) {
+        if (!cur.fixed_all) nan_fill(P.xm, bvar(P, t), (size_t)P.B * P.N);
+        pa.notclose = 1;
+        fixed = -1;
+    }
+    if (threadIdx.x == 0) {
+        bamp_record(P, t, pa.notclose == 0, fixed);
+        xs->mode = 0;
+        xs->gmax[0] = 0.0;
+    }
+}
+
+__global__ __launch_bounds__(BRWG) void bamp_xr3(BampK P, Const64 c64, int t) {
+    __shared__ double s_d[2][BRWG / 64];
+    XState* xs = P.xs;
+    if (xs->mode != 2) {
+        if (threadIdx.x == 0) xs->fix[0] = xs->fix[1] = xs->fix[2] = 0.0;
+        return;
+    }
+    const PartAcc pa = bamp_xs_global(*xs);
+    const double G = xs->gmax[0], slack = logit_slack(pa.maxabs);
+    float* vn = bvar(P, t);
+    const float* vp = bvar(P, t + 1);
+    const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+    const float* cov = P.cov;
+    float2* x2 = reinterpret_cast<float2*>(P.xm);
+    const int M = P.M;
+    int dnc = 0, cnt = 0;
+    for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
+        if (!((double)P.secmax[sct] - G < AMP_DANGER + slack)) continue;
+        ++cnt;
+        const size_t o0 = (size_t)sct * M;
+        exact_section_f64<true>(
+            [=](int m, float& rr, float& ri, float& it) {
+                const float2 v = xp2[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (cov[o0 + m] * 0.5f);
+            },
+            [&](int m, float xr, float xi, float var) {
+                const size_t o = o0 + m;
+                dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(vn[o], vp[o]) ? 0 : 1);
+                x2[o] = make_float2(xr, xi);
+                vn[o] = var;
+            },
+            M, c64, G);
+    }
+    dnc = group_sum(dnc, 64);
+    cnt = group_sum(cnt, 64);
+    if ((threadIdx.x & 63) == 0) { s_d[0][threadIdx.x >> 6] = (double)dnc; s_d[1][threadIdx.x >> 6] = (double)cnt; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = 0.0, c = 0.0;
+        for (int w = 0; w < BRWG / 64; ++w) { b += s_d[0][w]; c += s_d[1][w]; }
+        xs->fix[0] = 0.0; xs->fix[1] = b; xs->fix[2] = c;
+    }
+}
+
+__global__ void bamp_xr4(BampK P, int t) {
+    const XState* xs = P.xs;
+    if (xs->mode != 2 || threadIdx.x != 0) return;
+    const PartAcc pa = bamp_xs_global(*xs);
+    const long long nc = (long long)pa.notclose + (long long)xs->fix[1];
+    bamp_record(P, t, nc == 0, (int)xs->fix[2]);
+}
+
 __global__ void bamp_init_kernel(BampK P) {
     const size_t BN_ = (size_t)P.B * P.N, Bn = (size_t)P.B * P.n;
     const size_t tot = BN_ > Bn ? BN_ : Bn;
@@ -455,6 +601,7 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.var0 = (float*)a->var; P.var1 = w.var1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
+    P.xs = w.xs;
     {
         // block-banded H: the ranges are formed by the prepare launch sequence (AMP_BAND_GEMM=0: off)
         const char* e = getenv("AMP_BAND_GEMM");
@@ -504,6 +651,28 @@ static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStrea
     return AMP_OK;
 }
 
+static int bamp_iterate_sharded(const BampK& P, const Const64& c64, int t, hipStream_t st) {
+    const int gr = cdiv(P.B, GBM);
+    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_kb2(P, c64, gr, t, st);
+    hipLaunchKernelGGL(bamp_xr1, dim3(1), dim3(BRWG), 0, st, P, t);
+    AMP_LAUNCH_CHECK("bamp_xr1");
+    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
+    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bamp_xr2, dim3(1), dim3(BRWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("bamp_xr2");
+    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hipLaunchKernelGGL(bamp_xr3, dim3(1), dim3(BRWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("bamp_xr3");
+    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hipLaunchKernelGGL(bamp_xr4, dim3(1), dim3(64), 0, st, P, t);
+    AMP_LAUNCH_CHECK("bamp_xr4");
+    return AMP_OK;
+}
+
 // the caller's var holds the last executed iteration's (ping-pong buffers)
 static int bamp_finalize_impl(const BampK& P, hipStream_t st) {
     hipLaunchKernelGGL(bamp_output_kernel, dim3((int)std::min<size_t>(((size_t)P.B * P.N + 255) / 256, 2048)),
@@ -515,6 +684,22 @@ static int bamp_finalize_impl(const BampK& P, hipStream_t st) {
 }  // namespace amp
 
 extern "C" {
+
+int amp_bamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, int32_t B_global,
+                         void* stream) {
+    BampK P;
+    Const64 c64;
+    int rc = bamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(allreduce_hook_set(), "amp_bamp_run_sharded: no all-reduce hook registered (amp_set_allreduce_hook)");
+    AMP_REQUIRE(B_global >= d->B, "amp_bamp_run_sharded: B_global = %d < this rank's B = %d", B_global, d->B);
+    AMP_REQUIRE(a->denoiser == 0, "amp_bamp_run_sharded: the element-wise denoiser (mode 'random', B = 1) has no "
+                "batch-global values to share");
+    hipStream_t st = (hipStream_t)stream;
+    rc = bamp_prepare_impl(P, a, st);
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = bamp_iterate_sharded(P, c64, t, st);
+    return rc ? rc : bamp_finalize_impl(P, st);
+}
 
 int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream) {
     BampK P;

@@ -131,6 +131,23 @@ inline Const64 to_const64(const amp_constellation* c) {
     return k;
 }
 
+// Batch-global values of one trial-sharded iteration (amp_vamp_run_sharded, amp_bamp_run_sharded):
+// each stage's float64 words are all-reduced across the ranks by the registered hook between
+// launches.
+struct XState {
+    double sum[2];    // SUM: sum var (VAMP, vamp.py:85), not-close count (vamp.py:185, bamp.py:140)
+    double mx[2];     // MAX: max|xi| (NaN -> +inf), -min section max (vamp.py:112, bamp.py:70)
+    double gmax[2];   // MAX: exact float64 max|xi| over the candidate sections (rare path); [1] pad
+    double fix[4];    // SUM: rare-path var delta, not-close delta, recomputed sections; [3] pad
+    int mode;         // 2: this iteration takes the rare path (xr3 / xr4 act), else 0
+    int pad[3];
+};
+
+// The registered amp_allreduce_fn (amp_set_allreduce_hook, amp_weights.hip): all-reduce `count`
+// float64 words at `buf` in place on `st` (op: AMP_ALLREDUCE_SUM / MAX).
+bool allreduce_hook_set();
+int call_allreduce_hook(double* buf, int count, int op, hipStream_t st);
+
 int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
 int device_cu_count();   // compute units of the current device (cached)
 

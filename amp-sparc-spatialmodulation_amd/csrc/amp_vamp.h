@@ -14,17 +14,6 @@ constexpr int RWG = 1024;   // threads of the reduction / fix-up workgroup
 constexpr int PBAR_EPOCH = 64;                 // first per-epoch barrier counter in pbar
 constexpr int PBAR_WORDS = PBAR_EPOCH + 256;   // one counter per epoch (E <= 256 workgroups)
 
-// Batch-global values of one trial-sharded iteration (amp_vamp_run_sharded): each stage's
-// float64 words are all-reduced across the ranks by the registered hook between launches.
-struct XState {
-    double sum[2];    // SUM: sum var, not-close count (vamp.py:85, 185)
-    double mx[2];     // MAX: max|xi| (NaN -> +inf), -min section max (vamp.py:112)
-    double gmax[2];   // MAX: exact float64 max|xi| over the candidate sections (rare path); [1] pad
-    double fix[4];    // SUM: rare-path var delta, not-close delta, recomputed sections; [3] pad
-    int mode;         // 2: this iteration takes the rare path (xr3 / xr4 act), else 0
-    int pad[3];
-};
-
 struct VampK {
     int B, N, n, k, L, M;
     int Bmean;          // the batch var.mean() runs over (vamp.py:85): B, or the whole batch when sharded

@@ -571,15 +571,6 @@ static int vamp_finalize_impl(const VampK& P, hipStream_t st) {
     return AMP_OK;
 }
 
-static amp_allreduce_fn g_hook = nullptr;
-static void* g_hook_ctx = nullptr;
-
-static int call_hook(double* buf, int count, int op, hipStream_t st) {
-    const int rc = g_hook((void*)buf, count, op, (void*)st, g_hook_ctx);
-    if (rc) set_error("amp_vamp_run_sharded: all-reduce hook returned %d", rc);
-    return rc ? AMP_E_LAUNCH : AMP_OK;
-}
-
 static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipStream_t st) {
     dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
     hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
@@ -588,15 +579,15 @@ static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipSt
     AMP_LAUNCH_CHECK("vamp_k2");
     hipLaunchKernelGGL(vamp_xr1, dim3(1), dim3(RWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("vamp_xr1");
-    int rc = call_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
-    if (!rc) rc = call_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
+    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
+    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
     if (rc) return rc;
     hipLaunchKernelGGL(vamp_xr2, dim3(1), dim3(RWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("vamp_xr2");
-    if ((rc = call_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
     hipLaunchKernelGGL(vamp_xr3, dim3(1), dim3(RWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("vamp_xr3");
-    if ((rc = call_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
     hipLaunchKernelGGL(vamp_xr4, dim3(1), dim3(RWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("vamp_xr4");
     return AMP_OK;
@@ -608,19 +599,13 @@ using namespace amp;
 
 extern "C" {
 
-int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx) {
-    g_hook = fn;
-    g_hook_ctx = ctx;
-    return AMP_OK;
-}
-
 int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t B_global,
                          void* stream) {
     VampK P;
     Const64 c64;
     int rc = vamp_setup(d, c, a, P, c64);
     if (rc) return rc;
-    AMP_REQUIRE(g_hook, "amp_vamp_run_sharded: no all-reduce hook registered (amp_set_allreduce_hook)");
+    AMP_REQUIRE(allreduce_hook_set(), "amp_vamp_run_sharded: no all-reduce hook registered (amp_set_allreduce_hook)");
     AMP_REQUIRE(B_global >= d->B, "amp_vamp_run_sharded: B_global = %d < this rank's B = %d", B_global, d->B);
     P.Bmean = B_global;
     hipStream_t st = (hipStream_t)stream;

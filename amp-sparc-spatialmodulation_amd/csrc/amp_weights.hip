@@ -278,9 +278,26 @@ int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int k
     return AMP_OK;
 }
 
+static amp_allreduce_fn g_hook = nullptr;
+static void* g_hook_ctx = nullptr;
+
+bool allreduce_hook_set() { return g_hook != nullptr; }
+
+int call_allreduce_hook(double* buf, int count, int op, hipStream_t st) {
+    const int rc = g_hook((void*)buf, count, op, (void*)st, g_hook_ctx);
+    if (rc) set_error("trial-sharded run: all-reduce hook returned %d", rc);
+    return rc ? AMP_E_LAUNCH : AMP_OK;
+}
+
 }  // namespace amp
 
 extern "C" {
+
+int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx) {
+    amp::g_hook = fn;
+    amp::g_hook_ctx = ctx;
+    return AMP_OK;
+}
 
 const char* amp_last_error(void) { return amp::g_err; }
 

@@ -384,22 +384,13 @@ class VAMP(LazyResult, nn.Module):
         return d[:nbytes], h[:nbytes]
 
 
-class ShardedVAMP(VAMP):
-    """SURVEY §8(e) exact-compat mode: ONE batch of config.B trials split over the ranks of
-    torch.distributed, rank r detecting trials [r B / P, (r + 1) B / P).
+class ShardHook:
+    """Shared host side of the trial-sharded detectors (SURVEY §8(e) exact-compat mode): the rank's
+    slice of the batch, the all-reduce hook the C drivers call between launches
+    (amp_set_allreduce_hook), and the slice's decision + the ONE counter all-reduce that gives
+    every rank the whole batch's Loss."""
 
-    ``forward`` keeps VAMP.forward's signature and takes the WHOLE batch's inputs (every rank
-    draws the same epoch from the same seed: channel, messages and noise are replicated with no
-    communication, SURVEY §8(e)); the rank runs its slice through amp_vamp_run_sharded, whose
-    registered hook all-reduces the batch-global scalars of every iteration (var.mean(),
-    max |xi|, allclose; vamp.py:85, 112, 185) five times per iteration, decides its rows with
-    amp_map_decide_count_rows and merges the error counters with ONE all-reduce.  The returned
-    Loss equals the whole-batch forward's, up to the float64 summation order of var.mean().
-    The hook runs torch.distributed.all_reduce on the device words for RCCL ('nccl') and
-    through host memory for gloo."""
-
-    def __init__(self, config: Config, group=None) -> None:
-        super().__init__(config, engine=nat.ENGINE_LAUNCHES)
+    def _shard_init(self, group) -> None:
         self.group = group
         self._ws = None
         self._hook_error = None
@@ -433,10 +424,64 @@ class ShardedVAMP(VAMP):
         B = self.config.B
         return rank * B // world, (rank + 1) * B // world
 
-    def _forward(self, U, s, Vh, y, SNR, x, symbols, indices) -> Loss:
+    def _run_hooked(self, fn, what, *args) -> None:
+        lib = nat.lib()
+        self._hook_error = None
+        nat.check(lib.amp_set_allreduce_hook(C.cast(self._hook, C.c_void_p), None), 'amp_set_allreduce_hook')
+        rc = fn(*args)
+        if self._hook_error is not None:
+            raise RuntimeError(f'{what}: all-reduce hook failed') from self._hook_error
+        nat.check(rc, what)
+
+    def _decide_merge(self, d, cst, xmap, xm, x, symbols, indices, b0, b1, res, st) -> Loss:
+        """Decision on this slice (flat indices of the whole batch), ONE all-reduce of the
+        counters, the whole batch's metrics recorded on self.L."""
         from loss import _as_device_labels, _flat_c64, allreduce_counts, counts_to_vector, vector_to_counts
         cfg = self.config
         B, L = cfg.B, cfg.L
+        dev = xmap.device
+        xl = _flat_c64(x, B, 'x')[b0:b1].contiguous()
+        syml = _as_device_labels(symbols, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
+        idxl = _as_device_labels(indices, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
+        lib = nat.lib()
+        dwsb = lib.amp_map_decide_workspace_bytes(C.byref(d))
+        dws = nat.WORKSPACE.get(dev, 'decide_sharded', dwsb)
+        nat.check(lib.amp_map_decide_count_rows(C.byref(d), C.byref(cst), nat.dptr(xmap), nat.dptr(xm), nat.dptr(xl),
+                                                nat.dptr(syml), nat.dptr(idxl), self.L._ibits, b0,
+                                                nat.dptr(res) + 64, None, nat.dptr(dws), dwsb, st),
+                  'amp_map_decide_count_rows')
+        raw = res.cpu().numpy().tobytes()
+        status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
+        counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
+        merged = vector_to_counts(allreduce_counts(counts_to_vector(counts)))   # the ONE counter all-reduce
+        self.L.resolve()
+        self.L.dump()
+        self.L.last_counts, self.L.last_status = merged, status
+        self.L.record(self.L.rates_from_counts(merged), int(status.T))
+        return self.L
+
+
+class ShardedVAMP(ShardHook, VAMP):
+    """SURVEY §8(e) exact-compat mode: ONE batch of config.B trials split over the ranks of
+    torch.distributed, rank r detecting trials [r B / P, (r + 1) B / P).
+
+    ``forward`` keeps VAMP.forward's signature and takes the WHOLE batch's inputs (every rank
+    draws the same epoch from the same seed: channel, messages and noise are replicated with no
+    communication, SURVEY §8(e)); the rank runs its slice through amp_vamp_run_sharded, whose
+    registered hook all-reduces the batch-global scalars of every iteration (var.mean(),
+    max |xi|, allclose; vamp.py:85, 112, 185) five times per iteration, decides its rows with
+    amp_map_decide_count_rows and merges the error counters with ONE all-reduce.  The returned
+    Loss equals the whole-batch forward's, up to the float64 summation order of var.mean().
+    The hook runs torch.distributed.all_reduce on the device words for RCCL ('nccl') and
+    through host memory for gloo."""
+
+    def __init__(self, config: Config, group=None) -> None:
+        super().__init__(config, engine=nat.ENGINE_LAUNCHES)
+        self._shard_init(group)
+
+    def _forward(self, U, s, Vh, y, SNR, x, symbols, indices) -> Loss:
+        cfg = self.config
+        B = cfg.B
         b0, b1 = self.shard()
         Bl = b1 - b0
         n, k = U.shape[0], U.shape[1]
@@ -445,9 +490,6 @@ class ShardedVAMP(VAMP):
         Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
         sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
         yl = _c64(y, (B, n))[b0:b1].contiguous()
-        xl = _flat_c64(x, B, 'x')[b0:b1].contiguous()
-        syml = _as_device_labels(symbols, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
-        idxl = _as_device_labels(indices, dev).reshape(-1)[b0 * L:b1 * L].contiguous()
         d, cst = cfg.dims(batch=Bl), cfg.constellation()
         lib = nat.lib()
         wsb = lib.amp_vamp_workspace_bytes(C.byref(d), k, cfg.N_Layers)
@@ -467,29 +509,12 @@ class ShardedVAMP(VAMP):
         a.status = nat.dptr(res)
         a.ws, a.ws_bytes = nat.dptr(self._ws), self._ws.numel()
         st = nat.stream_ptr(dev)
-        self._hook_error = None
-        nat.check(lib.amp_set_allreduce_hook(C.cast(self._hook, C.c_void_p), None), 'amp_set_allreduce_hook')
-        rc = lib.amp_vamp_run_sharded(C.byref(d), C.byref(cst), C.byref(a), B, st)
-        if self._hook_error is not None:
-            raise RuntimeError('amp_vamp_run_sharded: all-reduce hook failed') from self._hook_error
-        nat.check(rc, 'amp_vamp_run_sharded')
-        # decision on T.r (vamp.py:187) over this slice, flat indices of the whole batch
-        dwsb = lib.amp_map_decide_workspace_bytes(C.byref(d))
-        dws = nat.WORKSPACE.get(dev, 'decide_sharded', dwsb)
-        nat.check(lib.amp_map_decide_count_rows(C.byref(d), C.byref(cst), nat.dptr(r), nat.dptr(xm), nat.dptr(xl),
-                                                nat.dptr(syml), nat.dptr(idxl), self.L._ibits, b0,
-                                                nat.dptr(res) + 64, None, nat.dptr(dws), dwsb, st),
-                  'amp_map_decide_count_rows')
-        raw = res.cpu().numpy().tobytes()
-        status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
-        counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
-        merged = vector_to_counts(allreduce_counts(counts_to_vector(counts)))   # the ONE counter all-reduce
-        self.L.resolve()
-        self.L.dump()
-        self.L.last_counts, self.L.last_status = merged, status
-        self.L.record(self.L.rates_from_counts(merged), int(status.T))
+        self._run_hooked(lib.amp_vamp_run_sharded, 'amp_vamp_run_sharded', C.byref(d), C.byref(cst), C.byref(a), B,
+                         st)
+        # decision on T.r (vamp.py:187) over this slice
+        L = self._decide_merge(d, cst, r, xm, x, symbols, indices, b0, b1, res, st)
         self.last_shard = (r.view(Bl, N, 1), xm.view(Bl, N, 1), var.view(Bl, N, 1))
-        return self.L
+        return L
 
 
 def read_result(res: torch.Tensor):

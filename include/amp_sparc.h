@@ -214,6 +214,12 @@ typedef struct amp_bamp_args {
 
 size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
 int amp_bamp_run(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, void* stream);
+/* amp_bamp_run on one rank's slice of a trial-sharded batch (amp_vamp_run_sharded's protocol,
+ * the hook of amp_set_allreduce_hook): max|xi| / min section max (bamp.py:70) and the allclose
+ * count (bamp.py:140) all-reduced per iteration; decision on xmap with amp_map_decide_count_rows.
+ * denoiser 0 only (the element-wise mode runs at B = 1). */
+int amp_bamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_bamp_args* a, int32_t B_global,
+                         void* stream);
 /* Layer-level pieces of amp_bamp_run (same arguments; amp_bamp_run = prepare, iterate(t) for
  * t < max_iter, finalize): prepare = Tracker (bamp.py:13-25: the H / H^H / |H|^2 operators,
  * xmmse = 0, var = 1, z = y, u = sigma2); iterate(t) = one BAMPLayer.forward (bamp.py:48-64) +

@@ -13,25 +13,31 @@ import torch  # noqa: E402
 
 
 def case_inputs(name):
-    """CASE = alphabet:EbN0:B[:yscale] — cfg2 shape (Nt=64 Na=4 Nr=128), host replica, seed 7."""
+    """CASE = [bamp:|bampisi:]alphabet:EbN0:B[:yscale] — VAMP / BAMP at the cfg2 shape (Nt=64 Na=4
+    Nr=128), or BAMP at a small ISI shape (Nt=32 Na=4 Nr=32 Lin=4 Lh=2: banded GEMMs); host
+    replica, seed 7.  Returns (detector, cfg, forward arguments)."""
     from channel import Channel
     from config import Config
     from data import Data
     f = name.split(':')
+    algo = f.pop(0) if f[0] in ('bamp', 'bampisi') else 'vamp'
     alph, ebn0, B = f[0], float(f[1]), int(f[2])
     scale = float(f[3]) if len(f) > 3 else 1.0
-    cfg = Config(64, 4, 128, 1, 1, batch=B, generator_mode='sparc', iterations=20, alphabet=alph,
+    shape = (32, 4, 32, 4, 2) if algo == 'bampisi' else (64, 4, 128, 1, 1)
+    cfg = Config(*shape, batch=B, generator_mode='sparc', iterations=20, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cpu')
     np.random.seed(7)
     torch.manual_seed(7)
     ch, da = Channel(cfg), Data(cfg)
     _, A = ch.generate_as_sparc()
-    U, s, Vh = torch.linalg.svd(A, full_matrices=False)
     x, sym, idx = da.generate_message()
     SNR = cfg.snr(ebn0)
     y = (A @ x + ch.awgn(SNR)) * scale
     cfg.device = 'cuda'
-    return cfg, (U, s, Vh, y, SNR, x, sym, idx)
+    if algo == 'vamp':
+        U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+        return 'vamp', cfg, (U, s, Vh, y, SNR, x, sym, idx)
+    return 'bamp', cfg, (A, y, SNR, x, sym, idx)
 
 
 def main():
@@ -39,14 +45,15 @@ def main():
     torch.distributed.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
                                          world_size=world)
     try:
+        from bamp import ShardedBAMP
         from vamp import ShardedVAMP
         dev = torch.device('cuda:0')
         res = {}
         for name in sys.argv[5:]:
-            cfg, (U, s, Vh, y, SNR, x, sym, idx) = case_inputs(name)
-            det = ShardedVAMP(cfg)
-            mv = lambda t: t.to(dev).contiguous()  # noqa: E731
-            L = det(mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
+            algo, cfg, args = case_inputs(name)
+            det = ShardedVAMP(cfg) if algo == 'vamp' else ShardedBAMP(cfg)
+            mv = lambda t: t.to(dev).contiguous() if isinstance(t, torch.Tensor) else t  # noqa: E731
+            L = det(*(mv(a) for a in args))
             res[name] = {k: (float(v) if np.ndim(v) == 0 else np.asarray(v).tolist()) for k, v in L.loss.items()}
             res[name]['slice'] = list(det.shard())
             np.save(os.path.join(out, f'{name.replace(":", "_")}_r{rank}.npy'), det.last_shard[0].cpu().numpy())

@@ -1,5 +1,5 @@
 """GPU: trial sharding across ranks (SURVEY §8(e) exact-compat mode; ShardedVAMP /
-amp_vamp_run_sharded).  2 and 3 rank processes on the one GPU, gloo process group (the hook
+amp_vamp_run_sharded, ShardedBAMP / amp_bamp_run_sharded incl. an ISI shape on the banded GEMMs).  2 and 3 rank processes on the one GPU, gloo process group (the hook
 all-reduces the batch scalars through host memory; RCCL is the same hook on the device words).
 
 Bar: every rank's Loss equals the single-process whole-batch forward's — T exact, VER / SER /
@@ -23,7 +23,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from shard_trials_worker import case_inputs  # noqa: E402
 
-CASES = ['16QAM:8:1024', 'QPSK:4:1024', '16QAM:20:1024', 'QPSK:12:1000', '16QAM:14:1024:40']
+CASES = ['16QAM:8:1024', 'QPSK:4:1024', '16QAM:20:1024', 'QPSK:12:1000', '16QAM:14:1024:40',
+         'bamp:QPSK:6:1024', 'bamp:16QAM:12:1000', 'bamp:16QAM:20:1024', 'bampisi:QPSK:6:256']
 
 
 def _free_port():
@@ -45,13 +46,14 @@ def test_sharded_equals_whole_batch(device, tmp_path, world):
     rcs = [p.wait(timeout=100) for p in procs]
     assert rcs == [0] * world, rcs
     outs = [json.load(open(tmp_path / f'rank{r}.json')) for r in range(world)]
+    from bamp import BAMP
     for name in CASES:
-        cfg, (U, s, Vh, y, SNR, x, sym, idx) = case_inputs(name)
-        mv = lambda t: t.to(device).contiguous()  # noqa: E731
-        det = VAMP(cfg, engine=nat.ENGINE_LAUNCHES)
-        L = det(mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
+        algo, cfg, args = case_inputs(name)
+        mv = lambda t: t.to(device).contiguous() if isinstance(t, torch.Tensor) else t  # noqa: E731
+        det = VAMP(cfg, engine=nat.ENGINE_LAUNCHES) if algo == 'vamp' else BAMP(cfg)
+        L = det(*(mv(a) for a in args))
         whole = dict(L.loss)
-        r_whole = det.last.r.cpu().numpy()
+        r_whole = (det.last.r if algo == 'vamp' else det.last.xmap).cpu().numpy()
         for r in range(world):
             o = outs[r][name]
             assert int(o['T']) == int(whole['T']), (name, r, o['T'], whole['T'])
