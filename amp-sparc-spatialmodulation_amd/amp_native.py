@@ -106,6 +106,7 @@ SIGNATURES = {
     'amp_set_allreduce_hook': (C.c_int, [_P, _P]),
     'amp_vamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
     'amp_bamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _I, _P]),
+    'amp_scamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _I, _P]),
     'amp_map_decide_count_rows': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, C.c_int64, _P, _P, _P, C.c_size_t, _P]),
     'amp_vamp_detect_count_epochs': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
                                                _P]),

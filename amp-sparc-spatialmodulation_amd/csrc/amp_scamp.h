@@ -62,6 +62,7 @@ struct ScampK {
     // tile of WA (128 wide) / WAH (bn wide) the reduction range holding its nonzero blocks
     const int* bandA;
     const int* bandB;
+    XState* xs;            // trial-sharded exchange words (amp_scamp_run_sharded)
     Const c;
 };
 
@@ -76,6 +77,7 @@ struct ScampWs {
     Partial* pparts;
     double* pxch;
     int *bandA, *bandB;
+    XState* xs;
     size_t bytes;
 };
 
@@ -121,6 +123,7 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);
     w.bandA = cv.take<int>((size_t)2 * (P.ncpA / 128));
     w.bandB = cv.take<int>((size_t)2 * (P.ncpB / P.bn));
+    w.xs = cv.take<XState>(1);
     w.bytes = cv.off;
     return w;
 }

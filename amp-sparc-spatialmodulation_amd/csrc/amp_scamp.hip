@@ -346,6 +346,115 @@ __global__ __launch_bounds__(AMP_WG) void scamp_fin(ScampK P, int t, int nfix) {
     if (threadIdx.x == 0) scamp_finish(P, t, (uint32_t)((int)pend.notclose + dnc), fixed, 0);
 }
 
+// ---- trial-sharded iteration (amp_scamp_run_sharded; SURVEY §8(e) exact-compat) ----
+// scamp_r / scamp_fin split at their batch-global values, as the VAMP and BAMP stages: the
+// denoiser's max|xi| / min section max (scamp.py:64) and the psi allclose count (scamp.py:105)
+// after sxr1, the rare path's exact max|xi| after sxr2 (scamp_fix_sec / scamp_fix_psi then
+// recompute this rank's sections and psi), the fix-up counts after sxr4.
+__global__ __launch_bounds__(SRWG) void scamp_sxr1(ScampK P, int t) {
+    __shared__ __attribute__((aligned(16))) float lds[512];
+    __shared__ unsigned s_u[SRWG / 64];
+    XState* xs = P.xs;
+    if (P.iters[t].stopped) {
+        if (threadIdx.x == 0) { xs->sum[0] = xs->sum[1] = 0.0; xs->mx[0] = xs->mx[1] = 0.0; }
+        return;
+    }
+    PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
+    if (P.psi_split) {
+        unsigned nc = 0;
+        for (int i = threadIdx.x; i < P.psi_nblk; i += blockDim.x) nc += P.psi_nc[(size_t)t * P.psi_nblk + i];
+        pa.notclose += block_sum_u32(nc, s_u);
+    }
+    if (threadIdx.x == 0) {
+        xs->sum[0] = 0.0;
+        xs->sum[1] = (double)pa.notclose;
+        xs->mx[0] = (pa.maxabs <= 1.7976931348623157e308) ? pa.maxabs : INFINITY;   // NaN / inf wins
+        xs->mx[1] = (pa.minsecmax == pa.minsecmax) ? -pa.minsecmax : INFINITY;
+    }
+}
+
+__global__ __launch_bounds__(SRWG) void scamp_sxr2(ScampK P, Const64 c64, int t) {
+    __shared__ double s_d[SRWG / 64];
+    XState* xs = P.xs;
+    const ScampIter cur = P.iters[t];
+    if (cur.stopped) {
+        if (threadIdx.x == 0) { P.iters[t + 1] = cur; xs->mode = 0; xs->gmax[0] = 0.0; }
+        return;
+    }
+    PartAcc pa;
+    pa.notclose = (uint32_t)xs->sum[1];
+    pa.maxabs = xs->mx[0];
+    pa.minsecmax = -xs->mx[1];
+    if (part_allnan(pa)) {
+        if (!cur.fixed_all) {
+            nan_fill(P.xm, nullptr, (size_t)P.B * P.N);
+            float* psi_new = spsi(P, t);
+            for (int e = threadIdx.x; e < P.B * P.Lin; e += blockDim.x) psi_new[e] = __int_as_float(0x7fc00000);
+        }
+        if (threadIdx.x == 0) { scamp_finish(P, t, 1u, -1, 1); xs->mode = 0; xs->gmax[0] = 0.0; }
+    } else if (part_danger(pa)) {
+        // this rank's exact float64 max |xi| over its candidate sections (scamp_r's first stage)
+        const double slack = logit_slack(pa.maxabs);
+        const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+        const float* tau = P.tau;
+        const int M = P.M, L = P.L, N = P.N, Nt = P.Nt, Lin = P.Lin;
+        double gm = 0.0;
+        for (int sct = threadIdx.x; sct < P.B * L; sct += blockDim.x) {
+            if ((double)P.secabs[sct] < pa.maxabs - slack) continue;
+            const size_t o0 = (size_t)sct * M;
+            const int b = sct / L, lc = (int)((o0 % (size_t)N) / Nt);
+            const float tv = tau[(size_t)b * Lin + lc];
+            gm = fmax(gm, section_absmax_f64([=](int m, float& rr, float& ri, float& it) {
+                const float2 v = xp2[o0 + m];
+                rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
+            }, M, c64));
+        }
+        gm = group_max(gm, 64);
+        if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double G = 0.0;
+            for (int w = 0; w < SRWG / 64; ++w) G = fmax(G, s_d[w]);
+            xs->gmax[0] = G;
+            xs->mode = 2;
+            ScampIter nx;   // pending record: G is set to the global value by scamp_sxr3
+            nx.stopped = 0; nx.T = t + 1; nx.fixed = 0; nx.fixed_all = 0;
+            nx.G = G; nx.slack = slack; nx.notclose = pa.notclose; nx.active = 1; nx.pad[0] = nx.pad[1] = 0;
+            P.iters[t + 1] = nx;
+        }
+    } else if (threadIdx.x == 0) {
+        scamp_finish(P, t, pa.notclose, 0, 0);
+        xs->mode = 0;
+        xs->gmax[0] = 0.0;
+    }
+}
+
+__global__ void scamp_sxr3(ScampK P, int t) {   // the global exact G into the pending record
+    if (threadIdx.x == 0 && P.xs->mode == 2) P.iters[t + 1].G = P.xs->gmax[0];
+}
+
+__global__ __launch_bounds__(AMP_WG) void scamp_sxr4(ScampK P, int t, int nfix) {   // this rank's fix-up counts
+    __shared__ int s_i[AMP_WG / 64];
+    XState* xs = P.xs;
+    if (xs->mode != 2) {
+        if (threadIdx.x == 0) xs->fix[0] = xs->fix[1] = xs->fix[2] = 0.0;
+        return;
+    }
+    const int2* c = scamp_fix_counts(P, t);
+    int fixed = 0, dnc = 0;
+    for (int i = threadIdx.x; i < nfix; i += blockDim.x) { fixed += c[i].x; dnc += c[i].y; }
+    fixed = block_sum_int(fixed, s_i);
+    dnc = block_sum_int(dnc, s_i);
+    if (threadIdx.x == 0) { xs->fix[0] = 0.0; xs->fix[1] = (double)dnc; xs->fix[2] = (double)fixed; }
+}
+
+__global__ void scamp_sxr5(ScampK P, int t) {
+    const XState* xs = P.xs;
+    if (threadIdx.x != 0 || xs->mode != 2) return;
+    const long long nc = (long long)xs->sum[1] + (long long)xs->fix[1];
+    scamp_finish(P, t, (uint32_t)nc, (int)xs->fix[2], 0);
+}
+
 // Tracker (scamp.py:9-25): z = y, psi = 1, phi = inf, xmmse = 0
 __global__ void scamp_init_kernel(ScampK P) {
     const size_t BN_ = (size_t)P.B * P.N, Bn = (size_t)P.B * P.n, BL = (size_t)P.B * P.Lout;
@@ -471,6 +580,7 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     const bool band = (d->Lin > 1 || d->Lout > 1) && band_gemm_enabled();
     P.bandA = band ? w.bandA : nullptr;
     P.bandB = band ? w.bandB : nullptr;
+    P.xs = w.xs;
     P.y = (const float*)a->y; P.z = w.z; P.s = w.s; P.phi = w.phi; P.tau = w.tau;
     P.xmap = (float*)a->xmap; P.xm = (float*)a->xmmse; P.psi0 = (float*)a->psi; P.psi1 = w.psi1;
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
@@ -542,6 +652,32 @@ static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStr
     return AMP_OK;
 }
 
+static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hipStream_t st) {
+    const int gr = cdiv(P.B, GBM);
+    const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
+    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
+    hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_kb(P, gr, ldsB, t, st);
+    if (P.psi_split) hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
+    hipLaunchKernelGGL(scamp_sxr1, dim3(1), dim3(SRWG), 0, st, P, t);
+    AMP_LAUNCH_CHECK("scamp_sxr1");
+    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
+    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(scamp_sxr2, dim3(1), dim3(SRWG), 0, st, P, c64, t);
+    AMP_LAUNCH_CHECK("scamp_sxr2");
+    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hipLaunchKernelGGL(scamp_sxr3, dim3(1), dim3(64), 0, st, P, t);
+    hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
+    hipLaunchKernelGGL(scamp_sxr4, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
+    AMP_LAUNCH_CHECK("scamp_sxr4");
+    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hipLaunchKernelGGL(scamp_sxr5, dim3(1), dim3(64), 0, st, P, t);
+    AMP_LAUNCH_CHECK("scamp_sxr5");
+    return AMP_OK;
+}
+
 static int scamp_finalize_impl(const ScampK& P, hipStream_t st) {
     hipLaunchKernelGGL(scamp_output_kernel, dim3(64), dim3(256), 0, st, P);
     AMP_LAUNCH_CHECK("scamp_output");
@@ -558,6 +694,20 @@ int amp_scamp_select_engine(const amp_dims* d, int32_t engine) {
     if (engine == AMP_ENGINE_PERSISTENT) return elig ? AMP_ENGINE_PERSISTENT : AMP_E_ARG;
     if (engine == AMP_ENGINE_AUTO && elig) return AMP_ENGINE_PERSISTENT;
     return engine == AMP_ENGINE_AUTO || engine == AMP_ENGINE_LAUNCHES ? AMP_ENGINE_LAUNCHES : AMP_E_ARG;
+}
+
+int amp_scamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a,
+                          int32_t B_global, void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(allreduce_hook_set(), "amp_scamp_run_sharded: no all-reduce hook registered (amp_set_allreduce_hook)");
+    AMP_REQUIRE(B_global >= d->B, "amp_scamp_run_sharded: B_global = %d < this rank's B = %d", B_global, d->B);
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = scamp_prepare_impl(P, a, st))) return rc;
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = scamp_iterate_sharded(P, c64, t, st);
+    return rc ? rc : scamp_finalize_impl(P, st);
 }
 
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {

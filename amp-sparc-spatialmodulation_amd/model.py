@@ -72,7 +72,7 @@ class Model(nn.Module):
         one persistent launch (VAMP.forward_epochs; same results, fills the GPU at small B).
         shard (with torch.distributed): 'epochs' (default) gives each rank whole epochs with its
         own random stream and merges the metrics once per SNR point; 'trials' (SURVEY §8(e)
-        exact-compat, VAMP and BAMP) gives every rank the SAME epochs (one seed) and splits each batch's
+        exact-compat, VAMP / BAMP / SCAMP) gives every rank the SAME epochs (one seed) and splits each batch's
         trials over the ranks with the batch scalars all-reduced every iteration (ShardedVAMP),
         so the sweep equals the single-process sweep."""
         super().__init__()
@@ -83,16 +83,17 @@ class Model(nn.Module):
         self.min_snr = self.shannon_limit
         if shard not in ('epochs', 'trials'):
             raise ValueError(f"shard must be 'epochs' or 'trials', got {shard!r}")
-        if shard == 'trials' and detector not in ('vamp', 'bamp'):
-            raise ValueError("shard='trials' is built for the VAMP and BAMP detectors")
         self.shard = shard
         if amp is None and shard == 'trials':
             if detector == 'vamp':
                 from vamp import ShardedVAMP
                 amp = ShardedVAMP(config)
-            else:
+            elif detector == 'bamp':
                 from bamp import ShardedBAMP
                 amp = ShardedBAMP(config)
+            else:
+                from scamp import ShardedSCAMP
+                amp = ShardedSCAMP(config)
         self.amp = amp if amp is not None else _detector(detector, config)
         self.loss = Loss(config)
         self.rng = rng

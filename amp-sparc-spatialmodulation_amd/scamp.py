@@ -17,7 +17,7 @@ from torch import nn
 import amp_native as nat
 from config import Config
 from loss import Loss
-from vamp import LazyResult, _c64, block_denoise
+from vamp import LazyResult, ShardHook, _c64, block_denoise
 
 
 class _Buffers:
@@ -177,3 +177,57 @@ class SCAMP(LazyResult, nn.Module):
         self._keep = T
         self.last = T
         return self.L
+
+
+class ShardedSCAMP(ShardHook, SCAMP):
+    """SURVEY §8(e) exact-compat mode for SCAMP: ONE batch split over the ranks of
+    torch.distributed (rank r detects trials [r B / P, (r + 1) B / P)).  ``forward`` keeps
+    SCAMP.forward's signature and takes the whole batch's inputs (replicated from one seed); the
+    rank runs its slice through amp_scamp_run_sharded (launch engine), whose hook all-reduces the
+    batch-global values of every iteration (the denoiser's max |xi| shift, scamp.py:64; the psi
+    allclose count, scamp.py:105; the rare path's exact values), decides its rows on xmap
+    (scamp.py:107) and merges the counters with ONE all-reduce."""
+
+    def __init__(self, config: Config, group=None) -> None:
+        super().__init__(config)
+        self._shard_init(group)
+
+    def forward(self, W: torch.Tensor, A: torch.Tensor, y: torch.Tensor, SNR: float, x: torch.Tensor, symbol,
+                index) -> Loss:
+        with torch.cuda.device(y.device):
+            return self._forward_sharded(W, A, y, SNR, x, symbol, index)
+
+    def _forward_sharded(self, W, A, y, SNR, x, symbol, index) -> Loss:
+        cfg = self.config
+        B = cfg.B
+        b0, b1 = self.shard()
+        Bl = b1 - b0
+        n, N = A.shape[-2], A.shape[-1]
+        dev = y.device
+        Ac = _c64(A, (n, N))
+        yl = _c64(y, (B, n))[b0:b1].contiguous()
+        Wc = W.reshape(cfg.Lout, cfg.Lin).to(device=dev, dtype=torch.float32).resolve_neg().contiguous()
+        d, cst = cfg.dims(batch=Bl), cfg.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_scamp_workspace_bytes(C.byref(d), cfg.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_scamp_workspace_bytes: invalid dimensions')
+        self._ws = nat.WORKSPACE.get(dev, 'scamp_sharded', wsb)
+        xmap = torch.empty(Bl, N, dtype=torch.complex64, device=dev)
+        xm = torch.empty_like(xmap)
+        psi = torch.empty(Bl, cfg.Lin, dtype=torch.float32, device=dev)
+        res = torch.zeros(256, dtype=torch.uint8, device=dev)      # amp_status @0, amp_counts @64
+        a = nat.AmpScampArgs()
+        a.W, a.A, a.y = nat.dptr(Wc, torch.float32, 'W'), nat.dptr(Ac, name='A'), nat.dptr(yl, name='y')
+        a.max_iter = cfg.N_Layers
+        a.engine = nat.ENGINE_LAUNCHES
+        a.noise_var = float(self.E / SNR)                                  # scamp.py:98
+        a.xmap, a.xmmse, a.psi = nat.dptr(xmap), nat.dptr(xm), nat.dptr(psi)
+        a.status = nat.dptr(res)
+        a.ws, a.ws_bytes = nat.dptr(self._ws), self._ws.numel()
+        st = nat.stream_ptr(dev)
+        self._run_hooked(lib.amp_scamp_run_sharded, 'amp_scamp_run_sharded', C.byref(d), C.byref(cst), C.byref(a), B,
+                         st)
+        L = self._decide_merge(d, cst, xmap, xm, x, symbol, index, b0, b1, res, st)
+        self.last_shard = (xmap.view(Bl, N, 1), xm.view(Bl, N, 1), psi.view(Bl, cfg.Lin, 1))
+        return L

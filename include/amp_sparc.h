@@ -262,6 +262,12 @@ size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
  *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
 int amp_scamp_select_engine(const amp_dims* d, int32_t engine);
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+/* amp_scamp_run (launch engine) on one rank's slice of a trial-sharded batch (the protocol of
+ * amp_vamp_run_sharded, the hook of amp_set_allreduce_hook): max|xi| / min section max
+ * (scamp.py:64), the psi allclose count (scamp.py:105) and the rare path's exact values
+ * all-reduced per iteration; decision on xmap with amp_map_decide_count_rows. */
+int amp_scamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a,
+                          int32_t B_global, void* stream);
 /* Layer-level pieces of amp_scamp_run, as for BAMP: prepare = Tracker (scamp.py:9-25), iterate(t)
  * = one SCAMPLayer.forward (scamp.py:43-59) + the allclose(psi) early exit of scamp.py:105,
  * finalize = the last psi into a->psi. */

@@ -13,23 +13,24 @@ import torch  # noqa: E402
 
 
 def case_inputs(name):
-    """CASE = [bamp:|bampisi:]alphabet:EbN0:B[:yscale] — VAMP / BAMP at the cfg2 shape (Nt=64 Na=4
-    Nr=128), or BAMP at a small ISI shape (Nt=32 Na=4 Nr=32 Lin=4 Lh=2: banded GEMMs); host
+    """CASE = [bamp:|bampisi:|scampisi:]alphabet:EbN0:B[:yscale] — VAMP / BAMP at the cfg2 shape
+    (Nt=64 Na=4 Nr=128), or BAMP / SCAMP at a small ISI shape (Nt=32 Na=4 Nr=32 Lin=4 Lh=2:
+    banded GEMMs); host
     replica, seed 7.  Returns (detector, cfg, forward arguments)."""
     from channel import Channel
     from config import Config
     from data import Data
     f = name.split(':')
-    algo = f.pop(0) if f[0] in ('bamp', 'bampisi') else 'vamp'
+    algo = f.pop(0) if f[0] in ('bamp', 'bampisi', 'scampisi') else 'vamp'
     alph, ebn0, B = f[0], float(f[1]), int(f[2])
     scale = float(f[3]) if len(f) > 3 else 1.0
-    shape = (32, 4, 32, 4, 2) if algo == 'bampisi' else (64, 4, 128, 1, 1)
+    shape = (32, 4, 32, 4, 2) if algo in ('bampisi', 'scampisi') else (64, 4, 128, 1, 1)
     cfg = Config(*shape, batch=B, generator_mode='sparc', iterations=20, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cpu')
     np.random.seed(7)
     torch.manual_seed(7)
     ch, da = Channel(cfg), Data(cfg)
-    _, A = ch.generate_as_sparc()
+    Wc, A = ch.generate_as_sparc()
     x, sym, idx = da.generate_message()
     SNR = cfg.snr(ebn0)
     y = (A @ x + ch.awgn(SNR)) * scale
@@ -37,6 +38,8 @@ def case_inputs(name):
     if algo == 'vamp':
         U, s, Vh = torch.linalg.svd(A, full_matrices=False)
         return 'vamp', cfg, (U, s, Vh, y, SNR, x, sym, idx)
+    if algo == 'scampisi':
+        return 'scamp', cfg, (Wc, A, y, SNR, x, sym, idx)
     return 'bamp', cfg, (A, y, SNR, x, sym, idx)
 
 
@@ -46,12 +49,13 @@ def main():
                                          world_size=world)
     try:
         from bamp import ShardedBAMP
+        from scamp import ShardedSCAMP
         from vamp import ShardedVAMP
         dev = torch.device('cuda:0')
         res = {}
         for name in sys.argv[5:]:
             algo, cfg, args = case_inputs(name)
-            det = ShardedVAMP(cfg) if algo == 'vamp' else ShardedBAMP(cfg)
+            det = {'vamp': ShardedVAMP, 'bamp': ShardedBAMP, 'scamp': ShardedSCAMP}[algo](cfg)
             mv = lambda t: t.to(dev).contiguous() if isinstance(t, torch.Tensor) else t  # noqa: E731
             L = det(*(mv(a) for a in args))
             res[name] = {k: (float(v) if np.ndim(v) == 0 else np.asarray(v).tolist()) for k, v in L.loss.items()}

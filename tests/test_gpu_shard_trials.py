@@ -1,5 +1,6 @@
 """GPU: trial sharding across ranks (SURVEY §8(e) exact-compat mode; ShardedVAMP /
-amp_vamp_run_sharded, ShardedBAMP / amp_bamp_run_sharded incl. an ISI shape on the banded GEMMs).  2 and 3 rank processes on the one GPU, gloo process group (the hook
+amp_vamp_run_sharded, ShardedBAMP / amp_bamp_run_sharded, ShardedSCAMP / amp_scamp_run_sharded,
+incl. ISI shapes on the banded GEMMs).  2 and 3 rank processes on the one GPU, gloo process group (the hook
 all-reduces the batch scalars through host memory; RCCL is the same hook on the device words).
 
 Bar: every rank's Loss equals the single-process whole-batch forward's — T exact, VER / SER /
@@ -24,7 +25,8 @@ sys.path.insert(0, HERE)
 from shard_trials_worker import case_inputs  # noqa: E402
 
 CASES = ['16QAM:8:1024', 'QPSK:4:1024', '16QAM:20:1024', 'QPSK:12:1000', '16QAM:14:1024:40',
-         'bamp:QPSK:6:1024', 'bamp:16QAM:12:1000', 'bamp:16QAM:20:1024', 'bampisi:QPSK:6:256']
+         'bamp:QPSK:6:1024', 'bamp:16QAM:12:1000', 'bamp:16QAM:20:1024', 'bampisi:QPSK:6:256',
+         'scampisi:QPSK:6:256', 'scampisi:16QAM:12:500', 'scampisi:16QAM:24:256']
 
 
 def _free_port():
@@ -47,10 +49,12 @@ def test_sharded_equals_whole_batch(device, tmp_path, world):
     assert rcs == [0] * world, rcs
     outs = [json.load(open(tmp_path / f'rank{r}.json')) for r in range(world)]
     from bamp import BAMP
+    from scamp import SCAMP
     for name in CASES:
         algo, cfg, args = case_inputs(name)
         mv = lambda t: t.to(device).contiguous() if isinstance(t, torch.Tensor) else t  # noqa: E731
-        det = VAMP(cfg, engine=nat.ENGINE_LAUNCHES) if algo == 'vamp' else BAMP(cfg)
+        det = {'vamp': lambda: VAMP(cfg, engine=nat.ENGINE_LAUNCHES), 'bamp': lambda: BAMP(cfg),
+               'scamp': lambda: SCAMP(cfg, engine=nat.ENGINE_LAUNCHES)}[algo]()
         L = det(*(mv(a) for a in args))
         whole = dict(L.loss)
         r_whole = (det.last.r if algo == 'vamp' else det.last.xmap).cpu().numpy()
