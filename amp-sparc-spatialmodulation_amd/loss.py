@@ -36,15 +36,17 @@ def vector_to_counts(v):
     return c
 
 
-def allreduce_counts(vec: np.ndarray) -> np.ndarray:
+def allreduce_counts(vec: np.ndarray, group=None) -> np.ndarray:
     """Sum the per-rank counter vectors with ONE all-reduce (RCCL on the rank's GPU for the
-    'nccl' backend, host memory for gloo); identity without torch.distributed."""
+    'nccl' backend, host memory for gloo) over `group` (default: the world); identity without
+    torch.distributed."""
     dist = torch.distributed
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return np.asarray(vec, dtype=np.float64)
-    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else torch.device('cpu')
+    dev = (torch.device('cuda', torch.cuda.current_device()) if dist.get_backend(group) == 'nccl'
+           else torch.device('cpu'))
     t = torch.as_tensor(np.asarray(vec, dtype=np.float64)).to(dev)
-    dist.all_reduce(t)
+    dist.all_reduce(t, group=group)
     return t.cpu().numpy()
 
 

@@ -405,6 +405,8 @@ class ShardHook:
             off = int(buf) - ws.data_ptr()
             if off < 0 or off + 8 * count > ws.numel():
                 raise ValueError(f'hook buffer outside the workspace (offset {off})')
+            if not (dist.is_available() and dist.is_initialized()):
+                return 0                       # one process: the reduction over one rank is the identity
             view = ws[off:off + 8 * count].view(torch.float64)
             rop = dist.ReduceOp.SUM if op == nat.ALLREDUCE_SUM else dist.ReduceOp.MAX
             if view.device.type == 'cuda' and dist.get_backend(self.group) == 'nccl':
@@ -453,7 +455,7 @@ class ShardHook:
         raw = res.cpu().numpy().tobytes()
         status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
         counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
-        merged = vector_to_counts(allreduce_counts(counts_to_vector(counts)))   # the ONE counter all-reduce
+        merged = vector_to_counts(allreduce_counts(counts_to_vector(counts), self.group))   # the ONE counter all-reduce
         self.L.resolve()
         self.L.dump()
         self.L.last_counts, self.L.last_status = merged, status

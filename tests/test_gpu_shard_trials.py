@@ -70,3 +70,24 @@ def test_sharded_equals_whole_batch(device, tmp_path, world):
         if fin.any():
             frac = float(np.mean(np.abs(rs[fin] - r_whole[fin]) > 1e-4 * max(1.0, float(np.abs(r_whole[fin]).max()))))
             assert frac <= 0.01, (name, frac)
+
+
+@pytest.mark.parametrize('name', ['16QAM:8:1024', 'bamp:QPSK:6:1024', 'scampisi:16QAM:12:500'])
+def test_sharded_single_process_is_whole_batch(device, name):
+    """Without torch.distributed the sharded detectors hold the whole batch and the hook is the
+    identity: the Loss equals the plain forward's exactly."""
+    import amp_native as nat
+    from bamp import BAMP, ShardedBAMP
+    from scamp import SCAMP, ShardedSCAMP
+    from vamp import VAMP, ShardedVAMP
+    assert not (torch.distributed.is_available() and torch.distributed.is_initialized())
+    algo, cfg, args = case_inputs(name)
+    mv = lambda t: t.to(device).contiguous() if isinstance(t, torch.Tensor) else t  # noqa: E731
+    plain = {'vamp': lambda: VAMP(cfg, engine=nat.ENGINE_LAUNCHES), 'bamp': lambda: BAMP(cfg),
+             'scamp': lambda: SCAMP(cfg, engine=nat.ENGINE_LAUNCHES)}[algo]()
+    shard = {'vamp': ShardedVAMP, 'bamp': ShardedBAMP, 'scamp': ShardedSCAMP}[algo](cfg)
+    a = dict(plain(*(mv(x) for x in args)).loss)
+    b = dict(shard(*(mv(x) for x in args)).loss)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), (k, a[k], b[k])
