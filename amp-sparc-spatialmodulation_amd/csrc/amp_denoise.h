@@ -435,6 +435,158 @@ __device__ __forceinline__ void denoise_step_grid(const P& pol, int base, int ns
     }
 }
 
+// denoise_step_grid with U = 2 written on float pairs (one element per section in flight): the
+// same operations in the same order per element — bit-identical results — issued as packed
+// v_pk_mul / v_pk_add / v_pk_fma (two positions per instruction); max / min, exp, rcp and the
+// DPP reductions stay per element.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v f2fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v f2splat(float v) { return f2v{v, v}; }
+
+template <bool kVar, int R, int PAT, int G, class P>
+__device__ __forceinline__ void denoise_step_grid2(const P& pol, int base, int nsec, const GridRegs<R>& Q,
+                                                   PartAcc& pa, DenStat& S) {
+    constexpr bool FULLG = PAT == GRID_FULL;
+    const int lane = threadIdx.x & 63;
+    constexpr int gpw = 64 / G;
+    const int gid = lane / G, g = lane % G;
+    int sec[2];
+    bool act[2];
+    f2v ur, ui;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        sec[u] = base + u * gpw + gid;
+        act[u] = sec[u] < nsec;
+        float rr, ri, it;
+        pol.load(act[u] ? sec[u] : nsec - 1, g, rr, ri, it);
+        ur[u] = rr * it;   // c64 / f32 == multiply by the reciprocal
+        ui[u] = ri * it;
+        S.st_bad |= act[u] && !(fabsf(ur[u]) <= FLT_MAX && fabsf(ui[u]) <= FLT_MAX);
+    }
+    f2v X[R], Y[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        X[i] = ur * f2splat(Q.re[i]);
+        Y[i] = ui * f2splat(Q.im[i]);
+    }
+    f2v mx, my, lmx, smax, sabs;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float ax = -FLT_MAX, nx = FLT_MAX, ay = -FLT_MAX, ny = FLT_MAX;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            ax = fmaxf(ax, X[i][u]); nx = fminf(nx, X[i][u]);
+            ay = fmaxf(ay, Y[i][u]); ny = fminf(ny, Y[i][u]);
+        }
+        mx[u] = ax; my[u] = ay;
+        lmx[u] = ax + ay;                          // max logit of the position (a corner)
+        smax[u] = group_fmax_c<G>(lmx[u]);
+        sabs[u] = group_fmax_c<G>(fmaxf(lmx[u], -(nx + ny)));   // max |logit|
+    }
+    const f2v l2e = f2splat(AMP_LOG2E);
+    f2v targ = (lmx - smax) * l2e;
+    f2v f = {__builtin_amdgcn_exp2f(targ.x), __builtin_amdgcn_exp2f(targ.y)};
+    f2v er[R], ei[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const f2v xa = (X[i] - mx) * l2e, ya = (Y[i] - my) * l2e;
+        er[i] = f2v{__builtin_amdgcn_exp2f(xa.x), __builtin_amdgcn_exp2f(xa.y)};
+        ei[i] = f2v{__builtin_amdgcn_exp2f(ya.x), __builtin_amdgcn_exp2f(ya.y)};
+    }
+    f2v zt, ar, ai, SI = f2splat(0.f);
+    f2v Sr[FULLG ? 1 : R];
+    if constexpr (FULLG) {
+        f2v sr = f2splat(0.f), si = f2splat(0.f), a = f2splat(0.f), b = f2splat(0.f);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            sr += er[i]; si += ei[i];
+            a = f2fma(f2splat(Q.re[i]), er[i], a);
+            b = f2fma(f2splat(Q.im[i]), ei[i], b);
+        }
+        SI = si; Sr[0] = sr;
+        zt = (sr * si) * f;
+        ar = (a * si) * f;
+        ai = (sr * b) * f;
+    } else {
+        f2v z = f2splat(0.f), a = f2splat(0.f), b = f2splat(0.f), w[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) w[j] = f2splat(Q.im[j]) * ei[j];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            f2v si = f2splat(0.f), ti = f2splat(0.f);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const float cw = grid_cnt<PAT>(i, j);
+                if (cw == 1.f) { si += ei[j]; ti += w[j]; }
+                else if (cw == 2.f) { si = f2fma(f2splat(2.f), ei[j], si); ti = f2fma(f2splat(2.f), w[j], ti); }
+            }
+            Sr[i] = si;
+            const f2v es = er[i] * si;
+            z += es;
+            a = f2fma(f2splat(Q.re[i]), es, a);
+            b = f2fma(er[i], ti, b);
+        }
+        zt = z * f;
+        ar = a * f;
+        ai = b * f;
+    }
+    float ze[2] = {0.f, 0.f}, zt1[2] = {zt.x, zt.y};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) group_sum_excl_c<G>(zt1[u], ze[u]);
+    const f2v iz = {__builtin_amdgcn_rcpf(zt1[0]), __builtin_amdgcn_rcpf(zt1[1])};
+    const f2v xr = ar * iz, xi = ai * iz;
+    f2v var = f2splat(0.f);
+    if (kVar) {
+        f2v vs;
+        if constexpr (FULLG) {
+            f2v vr = f2splat(0.f), vi = f2splat(0.f);
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const f2v dr = xr - f2splat(Q.re[i]), di = xi - f2splat(Q.im[i]);
+                vr = f2fma(dr * dr, er[i], vr);
+                vi = f2fma(di * di, ei[i], vi);
+            }
+            vs = f2fma(vr, SI, Sr[0] * vi) * f;
+        } else {
+            f2v d[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const f2v di = xi - f2splat(Q.im[j]);
+                d[j] = (di * di) * ei[j];
+            }
+            f2v acc = f2splat(0.f);
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                f2v vi = f2splat(0.f);
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    const float cw = grid_cnt<PAT>(i, j);
+                    if (cw == 1.f) vi += d[j];
+                    else if (cw == 2.f) vi = f2fma(f2splat(2.f), d[j], vi);
+                }
+                const f2v dr = xr - f2splat(Q.re[i]);
+                acc = f2fma(er[i], f2fma(dr * dr, Sr[i], vi), acc);
+            }
+            vs = acc * f;
+        }
+        const f2v zev = {ze[0], ze[1]};
+        var = (xr * xr + xi * xi) * (zev * iz) + vs * iz;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        if (act[u]) {
+            pol.store(sec[u], g, xr[u], xi[u], var[u], pa);
+            S.st_abs = nan_max(S.st_abs, sabs[u]);
+            S.st_min = nan_min(S.st_min, smax[u]);
+            if (g == 0) pol.section(sec[u], smax[u], sabs[u]);
+        }
+    }
+}
+
+#ifndef AMP_DEN_PACKED_GRID
+#define AMP_DEN_PACKED_GRID 1
+#endif
+
 // Grid dimension of a compile-time constellation size (0: no product-grid form).
 template <int KK>
 constexpr int grid_r() { return KK == 4 ? 2 : KK == 16 ? 4 : KK == 64 ? 8 : 0; }
@@ -456,11 +608,19 @@ __device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, co
         GridRegs<R> Q;
         Q.load(c);
         if (gfull == GRID_FULL) {
-            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U)   // wave-uniform trip count
-                denoise_step_grid<kVar, R, GRID_FULL, U, G>(pol, base, nsec, Q, pa, S);
+            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {   // wave-uniform trip count
+                if constexpr (U == 2 && AMP_DEN_PACKED_GRID)
+                    denoise_step_grid2<kVar, R, GRID_FULL, G>(pol, base, nsec, Q, pa, S);
+                else
+                    denoise_step_grid<kVar, R, GRID_FULL, U, G>(pol, base, nsec, Q, pa, S);
+            }
         } else if constexpr (R == 4) {
-            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U)
-                denoise_step_grid<kVar, R, GRID_REF16, U, G>(pol, base, nsec, Q, pa, S);
+            for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {
+                if constexpr (U == 2 && AMP_DEN_PACKED_GRID)
+                    denoise_step_grid2<kVar, R, GRID_REF16, G>(pol, base, nsec, Q, pa, S);
+                else
+                    denoise_step_grid<kVar, R, GRID_REF16, U, G>(pol, base, nsec, Q, pa, S);
+            }
         }
         S.fold(pa);
         return true;
