@@ -373,14 +373,14 @@ class VAMP(LazyResult, nn.Module):
 
     def _epochs_slot(self, device, nbytes):
         """One of two (device, pinned host) result buffers for forward_epochs, alternating per
-        call, so a call's records stay readable while the next call runs."""
+        call, so a call's records stay readable while the next call runs.  Not cleared: the
+        engine writes every epoch's status and counter record whole."""
         if self._epochs_ring is None or self._epochs_ring[0][0].device != device or \
                 self._epochs_ring[0][0].numel() < nbytes:
             self._epochs_ring = [(torch.zeros(nbytes, dtype=torch.uint8, device=device),
                                   torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)) for _ in range(2)]
         self._epochs_i ^= 1
         d, h = self._epochs_ring[self._epochs_i]
-        d.zero_()
         return d[:nbytes], h[:nbytes]
 
 
