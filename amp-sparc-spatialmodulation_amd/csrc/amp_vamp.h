@@ -55,7 +55,7 @@ struct VampK {
     const float2* xtrue;        // [B][N] transmitted x
     const long long* sym;       // [B*L] gray labels
     const long long* idx;       // [B*L] flat nonzero indices
-    DecWG* dwg;                 // [nwg][DEC_GRANS] tagged per-workgroup records (decide_epilogue)
+    DecWG* dwg;                 // [nwg] per-workgroup records
     amp_counts* counts;         // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
     int x3;                      // persistent engine GEMMs on the bf16x3 engine (Wx1 / Wx2)
@@ -115,7 +115,7 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(PBAR_WORDS);                  // barrier words (zeroed per launch); the
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // granules carry generation tags
-    w.dwg = cv.take<DecWG>((size_t)nwg * 2);                 // DEC_GRANS tagged granules per workgroup
+    w.dwg = cv.take<DecWG>((size_t)nwg);
     w.xs = cv.take<XState>(1);
     w.bytes = cv.off;
     return w;

@@ -36,6 +36,12 @@
 
 namespace amp {
 
+// one workgroup per epoch: epoch e's n per-workgroup records -> out[e]
+__global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out) {
+    __shared__ DecWG s[16];
+    dec_fold_block(w + (size_t)blockIdx.x * n, n, out + blockIdx.x, s);
+}
+
 static std::once_flag g_pers_once;
 static int g_ncu = 0;
 
@@ -89,7 +95,11 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
     (void)ncu;
     DecConst d2 = dc;
     static_cast<Const64&>(d2) = c64;
-    return persist_dispatch(P, d2, st);   // the decision counters are folded inside (decide_epilogue)
+    int rc = persist_dispatch(P, d2, st);
+    if (rc || !P.dec_on) return rc;
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.wpe, P.counts);
+    AMP_LAUNCH_CHECK("vamp_decide_fold");
+    return AMP_OK;
 }
 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) {

@@ -46,92 +46,9 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
     return y;
 }
 
-// A workgroup's decision record as DEC_GRANS 16-byte write-through (sc1) granules: 13 64-bit
-// counters / sums in 26 payload words, three per granule, each granule tagged with the launch
-// generation in its last word (the part_publish scheme, amp_persist.h).
-constexpr int DEC_GRANS = 9;
-
-__device__ __forceinline__ void dec_words(const DecWG& o, unsigned long long (&v)[13]) {
-    v[0] = (unsigned long long)o.p.ier; v[1] = (unsigned long long)o.p.ser;
-    v[2] = (unsigned long long)o.p.iber; v[3] = (unsigned long long)o.p.sber;
-    v[4] = (unsigned long long)__double_as_longlong(o.p.mse); v[5] = (unsigned long long)__double_as_longlong(o.p.msef);
-    v[6] = (unsigned long long)__double_as_longlong(o.p.msem); v[7] = (unsigned long long)__double_as_longlong(o.p.mseL);
-    v[8] = (unsigned long long)o.ver; v[9] = (unsigned long long)o.verf; v[10] = (unsigned long long)o.verm;
-    v[11] = (unsigned long long)o.verL; v[12] = (unsigned long long)o.fer;
-}
-
-__device__ __forceinline__ void dec_publish(const DecWG& o, __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned tag) {
-    unsigned long long v[13];
-    dec_words(o, v);
-    unsigned w[27];
-#pragma unroll
-    for (int i = 0; i < 13; ++i) { w[2 * i] = (unsigned)v[i]; w[2 * i + 1] = (unsigned)(v[i] >> 32); }
-    w[26] = 0u;
-#pragma unroll
-    for (int g = 0; g < DEC_GRANS; ++g) {
-        const u32x4 q = {w[3 * g], w[3 * g + 1], w[3 * g + 2], tag};
-        __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(off + 16u * g), 0, 16);   // aux 16 = sc1
-    }
-}
-
-// One wave sweeps the n (<= 256) records of an epoch, lane l taking records l, l + 64, ... in
-// that order, then the fixed butterfly of group_sum: every launch folds in the same order.  A
-// bounded spin (2 s) raises the abort word, as part_gather does; returns false then.
-__device__ inline bool dec_gather(__amdgpu_buffer_rsrc_t rs, unsigned off0, int n, unsigned tag, unsigned* abort_word,
-                                  DecWG& out) {
-    const int lane = threadIdx.x & 63;
-    unsigned long long acc[13] = {};
-    double dacc[4] = {0.0, 0.0, 0.0, 0.0};
-    bool ok_all = true;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (int r0 = 0; r0 < n; r0 += 64) {
-        const int r = r0 + lane;
-        u32x4 q[DEC_GRANS];
-        for (;;) {
-            bool ok = true;
-            if (r < n) {
-#pragma unroll
-                for (int g = 0; g < DEC_GRANS; ++g) {
-                    q[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off0 + (unsigned)r * DEC_GRANS * 16u + 16u * g),
-                                                                 0, 16);
-                    ok &= q[g].w == tag;
-                }
-            }
-            if (__all(ok)) break;
-            if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                __builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
-                __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok_all = false;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (!ok_all) break;
-        if (r < n) {
-            unsigned w[27];
-#pragma unroll
-            for (int g = 0; g < DEC_GRANS; ++g) { w[3 * g] = q[g].x; w[3 * g + 1] = q[g].y; w[3 * g + 2] = q[g].z; }
-#pragma unroll
-            for (int i = 0; i < 13; ++i) {
-                const unsigned long long v = (unsigned long long)w[2 * i] | ((unsigned long long)w[2 * i + 1] << 32);
-                if (i >= 4 && i < 8) dacc[i - 4] += __longlong_as_double((long long)v);
-                else acc[i] += v;
-            }
-        }
-    }
-    out.p.ier = group_sum((long long)acc[0], 64); out.p.ser = group_sum((long long)acc[1], 64);
-    out.p.iber = group_sum((long long)acc[2], 64); out.p.sber = group_sum((long long)acc[3], 64);
-    out.p.mse = group_sum(dacc[0], 64); out.p.msef = group_sum(dacc[1], 64);
-    out.p.msem = group_sum(dacc[2], 64); out.p.mseL = group_sum(dacc[3], 64);
-    out.ver = group_sum((long long)acc[8], 64); out.verf = group_sum((long long)acc[9], 64);
-    out.verm = group_sum((long long)acc[10], 64); out.verL = group_sum((long long)acc[11], 64);
-    out.fer = group_sum((long long)acc[12], 64);
-    return __all(ok_all);
-}
-
 // Fused MAP decision + error counters (Loss.error_rate, loss.py:67-179, via amp_decide.h) on
 // this workgroup's rows while r (the decision input, vamp.py:187) and xmmse are still in LDS;
-// per-workgroup records, folded by the epoch's first workgroup (dec_publish / dec_gather).
+// per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
 // mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
 // row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
 // (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
@@ -233,34 +150,18 @@ __device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float*
         sw[wave] = w;
     }
     __syncthreads();
-    // The epoch's records meet in its first workgroup through tagged write-through granules, as
-    // the per-iteration partials do (no fence: an agent-scope release writes back the L2 and cost
-    // ~90 us), so no fold launch follows the engine.
-    const __amdgpu_buffer_rsrc_t rs = gran_rsrc(P.dwg, (unsigned)P.nwg * DEC_GRANS * 16u);
-    const unsigned tag = P.gen;
     if (tid == 0) {
         DecWG o = sw[0];
         for (int v = 1; v < PWG / 64; ++v) {
             decpart_add(o.p, sw[v].p);
             o.ver += sw[v].ver; o.verf += sw[v].verf; o.verm += sw[v].verm; o.verL += sw[v].verL; o.fer += sw[v].fer;
         }
-        dec_publish(o, rs, (unsigned)blockIdx.x * DEC_GRANS * 16u, tag);
-    }
-    const int wl = lrow0 / PBM;
-    if (wl == 0 && wave == 0) {
-        const int ep = (row0 - lrow0) / P.B;
-        DecWG f;
-        const bool ok = dec_gather(rs, (unsigned)(ep * P.wpe) * DEC_GRANS * 16u, P.wpe, tag, P.pbar + 1, f);
-        if (lane == 0) {
-            amp_counts c;
-            c.ier = f.p.ier; c.ser = f.p.ser; c.iber = f.p.iber; c.sber = f.p.sber;
-            c.ver = f.ver; c.verf = f.verf; c.verm = f.verm; c.verL = f.verL; c.fer = f.fer;
-            c.mse = f.p.mse; c.msef = f.p.msef; c.msem = f.p.msem; c.mseL = f.p.mseL;
-            P.counts[ep] = c;
-            if (!ok) P.status[ep].nan_state = -1;
-        }
+        P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
+                                 // an agent-scope release writes back the L2 and cost ~90 us)
     }
 }
+
+__global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out);
 
 // dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
 // X3: both per-iteration GEMMs on the split-precision bf16x3 engine (gemm_x3): the A operand
