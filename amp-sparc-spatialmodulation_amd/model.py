@@ -227,8 +227,11 @@ class Model(nn.Module):
             results.append(point)
             if self.rank == 0:
                 print(f'FER={fer}, iter={it}')
-                self.loss.export(SNRdB, EbN0dB, self.path)
-            elif self.shard == 'epochs':
+                self.loss.export(SNRdB, EbN0dB, self.path)   # also clears the totals (loss.py:323)
+            else:
+                # every other rank clears its totals too (both shard modes): its next point must
+                # start from zero, or its FER (and with it the stop decision below, which every
+                # rank takes on the same merged / whole-batch values) would drift from rank 0's
                 self.loss.loss = {'T': 0}
             if fer < 1e-3:
                 break

@@ -98,3 +98,48 @@ def test_simulate_two_ranks_gloo(tmp_path):
     # only rank 0 writes the JSON files
     assert sorted(p for p in os.listdir(tmp_path) if p.endswith('.json') and not p.startswith('rank')) == \
         ['0.0.json', '1.0.json']
+
+
+class FakeShardedAmp(FakeAmp):
+    """Stands in for ShardedVAMP: every rank returns the WHOLE batch's Loss (the same values on
+    every rank), FER 1 below `fer_until_snr` and 0 from there on."""
+
+    def __call__(self, U, s, Vh, y, SNR, x, sym, idx):
+        self.calls += 1
+        fer = 1.0 if SNR < self.fer_until_snr else 0.0
+        self.L.dump()
+        self.L.loss = {'T': 0}
+        self.L.record([fer] + [0.5] * 13, 3)
+        return self.L
+
+
+def _worker_trials(rank, world, port, out):
+    torch.distributed.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                                         world_size=world)
+    try:
+        from model import Model
+        cfg = _cfg()
+        amp = FakeShardedAmp(cfg, fer_until_snr=10 ** ((2 + 10 * np.log10(cfg.code_rate)) / 10))
+        m = Model(cfg, 'vamp', path=out, amp=amp, seed=3, shard='trials')
+        res = m.simulate(epochs=3, start=0, final=6.0, step=1)
+        with open(os.path.join(out, f'rank{rank}.json'), 'w') as f:
+            json.dump({'calls': amp.calls, 'res': res}, f)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_simulate_trial_shard_two_ranks_gloo(tmp_path):
+    """shard='trials' over several SNR points: every rank must clear its totals after each point
+    (only rank 0 did, so the other ranks carried the previous point's averages into
+    the next, their FER never reached the stop and their results differed from rank 0's)."""
+    world = 2
+    mp.start_processes(_worker_trials, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method='spawn')
+    r0 = json.load(open(tmp_path / 'rank0.json'))
+    r1 = json.load(open(tmp_path / 'rank1.json'))
+    # every rank runs every epoch of every point (the detector splits each batch), 3 points, stop
+    assert r0['calls'] == r1['calls'] == 3 * 3
+    assert [p['EbN0dB'] for p in r0['res']] == [0.0, 1.0, 2.0]
+    assert r0['res'] == r1['res']
+    assert [p['fer'] for p in r0['res']] == [1.0, 1.0, 0.0]
