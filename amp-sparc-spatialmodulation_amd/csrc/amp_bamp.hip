@@ -651,7 +651,7 @@ static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStrea
     return AMP_OK;
 }
 
-static int bamp_iterate_sharded(const BampK& P, const Const64& c64, int t, hipStream_t st) {
+static int bamp_iterate_sharded(const BampK& P, const Const64& c64, int t, hipStream_t st, bool& hook_failed) {
     const int gr = cdiv(P.B, GBM);
     hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
     hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
@@ -659,15 +659,16 @@ static int bamp_iterate_sharded(const BampK& P, const Const64& c64, int t, hipSt
     launch_kb2(P, c64, gr, t, st);
     hipLaunchKernelGGL(bamp_xr1, dim3(1), dim3(BRWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("bamp_xr1");
-    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
-    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
-    if (rc) return rc;
+    // every hook call is made on every rank even after one failed: the ranks' collectives stay
+    // matched and a failed rank's poisoned words reach the others (amp_sparc.h)
+    hook_failed |= call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st) != AMP_OK;
+    hook_failed |= call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(bamp_xr2, dim3(1), dim3(BRWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("bamp_xr2");
-    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(bamp_xr3, dim3(1), dim3(BRWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("bamp_xr3");
-    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st) != AMP_OK;
     hipLaunchKernelGGL(bamp_xr4, dim3(1), dim3(64), 0, st, P, t);
     AMP_LAUNCH_CHECK("bamp_xr4");
     return AMP_OK;
@@ -697,7 +698,9 @@ int amp_bamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
                 "batch-global values to share");
     hipStream_t st = (hipStream_t)stream;
     rc = bamp_prepare_impl(P, a, st);
-    for (int t = 0; t < P.max_iter && !rc; ++t) rc = bamp_iterate_sharded(P, c64, t, st);
+    bool hook_failed = false;
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = bamp_iterate_sharded(P, c64, t, st, hook_failed);
+    if (!rc && hook_failed) rc = hook_failure("bamp");
     return rc ? rc : bamp_finalize_impl(P, st);
 }
 

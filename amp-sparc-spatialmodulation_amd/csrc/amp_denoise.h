@@ -161,6 +161,11 @@ struct DenRegs {
     }
 };
 
+// Diagnostic hook (amp_vamp_debug_dump): a policy may record the intermediate ze / vs of the
+// variance; the generic form records nothing.
+template <class P>
+__device__ __forceinline__ void den_debug(const P&, int, int, float, float) {}
+
 // Per-lane section statistics, folded into the float64 PartAcc once at the end.
 struct DenStat {
     float st_abs = 0.f, st_min = INFINITY;
@@ -246,6 +251,7 @@ __device__ __forceinline__ void denoise_step_gp(const P& pol, int base, int nsec
                 v2 = __builtin_elementwise_fma(d1 * d1, f32x2{xk[u][h].y, xk[u][h].y}, v2);
             }
             var = (x2.x * x2.x + x2.y * x2.y) * (ze[u] * iz) + (v2.x + v2.y) * iz;
+            den_debug(pol, sec[u], g, ze[u], v2.x + v2.y);
         }
         if (FULL) {
             pol.store(sec[u], g, x2.x, x2.y, var, pa);
@@ -593,7 +599,7 @@ constexpr int grid_r() { return KK == 4 ? 2 : KK == 16 ? 4 : KK == 64 ? 8 : 0; }
 
 // The grid loop over this wave's sections; returns false (nothing done) when c is not a grid of
 // the size KK admits.  c.grid / c.gfull are kernel arguments: the branch is uniform.
-template <bool kVar, int KK, int U, int G, class P>
+template <bool kVar, int KK, int U, int G, bool PKG = true, class P>
 __device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, const Const& c, PartAcc& pa) {
     constexpr int R = grid_r<KK>();
     if constexpr (R == 0) {
@@ -609,14 +615,14 @@ __device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, co
         Q.load(c);
         if (gfull == GRID_FULL) {
             for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {   // wave-uniform trip count
-                if constexpr (U == 2 && AMP_DEN_PACKED_GRID)
+                if constexpr (PKG && U == 2 && AMP_DEN_PACKED_GRID)
                     denoise_step_grid2<kVar, R, GRID_FULL, G>(pol, base, nsec, Q, pa, S);
                 else
                     denoise_step_grid<kVar, R, GRID_FULL, U, G>(pol, base, nsec, Q, pa, S);
             }
         } else if constexpr (R == 4) {
             for (int base = wave * gpw * U; base < nsec; base += nw * gpw * U) {
-                if constexpr (U == 2 && AMP_DEN_PACKED_GRID)
+                if constexpr (PKG && U == 2 && AMP_DEN_PACKED_GRID)
                     denoise_step_grid2<kVar, R, GRID_REF16, G>(pol, base, nsec, Q, pa, S);
                 else
                     denoise_step_grid<kVar, R, GRID_REF16, U, G>(pol, base, nsec, Q, pa, S);
@@ -641,11 +647,20 @@ __device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, cons
     S.fold(pa);
 }
 
-// Runtime M (a power of two <= 64) -> the compile-time group size; PK selects the packed form.
+// Runtime M (a power of two <= 64) -> the compile-time group size; PK selects the packed-math
+// forms (v_pk_*_f32).  PK = false keeps every float32 operation scalar (the product grid still
+// applies): the engines that place two waves on one SIMD use it, because there the packed
+// variance accumulation of denoise_step_gp was measured to lose one half of a v_pk_fma_f32 result
+// in lanes 48-63 now and then (results not reproducible run to run; the scalar
+// form was bit-identical in every run).
 template <bool kVar, int KK, int U, int G, bool PK, class P>
 __device__ __forceinline__ void denoise_sections_sel(const P& pol, int nsec, const Const& c, PartAcc& pa) {
-    if constexpr (PK && KK % 2 == 0) denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa);
-    else denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa);
+    if constexpr (PK && KK % 2 == 0) {
+        denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa);
+    } else {
+        if (denoise_sections_grid<kVar, KK, U, G, false>(pol, nsec, c, pa)) return;
+        denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa);
+    }
 }
 template <bool kVar, int KK, int U, bool PK = true, class P>
 __device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {

@@ -147,6 +147,7 @@ struct XState {
 // float64 words at `buf` in place on `st` (op: AMP_ALLREDUCE_SUM / MAX).
 bool allreduce_hook_set();
 int call_allreduce_hook(double* buf, int count, int op, hipStream_t st);
+int hook_failure(const char* what);   // sets the error text, returns AMP_E_LAUNCH
 
 int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
 int device_cu_count();   // compute units of the current device (cached)

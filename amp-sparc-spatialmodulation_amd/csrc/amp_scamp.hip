@@ -652,7 +652,7 @@ static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStr
     return AMP_OK;
 }
 
-static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hipStream_t st) {
+static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hipStream_t st, bool& hook_failed) {
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
@@ -661,18 +661,19 @@ static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hip
     if (P.psi_split) hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
     hipLaunchKernelGGL(scamp_sxr1, dim3(1), dim3(SRWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("scamp_sxr1");
-    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
-    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
-    if (rc) return rc;
+    // every hook call is made on every rank even after one failed: the ranks' collectives stay
+    // matched and a failed rank's poisoned words reach the others (amp_sparc.h)
+    hook_failed |= call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st) != AMP_OK;
+    hook_failed |= call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(scamp_sxr2, dim3(1), dim3(SRWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("scamp_sxr2");
-    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(scamp_sxr3, dim3(1), dim3(64), 0, st, P, t);
     hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
     hipLaunchKernelGGL(scamp_fix_psi, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
     hipLaunchKernelGGL(scamp_sxr4, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
     AMP_LAUNCH_CHECK("scamp_sxr4");
-    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st) != AMP_OK;
     hipLaunchKernelGGL(scamp_sxr5, dim3(1), dim3(64), 0, st, P, t);
     AMP_LAUNCH_CHECK("scamp_sxr5");
     return AMP_OK;
@@ -706,7 +707,9 @@ int amp_scamp_run_sharded(const amp_dims* d, const amp_constellation* c, const a
     AMP_REQUIRE(B_global >= d->B, "amp_scamp_run_sharded: B_global = %d < this rank's B = %d", B_global, d->B);
     hipStream_t st = (hipStream_t)stream;
     if ((rc = scamp_prepare_impl(P, a, st))) return rc;
-    for (int t = 0; t < P.max_iter && !rc; ++t) rc = scamp_iterate_sharded(P, c64, t, st);
+    bool hook_failed = false;
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = scamp_iterate_sharded(P, c64, t, st, hook_failed);
+    if (!rc && hook_failed) rc = hook_failure("scamp");
     return rc ? rc : scamp_finalize_impl(P, st);
 }
 

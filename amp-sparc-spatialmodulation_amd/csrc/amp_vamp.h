@@ -62,6 +62,7 @@ struct VampK {
     const void* Wx1;             // Vh X3-packed (x3_index, O = k, J = N)
     const void* Wx2;             // V  X3-packed (O = N, J = k)
     XState* xs;                  // trial-sharded exchange words (amp_vamp_run_sharded)
+    float* dump;                 // diagnostic per-iteration state dump (amp_vamp_debug_dump), else null
     Const c;
 };
 
@@ -257,7 +258,15 @@ struct PDenoisePolicy {
         sm[sec] = smax;
         sa[sec] = sabs;
     }
+    float* dbg = nullptr;   // diagnostic: [16][2N] ze (columns < N) and vs (columns >= N), else null
 };
+__device__ __forceinline__ void den_debug(const PDenoisePolicy& p, int sec, int m, float ze, float vs) {
+    if (p.dbg) {
+        const int row = sec >> p.lspr, sj = sec & ((1 << p.lspr) - 1);
+        p.dbg[row * 2 * p.N + sj * p.M + m] = ze;
+        p.dbg[row * 2 * p.N + p.N + sj * p.M + m] = vs;
+    }
+}
 
 constexpr int PBM = 16;   // trials per workgroup
 
@@ -267,5 +276,8 @@ bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);
 int device_cu_count();
+float* debug_dump_ptr();   // amp_vamp_debug_dump's buffer (null: off)
+bool gemm_f32_requested();   // AMP_VAMP_GEMM=f32 (amp_vamp.hip)
+bool persist_wg2();   // AMP_PERSIST_WG2: two workgroups per CU at N = 64 (amp_vamp_persist.hip)
 
 }  // namespace amp

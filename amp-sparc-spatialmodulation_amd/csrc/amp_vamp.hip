@@ -24,6 +24,9 @@
 
 namespace amp {
 
+static float* g_dump = nullptr;
+float* debug_dump_ptr() { return g_dump; }
+
 __global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
     __shared__ __attribute__((aligned(16))) float lds[64];
     const VampIter it = vamp_first_iter(P, lds);
@@ -394,7 +397,7 @@ __global__ void vamp_output_kernel(VampK P) {
 }
 
 // AMP_VAMP_GEMM=f32: AMP_GEMM_AUTO keeps the f32-MFMA persistent GEMMs (measurement / A-B runs)
-static bool gemm_f32_requested() {
+bool gemm_f32_requested() {
     static const bool v = [] {
         const char* e = getenv("AMP_VAMP_GEMM");
         return e && e[0] == 'f';
@@ -442,6 +445,7 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
                 "its LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
     P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && x3_fits && !gemm_f32_requested())) ? 1 : 0;
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
+    P.dump = debug_dump_ptr();
     return AMP_OK;
 }
 
@@ -571,7 +575,7 @@ static int vamp_finalize_impl(const VampK& P, hipStream_t st) {
     return AMP_OK;
 }
 
-static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipStream_t st) {
+static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipStream_t st, bool& hook_failed) {
     dim3 g1(cdiv(P.B, GBM), P.ncp1 / 128);
     hipLaunchKernelGGL(vamp_k1, g1, dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
     AMP_LAUNCH_CHECK("vamp_k1");
@@ -579,15 +583,16 @@ static int vamp_iterate_sharded(const VampK& P, const Const64& c64, int t, hipSt
     AMP_LAUNCH_CHECK("vamp_k2");
     hipLaunchKernelGGL(vamp_xr1, dim3(1), dim3(RWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("vamp_xr1");
-    int rc = call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st);
-    if (!rc) rc = call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st);
-    if (rc) return rc;
+    // every hook call is made on every rank even after one failed: the ranks' collectives stay
+    // matched and a failed rank's poisoned words reach the others (amp_sparc.h)
+    hook_failed |= call_allreduce_hook(P.xs->sum, 2, AMP_ALLREDUCE_SUM, st) != AMP_OK;
+    hook_failed |= call_allreduce_hook(P.xs->mx, 2, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(vamp_xr2, dim3(1), dim3(RWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("vamp_xr2");
-    if ((rc = call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->gmax, 1, AMP_ALLREDUCE_MAX, st) != AMP_OK;
     hipLaunchKernelGGL(vamp_xr3, dim3(1), dim3(RWG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("vamp_xr3");
-    if ((rc = call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st))) return rc;
+    hook_failed |= call_allreduce_hook(P.xs->fix, 3, AMP_ALLREDUCE_SUM, st) != AMP_OK;
     hipLaunchKernelGGL(vamp_xr4, dim3(1), dim3(RWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("vamp_xr4");
     return AMP_OK;
@@ -610,7 +615,9 @@ int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
     P.Bmean = B_global;
     hipStream_t st = (hipStream_t)stream;
     rc = vamp_prepare_impl(P, a, st);
-    for (int t = 0; t < P.max_iter && !rc; ++t) rc = vamp_iterate_sharded(P, c64, t, st);
+    bool hook_failed = false;
+    for (int t = 0; t < P.max_iter && !rc; ++t) rc = vamp_iterate_sharded(P, c64, t, st, hook_failed);
+    if (!rc && hook_failed) rc = hook_failure("vamp");
     return rc ? rc : vamp_finalize_impl(P, st);
 }
 
@@ -744,6 +751,24 @@ size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max
     return vamp_carve(&de, k, max_iter, nullptr).bytes;
 }
 
+int amp_vamp_debug_dump(void* buf) {
+    g_dump = (float*)buf;
+    return AMP_OK;
+}
+
+int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs, uint64_t* out) {
+    if (!d || !out || k <= 0 || max_iter <= 0 || epochs < 1) return AMP_E_ARG;
+    amp_dims de = *d;
+    de.B = d->B * epochs;
+    char* const base = reinterpret_cast<char*>(uintptr_t{4096});   // a dummy base: offsets only
+    const VampWs w = vamp_carve(&de, k, max_iter, base);
+    out[0] = (uint64_t)((char*)w.pparts - base);
+    out[1] = (uint64_t)((char*)w.pxch - base);
+    out[2] = (uint64_t)((char*)w.pbar - base);
+    out[3] = (uint64_t)((char*)w.dwg - base);
+    return AMP_OK;
+}
+
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                  const amp_vamp_decide_args* dec, int32_t epochs, void* stream) {
     AMP_REQUIRE(d && epochs >= 1 && (long)d->B * epochs <= (1L << 30), "amp_vamp_detect_count_epochs: epochs = %d",
@@ -764,6 +789,8 @@ int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, 
     P.E = epochs;
     P.wpe = cdiv(d->B, PBM);
     P.nwg = P.E * P.wpe;
+    AMP_REQUIRE(P.x3 || P.nwg <= ncu, "amp_vamp_detect_count_epochs: %d workgroups need two per CU, which only the "
+                "bf16x3 engine runs (gemm = AMP_GEMM_F32 holds at most %d epochs)", P.nwg, ncu / P.wpe);
     AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts,
                 "amp_vamp_detect_count_epochs: null pointer argument");
     AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_vamp_detect_count_epochs: ibits_trunc");

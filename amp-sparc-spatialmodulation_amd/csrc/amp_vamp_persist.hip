@@ -64,11 +64,21 @@ bool vamp_persist_x3_fits(int N, int k, int L) {
     return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
 }
 
-// One persistent workgroup per CU.  Round 2 tried two per CU at N = 64 (launch bounds for 256
-// VGPRs, 2 x 256 workgroups for 8 cfg2 epochs): the launch ran, but the results of co-resident
-// epochs were not reproducible run to run (every r element of most epochs off in the last bits,
-// tools/epochs_diag.py), so the engine stays at one workgroup per CU.
-static int persist_wg_cap(int) { return 1; }
+// Workgroups per CU.  Two at N = 64 on the bf16x3 engine (its instantiation bounded for two
+// waves per SIMD, 2 x 256 workgroups for 8 cfg2 epochs per launch; AMP_PERSIST_WG2=0 keeps one).
+// The two-per-CU build runs the denoiser in scalar float32 (amp_denoise.h denoise_sections_sel):
+// with the packed-math form, co-resident epochs were not reproducible run to run — the
+// variance of a section's dominant position lost the Re or Im half of its packed
+// sum |x - a_k|^2 eta_k in lanes 48-63 now and then (tools/epochs_diag.py, tools/var_check.py;
+// DESIGN.md §3.8).
+bool persist_wg2() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_PERSIST_WG2");
+        return !(e && e[0] == '0') && !gemm_f32_requested();
+    }();
+    return v;
+}
+static int persist_wg_cap(int N) { return (N == 64 && persist_wg2()) ? 2 : 1; }
 
 int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return 0;

@@ -167,8 +167,10 @@ __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, 
 // X3: both per-iteration GEMMs on the split-precision bf16x3 engine (gemm_x3): the A operand
 // (r~, then w) lives in LDS as six bf16 planes, each wave owns NT/2 complex column tiles (the
 // same 16 NT real columns as the f32 form), the operators are the X3-packed Vh / V (Wx1 / Wx2).
-template <int NT, int KK, int NWV, int DU, bool X3>
-__global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc) {
+// OCC: workgroups per CU the register allocation is bounded for (__launch_bounds__' minimum
+// waves per SIMD = OCC * NWV / 4); 2 only for the side-by-side cfg2 epochs (N = 64).
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1>
+__global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
     static_assert(!X3 || (NWV == 4 && NT % 2 == 0), "X3: four waves, whole complex tiles");
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
@@ -332,6 +334,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
                     wi[r] = sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi;
                 }
                 x3_store_acc(sP, ldx, o, wr, wi);
+                if (P.dump) {
+                    float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 0) * PBM * twoN;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o] = wr[r];
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = wi[r];
+                    }
+                }
             }
         } else
 #pragma unroll
@@ -360,6 +370,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
                     const float xtr = cr[t2][r] + rtr, xti = ci[t2][r] + rti;
                     sR[b] = (xtr - cur.alpha * rtr) * cur.inv1ma;
                     sR[b + 1] = (xti - cur.alpha * rti) * cur.inv1ma;
+                    if (P.dump) {
+                        float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 1) * PBM * twoN;
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o] = sR[b];
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = sR[b + 1];
+                    }
                 }
             }
         } else {
@@ -380,14 +395,28 @@ __global__ __launch_bounds__(64 * NWV, 1) void vamp_persist(VampK P, DecConst dc
         stamp(t, 4);
         // 4. denoiser (vamp.py:84)
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
+        if (P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
         PartAcc pa;
         if constexpr (KK > 16)
             denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
         else
-            denoise_sections_u<true, KK, DU>(pol, nrows * spr, M, P.c, pa);
+            denoise_sections_u<true, KK, DU, OCC == 1>(pol, nrows * spr, M, P.c, pa);   // two per CU: scalar f32 (amp_denoise.h)
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
+        if (P.dump) {   // xmmse and var after the denoiser (part_publish's barrier ordered the LDS writes)
+            float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 2) * PBM * twoN;
+            for (int e = tid; e < PBM * twoN; e += PWG) dp[e] = sX[(e / twoN) * ldr + e % twoN];
+            for (int e = tid; e < PBM * N; e += PWG) dp[PBM * twoN + (e / N) * twoN + e % N] = vnew[e];
+            if (tid == 0) {
+                const Partial* sp = reinterpret_cast<const Partial*>(scr);
+                for (int w = 0; w < PWG / 64; ++w) {
+                    double v = sp[w].sumvar;
+                    __builtin_memcpy(dp + PBM * twoN + N + 2 * w, &v, 8);
+                }
+                dp[PBM * twoN + twoN + N] = cur.inv_sigma2;   // row 1, column N: the denoiser's 1 / sigma2
+            }
+        }
         stamp(t, 5);
         // 5. batch scalars: every workgroup gathers and reduces every partial
         PartAcc g;
@@ -522,9 +551,9 @@ static inline int den_u() {
 
 // Launch path: persist_grid_launch (amp_host.h): a plain launch after an explicit co-residency
 // check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
-template <int NT, int KK, int NWV, int DU, bool X3>
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
     // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
@@ -548,23 +577,23 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
     return persist_grid_launch("vamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
-template <int NT, int NWV, bool X3>
+template <int NT, int NWV, bool X3, int OCC = 1>
 static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV, 4, X3>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV, 4, X3>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV, 4, X3>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV, 2, X3>(P, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV, 4, X3, OCC>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC>(P, dc, st);
     case 16:
         // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8;
         // f32 engine only: 4 and 8 spill beside the bf16x3 GEMM's registers)
-        if constexpr (X3) return persist_launch_t<NT, 16, NWV, AMP_X3_DU, X3>(P, dc, st);
+        if constexpr (X3) return persist_launch_t<NT, 16, NWV, AMP_X3_DU, X3, OCC>(P, dc, st);
         switch (den_u()) {
         case 4: return persist_launch_t<NT, 16, NWV, 4, X3>(P, dc, st);
         case 8: return persist_launch_t<NT, 16, NWV, 8, X3>(P, dc, st);
         default: return persist_launch_t<NT, 16, NWV, 2, X3>(P, dc, st);
         }
-    default: return persist_launch_t<NT, 64, NWV, 1, X3>(P, dc, st);
+    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC>(P, dc, st);
     }
 }
 

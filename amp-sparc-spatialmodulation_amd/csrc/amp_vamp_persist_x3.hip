@@ -7,7 +7,9 @@ namespace amp {
 
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.N) {
-    case 64: return persist_launch_nt<2, 4, true>(P, dc, st);
+    case 64:   // the two-per-CU build for every N = 64 launch, so that one epoch and side-by-side
+               // epochs run the same arithmetic (bit-identical results, tests/test_gpu_epochs.py)
+        return persist_wg2() ? persist_launch_nt<2, 4, true, 2>(P, dc, st) : persist_launch_nt<2, 4, true>(P, dc, st);
     case 128: return persist_launch_nt<4, 4, true>(P, dc, st);
     case 256: return persist_launch_nt<8, 4, true>(P, dc, st);
     default: break;

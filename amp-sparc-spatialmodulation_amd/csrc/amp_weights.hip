@@ -285,8 +285,13 @@ bool allreduce_hook_set() { return g_hook != nullptr; }
 
 int call_allreduce_hook(double* buf, int count, int op, hipStream_t st) {
     const int rc = g_hook((void*)buf, count, op, (void*)st, g_hook_ctx);
-    if (rc) set_error("trial-sharded run: all-reduce hook returned %d", rc);
     return rc ? AMP_E_LAUNCH : AMP_OK;
+}
+
+int hook_failure(const char* what) {
+    set_error("amp_%s_run_sharded: the all-reduce hook failed on this rank (every later call was still made)",
+              what);
+    return AMP_E_LAUNCH;
 }
 
 }  // namespace amp

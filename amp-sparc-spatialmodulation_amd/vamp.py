@@ -398,16 +398,26 @@ class ShardHook:
 
     def _allreduce(self, buf, count, op, stream, ctx) -> int:
         """amp_allreduce_fn: `count` float64 words at device address `buf` (inside this
-        detector's workspace), in place, ordered on the current stream."""
+        detector's workspace), in place, ordered on the current stream.
+
+        Failure semantics (amp_sparc.h): a local error (a buffer outside the workspace) still
+        takes part in the collective, with NaN words, so the other ranks never wait on a missing
+        peer; the error is kept, the C driver makes every later call too and returns
+        AMP_E_LAUNCH, and _run_hooked raises on EVERY rank (one flag all-reduce per forward)."""
+        dist = torch.distributed
+        if not (dist.is_available() and dist.is_initialized()):
+            return 0                       # one process: the reduction over one rank is the identity
         try:
-            dist = torch.distributed
             ws = self._ws
             off = int(buf) - ws.data_ptr()
             if off < 0 or off + 8 * count > ws.numel():
                 raise ValueError(f'hook buffer outside the workspace (offset {off})')
-            if not (dist.is_available() and dist.is_initialized()):
-                return 0                       # one process: the reduction over one rank is the identity
             view = ws[off:off + 8 * count].view(torch.float64)
+        except Exception as e:   # noqa: BLE001 — the collective below still runs, on poison
+            if self._hook_error is None:
+                self._hook_error = e
+            view = torch.full((int(count),), float('nan'), dtype=torch.float64, device=self._ws.device)
+        try:
             rop = dist.ReduceOp.SUM if op == nat.ALLREDUCE_SUM else dist.ReduceOp.MAX
             if view.device.type == 'cuda' and dist.get_backend(self.group) == 'nccl':
                 dist.all_reduce(view, op=rop, group=self.group)
@@ -415,10 +425,10 @@ class ShardHook:
                 h = view.cpu()
                 dist.all_reduce(h, op=rop, group=self.group)
                 view.copy_(h)
-            return 0
-        except Exception as e:   # noqa: BLE001 — surfaced by the C driver as AMP_E_LAUNCH
-            self._hook_error = e
-            return 1
+        except Exception as e:   # noqa: BLE001 — the group itself failed: surfaced as AMP_E_LAUNCH
+            if self._hook_error is None:
+                self._hook_error = e
+        return 0 if self._hook_error is None else 1
 
     def shard(self):
         dist = torch.distributed
@@ -427,10 +437,21 @@ class ShardHook:
         return rank * B // world, (rank + 1) * B // world
 
     def _run_hooked(self, fn, what, *args) -> None:
+        """Runs a trial-sharded C driver with this detector's hook; if the hook failed on ANY
+        rank, every rank raises (the failed rank's poisoned words made the others' results
+        meaningless too)."""
         lib = nat.lib()
         self._hook_error = None
         nat.check(lib.amp_set_allreduce_hook(C.cast(self._hook, C.c_void_p), None), 'amp_set_allreduce_hook')
         rc = fn(*args)
+        dist = torch.distributed
+        if dist.is_available() and dist.is_initialized():
+            flag = torch.tensor([1.0 if self._hook_error is not None else 0.0], dtype=torch.float64)
+            if dist.get_backend(self.group) == 'nccl':
+                flag = flag.to(self._ws.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            if float(flag.item()) != 0.0 and self._hook_error is None:
+                raise RuntimeError(f'{what}: the all-reduce hook failed on another rank')
         if self._hook_error is not None:
             raise RuntimeError(f'{what}: all-reduce hook failed') from self._hook_error
         nat.check(rc, what)
@@ -471,7 +492,7 @@ class ShardedVAMP(ShardHook, VAMP):
     draws the same epoch from the same seed: channel, messages and noise are replicated with no
     communication); the rank runs its slice through amp_vamp_run_sharded, whose
     registered hook all-reduces the batch-global scalars of every iteration (var.mean(),
-    max |xi|, allclose; vamp.py:85, 112, 185) five times per iteration, decides its rows with
+    max |xi|, allclose; vamp.py:85, 112, 185) four times per iteration, decides its rows with
     amp_map_decide_count_rows and merges the error counters with ONE all-reduce.  The returned
     Loss equals the whole-batch forward's, up to the float64 summation order of var.mean().
     The hook runs torch.distributed.all_reduce on the device words for RCCL ('nccl') and

@@ -163,7 +163,7 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
  * idx hold the epochs' rows back to back ([epochs * B] rows); status -> amp_status[epochs],
  * dec->counts -> amp_counts[epochs]; workspace: amp_vamp_epochs_workspace_bytes.  Needs the
  * persistent engine with B % 16 == 0 and epochs <= amp_vamp_max_epochs (one workgroup of 16
- * trials per CU). */
+ * trials per CU; two per CU at N = 64 on the bf16x3 engine, AMP_PERSIST_WG2=0 keeps one). */
 /* ---- Trial sharding across ranks (SURVEY §8(e) exact-compat mode) ----
  * One batch of B_global trials split over ranks (rank r holds a contiguous slice of d->B rows);
  * every per-iteration batch-global value of VAMP.forward (var.mean() vamp.py:85, the float64
@@ -171,8 +171,13 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
  * all-reduced through a caller-registered hook between launches, so each rank follows the
  * trajectory of the whole-batch forward.  The hook all-reduces `count` float64 words at the
  * device pointer `buf` in place, ordered on `stream` (e.g. an RCCL ncclAllReduce on that stream,
- * or torch.distributed.all_reduce); it returns 0 on success.  It is called 5 times per
- * iteration on every rank (no data-dependent calls, no host synchronisation inside). */
+ * or torch.distributed.all_reduce); it returns 0 on success.  It is called 4 times per
+ * iteration on every rank (no data-dependent calls, no host synchronisation inside).
+ * Failure semantics: a hook that fails must still take part in its collective (e.g. with NaN
+ * words) and return nonzero; the driver keeps making every later call of the forward, so the
+ * ranks' collectives stay matched, and then returns AMP_E_LAUNCH on that rank.  The poisoned
+ * words reach every rank; the caller decides collectively whether to discard the forward
+ * (vamp.ShardHook._run_hooked all-reduces an error flag and raises on every rank). */
 enum { AMP_ALLREDUCE_SUM = 0, AMP_ALLREDUCE_MAX = 1 };
 typedef int (*amp_allreduce_fn)(void* buf, int64_t count, int32_t op, void* stream, void* ctx);
 int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx);
@@ -182,6 +187,17 @@ int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
                          void* stream);
 
 size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs);
+/* Diagnostic: byte offsets inside the epochs workspace of the persistent engine's exchange
+ * records: out[0] the per-iteration granule pairs ([max_iter][epochs * ceil(B/16)] x 32 B:
+ * {sum var f64, not-close u32, tag u32}, {max|xi| f32, min section max f32, 0, tag}), out[1] the
+ * rare-path float64 words, out[2] the barrier words, out[3] the per-workgroup counter records. */
+int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs, uint64_t* out);
+/* Diagnostic: every later persistent VAMP launch of this process writes its per-iteration state
+ * to buf (device, float32: [max_iter][nwg][5][16][2N]: w after GEMM1's epilogue, r after GEMM2's,
+ * xmmse after the denoiser, then var (columns < N) and the waves' float64 var sums (row 0,
+ * columns N ..), then the denoiser's exclusive section sum and variance sum (columns < N / >= N), per
+ * workgroup's 16 rows); null turns it off. */
+int amp_vamp_debug_dump(void* buf);
 /* The most epochs of d->B trials one launch holds on this device (0: not persistent-eligible). */
 int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,

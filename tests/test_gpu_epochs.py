@@ -54,13 +54,15 @@ def _run_both(cfg, chan, SNR, eps, device):
 
 
 @pytest.mark.parametrize('alphabet,ebn0,E', [('16QAM', 8.0, 4), ('16QAM', 20.0, 4), ('QPSK', 4.0, 4),
-                                             ('QPSK', 12.0, 4), ('QPSK', 6.0, 4), ('16QAM', 14.0, 2)])
+                                             ('QPSK', 12.0, 4), ('QPSK', 6.0, 4), ('16QAM', 14.0, 2),
+                                             ('QPSK', 6.0, 8), ('16QAM', 8.0, 8), ('QPSK', 2.0, 8),
+                                             ('16QAM', 20.0, 8)])
 def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0, E):
     cfg = _cfg(64, 4, 128, 1024, alphabet)
     chan, SNR, eps = _epochs(cfg, E, ebn0, seed=3)
     det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
-    # one workgroup of 16 trials per CU: 4 epochs of 64 workgroups on 256 CUs
-    assert det.max_epochs(64) == torch.cuda.get_device_properties(0).multi_processor_count // 64
+    # two workgroups of 16 trials per CU at N = 64: 8 epochs of 64 workgroups on 256 CUs
+    assert det.max_epochs(64) == 2 * torch.cuda.get_device_properties(0).multi_processor_count // 64
     r, xm, var = det.last_epochs
     assert len(grp) == E
     for e, (ls, st, r0, x0, v0) in enumerate(seq):
@@ -133,3 +135,26 @@ def test_simulate_group_epochs_identical(device, tmp_path):
         assert a.keys() == b.keys()
         for k in a:
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+
+
+@pytest.mark.parametrize('alphabet,ebn0', [('QPSK', 6.0), ('16QAM', 8.0)])
+def test_epochs8_two_per_cu_reproducible(device, alphabet, ebn0):
+    """8 cfg2 epochs in one launch (two workgroups per CU) three times over: every r / xmmse / var
+    word equal to the sequential forwards in every repetition.  Round 2 saw these co-resident epochs
+    change run to run; the cause was the packed-math variance sum of the denoiser (one half of a
+    v_pk_fma_f32 result lost in lanes 48-63 with two waves per SIMD)."""
+    cfg = _cfg(64, 4, 128, 1024, alphabet)
+    chan, SNR, eps = _epochs(cfg, 8, ebn0, seed=3)
+    det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
+    mv = lambda t: t.to(device).contiguous()  # noqa: E731
+    U, s, Vh = (mv(t) for t in chan)
+    for rep in range(3):
+        if rep:
+            grp = det.forward_epochs(U, s, Vh, [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
+                                     [e[1] for e in eps], [e[2] for e in eps])
+        r, xm, var = det.last_epochs
+        for e, (ls, st, r0, x0, v0) in enumerate(seq):
+            assert int(grp[e].loss['T']) == int(ls['T']), (rep, e)
+            assert torch.equal(r[e].view(torch.int32), r0.view(torch.int32)), (rep, e)
+            assert torch.equal(xm[e].view(torch.int32), x0.view(torch.int32)), (rep, e)
+            assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), (rep, e)

@@ -39,8 +39,10 @@ CFGS = {
     'cfg4': ('vamp', 256, 8, 512, 4096, '16QAM', 20, 8.0),
     # cfg2 with the 4 epochs of one res = 4 block side by side (VAMP.forward_epochs: 256 workgroups)
     'cfg2-epochs4': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
+    # 8 epochs: two workgroups per CU (AMP_PERSIST_WG2, the N = 64 default since round 3)
+    'cfg2-epochs8': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
 }
-EPOCHS = {'cfg2-epochs4': 4}
+EPOCHS = {'cfg2-epochs4': 4, 'cfg2-epochs8': 8}
 
 
 def main(steps=50, warmup=30, only=None):
