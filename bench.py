@@ -9,8 +9,10 @@ GPU) + the one 128-byte result read-back — exactly what Model.simulate calls p
 queued (Loss resolves lazily), so the GPU does not idle on the host between steps.  Input generation and the SVD are outside the timed region
 (SURVEY.md §8(d)).  Each rank runs its own independent epoch (its own seed): Monte-Carlo
 epochs are independent, so the path shards with no data-path collective ("weak").
+`--shard trials` instead splits ONE batch over the ranks (ShardedVAMP, exact-compat: the
+batch-global scalars of every iteration all-reduced through amp_set_allreduce_hook; "strong").
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--shard epochs|trials]
 """
 import argparse
 import json
@@ -110,6 +112,49 @@ def traffic_from_profile(persistent):
     return None
 
 
+def timed_epochs(step, counts_of, steps, warmup, merge, sync=lambda: None, barrier=lambda: None,
+                 max_over_ranks=lambda el: el, prewarm_s=0.0):
+    """The measured region of every mode (the driver contract), on any device:
+
+    * untimed: first `prewarm_s` seconds of steps (the chip's clocks ramp over the first ~25 ms of
+      back-to-back epochs, DESIGN.md §3.3: a short `--warmup` would time the ramp), then EXACTLY
+      `warmup` steps;
+    * barrier + sync, then EXACTLY `steps` timed steps. step() queues one epoch and returns its
+      handle; counts_of(handle) -> float64[13] counters of that epoch (for the GPU detector it
+      resolves the lazy read-back, so step k's counters are read while step k+1's launches run);
+    * merge(sum of the counters) inside the timed region: ONE all-reduce over the ranks for
+      independent epochs, the identity for trial sharding (the detector already merged them);
+    * sync, barrier, elapsed time max over ranks.
+    Returns (elapsed seconds, merged float64[13], last handle, prewarm steps run)."""
+    npre = 0
+    if prewarm_s > 0:
+        t_end = time.perf_counter() + prewarm_s
+        while time.perf_counter() < t_end:
+            h = step()
+            npre += 1
+        counts_of(h)
+    for _ in range(warmup):
+        h = step()
+    if warmup:
+        counts_of(h)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    acc = np.zeros(13)
+    h = None
+    for _ in range(steps):
+        prev = h
+        h = step()
+        if prev is not None:
+            acc += counts_of(prev)
+    acc += counts_of(h)          # the last step's counters inside the timed region too
+    merged = merge(acc)
+    sync()
+    el = time.perf_counter() - t0
+    barrier()
+    return max_over_ranks(el), merged, h, npre
+
+
 def spawn_ranks(n: int) -> int:
     """`bench.py --gpus N` started without a launcher: start N fresh child processes, one per
     GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), wait for
@@ -144,6 +189,11 @@ def main():
     ap.add_argument('--cpu-sample', type=int, default=4096)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--engine', default='auto', choices=['auto', 'launches', 'persistent'])
+    # independent epochs per rank (weak scaling, the default) or ONE batch of B trials split over
+    # the ranks (strong scaling: ShardedVAMP, the batch scalars all-reduced every iteration)
+    ap.add_argument('--shard', default='epochs', choices=['epochs', 'trials'])
+    ap.add_argument('--prewarm-ms', type=float, default=300.0,
+                    help='untimed steps for this long before the --warmup steps (clock ramp)')
     args = ap.parse_args()
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
@@ -162,7 +212,7 @@ def main():
     device = torch.device('cuda', local)
 
     from config import Config
-    from vamp import VAMP
+    from vamp import VAMP, ShardedVAMP
     from loss import allreduce_counts, counts_to_vector
     import ctypes as C
     import amp_native as nat
@@ -171,53 +221,63 @@ def main():
     Nt, Na, Nr, B, alph, iters = CONFIGS[args.config]
     cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cuda')
-    # every rank detects its own independent Monte-Carlo epoch (its own channel, messages and
-    # noise: seed + rank), as the trial-sharded sweep does
-    inp = make_inputs(cfg, args.seed + rank, args.ebn0, device)
+    trials = args.shard == 'trials'
+    # epochs: every rank detects its own independent Monte-Carlo epoch (its own channel, messages
+    # and noise: seed + rank); trials: every rank draws the SAME epoch and detects its slice
+    inp = make_inputs(cfg, args.seed + (0 if trials else rank), args.ebn0, device)
     engine = {'auto': nat.ENGINE_AUTO, 'launches': nat.ENGINE_LAUNCHES, 'persistent': nat.ENGINE_PERSISTENT}[args.engine]
-    det = VAMP(cfg, engine=engine)
+    det = ShardedVAMP(cfg) if trials else VAMP(cfg, engine=engine)
+    seq = [0]
 
     def step():
-        return det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        seq[0] += 1
+        return seq[0]
 
-    for _ in range(args.warmup):
-        step()
-    det.L.resolve()
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    acc = np.zeros(13)
-    L = None
-    for _ in range(args.steps):
-        prev = L
-        L = step()       # a step's counters are read back while the next step's launches run
-        if prev is not None:
-            acc += counts_to_vector(det.L.last_counts)   # resolved by step(): the previous forward's
-    L.resolve()          # ... and the last step's inside the timed region too
-    acc += counts_to_vector(L.last_counts)
-    merged = allreduce_counts(acc)   # ONE all-reduce (RCCL) of the error counters of every rank
-    torch.cuda.synchronize(device)
-    el = time.perf_counter() - t0
-    if dist:
-        tdist.barrier()
+    def counts_of(h):
+        # step() resolved the previous forward's read-back; only the newest one is waited for here
+        if h == seq[0]:
+            det.L.resolve()
+        return counts_to_vector(det.L.last_counts)
+
+    def max_over_ranks(el):
+        if not dist:
+            return el
         t = torch.tensor([el], dtype=torch.float64, device=device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        el = t.item()
+        return t.item()
+
+    el, merged, _, npre = timed_epochs(
+        step, counts_of, args.steps, args.warmup,
+        merge=(lambda v: v) if trials else allreduce_counts,    # ONE all-reduce (RCCL) of the counters
+        sync=lambda: torch.cuda.synchronize(device), barrier=(tdist.barrier if dist else (lambda: None)),
+        max_over_ranks=max_over_ranks, prewarm_s=args.prewarm_ms * 1e-3)
+    L = det.L
     T = int(L.loss['T'])
-    rates = dict(zip(L.keys, L.rates_from_vector(merged, epochs=world * args.steps)))
+    n_epochs = args.steps * (1 if trials else world)     # epochs whose counters `merged` holds
+    rates = dict(zip(L.keys, L.rates_from_vector(merged, epochs=n_epochs)))
     ver, ser = float(rates['ver']), float(rates['ser'])
 
     # dominant kernel timed with HIP events on the stream it runs on: the persistent engine's
     # single vamp_persist launch (T iterations: 2 complex mat-vecs per trial-iteration), or the
-    # launch engine's GEMM2 + fused denoiser kernel (one complex mat-vec per trial)
-    Tr = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+    # launch engine's GEMM2 + fused denoiser kernel (one complex mat-vec per trial); trial
+    # sharding profiles the launch engine on this rank's slice (what it runs per iteration)
+    if trials:
+        b0, b1 = det.shard()
+        Bp = b1 - b0
+        pcfg = Config(Nt, Na, Nr, 1, 1, batch=Bp, generator_mode='sparc', iterations=iters, alphabet=alph,
+                      channel_profile='uniform', channel_truncation='tail', device='cuda')
+        prof = VAMP(pcfg, engine=nat.ENGINE_LAUNCHES)
+        Tr = prof.detect(inp['U'], inp['s'], inp['Vh'], inp['y'][b0:b1].contiguous(), inp['SNR'])
+    else:
+        Bp = B
+        Tr = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     persistent = nat.lib().amp_vamp_select_engine(C.byref(Tr.dims), Tr.k, Tr.args.engine) == nat.ENGINE_PERSISTENT
     ms = (C.c_float * 4)()
     nat.check(nat.lib().amp_vamp_profile(C.byref(Tr.dims), C.byref(Tr.const), C.byref(Tr.args), ms, Tr.stream),
               'amp_vamp_profile')
     N, k = Nt, min(Nt, Nr)
-    flops_mv = 8.0 * B * N * k                     # complex [N x k] . [k] per trial = 8 real flop / CMAC
+    flops_mv = 8.0 * Bp * N * k                    # complex [N x k] . [k] per trial = 8 real flop / CMAC
     if persistent:
         kern, flops_launch = 'vamp_persist (whole iteration loop: 2 GEMMs + LMMSE + Onsager + denoiser per iteration)', \
             2.0 * flops_mv * T
@@ -233,19 +293,27 @@ def main():
         nat.unload()
         return
     ms_step = el / args.steps * 1e3
-    value = world * B / (el / args.steps)
+    gb = B if trials else world * B                # trials detected per step, all ranks together
+    value = gb / (el / args.steps)
+    if trials:
+        par = (f'trial-shard x{world} of ONE batch (exact-compat: rank r detects trials [r B/{world}, (r+1) B/{world}), '
+               'the batch scalars all-reduced 4x per iteration, one counter all-reduce)')
+    else:
+        par = f'epoch-shard x{world} (independent epochs, one all-reduce of the error counters)'
     out = {
         'metric': 'detected symbol-vectors/sec, VAMP Nt=256 Nr=512 16-QAM; SER match vs ref',
         'value': value, 'unit': 'symbol-vectors/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-        'ms_per_step': ms_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'ms_per_step': ms_step, 'higher_is_better': True, 'scaling': 'strong' if trials else 'weak',
+        'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic (reference generators replayed: sparc channel, segmented 16-QAM messages, AWGN)',
         'config': {'workload': f'{args.config}: VAMP Nt={Nt} Nr={Nr} Na={Na} {alph} batch={B} iterations<={iters} '
                                f'EbN0={args.ebn0} dB, one channel per batch',
-                   'global_batch': world * B, 'parallelism': f'trial-shard x{world} (independent epochs, '
-                                                             'one all-reduce of the error counters)'},
-        'detail': {'T': T, 'ver': ver, 'ser': ser, 'epochs': world * args.steps,
-                   'trial_iterations_per_s': world * B * T / (el / args.steps),
-                   'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms},
+                   'global_batch': gb, 'shard': args.shard, 'parallelism': par},
+        'detail': {'T': T, 'ver': ver, 'ser': ser, 'epochs': n_epochs,
+                   'trial_iterations_per_s': gb * T / (el / args.steps),
+                   'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms,
+                   'prewarm': {'ms': args.prewarm_ms, 'steps': npre,
+                               'why': 'untimed steps before --warmup: the clocks ramp over the first ~25 ms'}},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),
                      'kernel': kern, 'flop_per_launch': flops_launch,
