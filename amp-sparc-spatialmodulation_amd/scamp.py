@@ -173,10 +173,28 @@ class SCAMP(LazyResult, nn.Module):
             T._call('amp_scamp_run')
             # decision on T.xmap (scamp.py:107); counters next to the status record
             self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
-            self._arm(self.L, res, host, 'amp_scamp_run')                 # + L.dump(), scamp.py:99
+            persistent = nat.lib().amp_scamp_select_engine(C.byref(T.dims), self.engine) == nat.ENGINE_PERSISTENT
+            rescue = (lambda: self._rescue_forward(W, A, y, SNR, x, symbol, index)) if persistent else None
+            self._arm(self.L, res, host, 'amp_scamp_run', rescue)          # + L.dump(), scamp.py:99
         self._keep = T
         self.last = T
         return self.L
+
+    def _rescue_forward(self, W, A, y, SNR, x, symbol, index):
+        """One forward on the launch engine, synchronously, into buffers of its own: the rescue
+        of a persistent launch whose grid was lost (vamp.LazyResult._check_grid)."""
+        from vamp import read_result
+        with torch.cuda.device(y.device):
+            if getattr(self, '_rescue_bufs', None) is None:
+                self._rescue_bufs = _Buffers()
+            T = Tracker(W, A, y, self.E / SNR, self.config, self._rescue_bufs)
+            T.args.engine = nat.ENGINE_LAUNCHES
+            T.args.gemm = nat.GEMM_AUTO
+            res = torch.zeros(256, dtype=torch.uint8, device=T.y.device)
+            T.args.status = nat.dptr(res)
+            T._call('amp_scamp_run')
+            self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
+            return read_result(res)
 
 
 class ShardedSCAMP(ShardHook, SCAMP):

@@ -180,9 +180,15 @@ class LazyResult:
         self._slot ^= 1
         return self._ring[self._slot]
 
-    def _arm(self, L: Loss, res: torch.Tensor, host: torch.Tensor, what: str) -> None:
+    def _arm(self, L: Loss, res: torch.Tensor, host: torch.Tensor, what: str, rescue=None) -> None:
         """Queue the copy of `res` to `host` on the device's current stream and make L resolve it
-        lazily; the previous forward's record is resolved first."""
+        lazily; the previous forward's record is resolved first.
+
+        A persistent launch whose grid exchange timed out reports nan_state = -1 (every spin is
+        bounded; the grid drains and the results are invalid).  `rescue()` then re-runs that
+        forward on the launch engine in this process (no exec, no co-residency needed) and
+        returns its (status, counts); the event is counted in self.grid_rescues.  Without a
+        rescue (or if it fails too) the resolve raises."""
         host.copy_(res, non_blocking=True)
         done = torch.cuda.Event()
         done.record(torch.cuda.current_stream(res.device))   # the stream the launches and the copy ran on
@@ -194,12 +200,32 @@ class LazyResult:
             raw = host.numpy().tobytes()
             status = nat.AmpStatus.from_buffer_copy(raw[:C.sizeof(nat.AmpStatus)])
             counts = nat.AmpCounts.from_buffer_copy(raw[64:64 + C.sizeof(nat.AmpCounts)])
-            if status.nan_state < 0:
-                raise RuntimeError(f'{what}: persistent engine grid barrier timed out (results invalid)')
+            status, counts = self._check_grid(status, counts, rescue, what)
             L.last_counts = counts
             L.last_status = status
             L.record(L.rates_from_counts(counts), int(status.T))
         L._pending = finish
+
+    grid_rescues = 0
+
+    def _check_grid(self, status, counts, rescue, what):
+        global _TEST_LOSE_GRID
+        if _TEST_LOSE_GRID > 0 and rescue is not None:     # test seam: report this launch's grid as lost
+            _TEST_LOSE_GRID -= 1
+            status.nan_state = -1
+        if status.nan_state >= 0:
+            return status, counts
+        if rescue is not None:
+            self.grid_rescues += 1
+            status, counts = rescue()
+            if status.nan_state >= 0:
+                return status, counts
+        raise RuntimeError(f'{what}: persistent engine grid barrier timed out (results invalid)')
+
+
+# Test seam (tests only): the next N persistent results resolved are reported as lost grids
+# (nan_state = -1, what a timed-out grid exchange writes), to exercise the launch-engine rescue.
+_TEST_LOSE_GRID = 0
 
 
 class VAMP(LazyResult, nn.Module):
@@ -261,9 +287,28 @@ class VAMP(LazyResult, nn.Module):
             nat.check(lib.amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream), 'amp_vamp_run')
             # decision on T.r (vamp.py:187); counters land next to the status record
             self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
-        self._arm(self.L, res, host, 'amp_vamp_run')                     # + L.dump(), vamp.py:180
+        persistent = lib.amp_vamp_select_engine(C.byref(T.dims), T.k, self.engine) == nat.ENGINE_PERSISTENT
+        rescue = (lambda: self._rescue_forward(U, s, Vh, y, SNR, x, symbols, indices)) if persistent else None
+        self._arm(self.L, res, host, 'amp_vamp_run', rescue)              # + L.dump(), vamp.py:180
         self.last = T
         return self.L
+
+    def _rescue_forward(self, U, s, Vh, y, SNR, x, symbols, indices):
+        """One forward on the launch engine (three launches per iteration: no grid-wide
+        exchange inside a kernel), synchronously, into buffers of its own: the rescue of a
+        persistent launch whose grid was lost (LazyResult._check_grid).  Returns (status, counts)."""
+        with torch.cuda.device(y.device):
+            if getattr(self, '_rescue_bufs', None) is None:
+                self._rescue_bufs = _Buffers()
+            T = Tracker(U, s, Vh, y, None, self.E / SNR, self.sparsity, self.config, self._rescue_bufs)
+            T.args.engine = nat.ENGINE_LAUNCHES
+            T.args.gemm = nat.GEMM_AUTO
+            res = torch.zeros(256, dtype=torch.uint8, device=T.y.device)
+            T.args.status = nat.dptr(res)
+            nat.check(nat.lib().amp_vamp_run(C.byref(T.dims), C.byref(T.const), C.byref(T.args), T.stream),
+                      'amp_vamp_run (rescue)')
+            self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
+            return read_result(res)
 
     def max_epochs(self, k: int) -> int:
         """The most epochs of this config ONE persistent launch holds (amp_vamp_max_epochs:
@@ -353,8 +398,11 @@ class VAMP(LazyResult, nn.Module):
             raw = host.numpy()
             status = nat.AmpStatus.from_buffer_copy(raw[e * st_sz:(e + 1) * st_sz].tobytes())
             counts = nat.AmpCounts.from_buffer_copy(raw[E * st_sz + e * ct_sz:E * st_sz + (e + 1) * ct_sz].tobytes())
-            if status.nan_state < 0:
-                raise RuntimeError('amp_vamp_detect_count_epochs: persistent engine grid barrier timed out')
+            status, counts = self._check_grid(
+                status, counts, lambda: self._rescue_forward(Uc, sc, Vhc, y[e * B:(e + 1) * B], SNR,
+                                                             x[e * B:(e + 1) * B], sym[e * B * cfg.L:(e + 1) * B * cfg.L],
+                                                             idx[e * B * cfg.L:(e + 1) * B * cfg.L]),
+                'amp_vamp_detect_count_epochs')
             L.last_counts, L.last_status = counts, status
             L.record(L.rates_from_counts(counts), int(status.T))
 

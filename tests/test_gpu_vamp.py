@@ -299,15 +299,24 @@ def _check_T(got, ref, max_iter, ver_ref=0.0, ref_pert=None):
 
     With `ref_pert` — the reference rerun on the same inputs with y moved by one float32 ulp
     (make_goldens.perturbed_rerun), i.e. how far the reference's own early exit moves under a
-    rounding-sized change — the count must lie within one iteration of the span of the two
-    reference runs: exact where the early exit is well conditioned (both runs agree and the
-    loop ran to the end or stopped within 3 iterations), +-1 elsewhere, wider only where the
-    reference itself moved.  Without it (goldens that predate the rerun): exact at the end / by
-    3 iterations, the noise-limited range where the detector fails (VER > 0.5), else +-5."""
+    rounding-sized change:
+    * both runs agree: exact where the exit is well conditioned (the loop ran to the end or
+      stopped within 3 iterations), else within one iteration;
+    * the reference itself moved (lo != hi: its exit is decided by rounding): within one
+      iteration of the span; in the noise-limited regime where the detector fails (VER > 0.5) the
+      allclose test compares a non-converging var trajectory, so any count from lo - 1 up to the
+      cap.
+    Without it (goldens that predate the rerun): exact at the end / by 3 iterations, the
+    noise-limited range where the detector fails (VER > 0.5), else +-5."""
     if ref_pert is not None:
         lo, hi = min(ref, ref_pert), max(ref, ref_pert)
-        if lo == hi and (ref == max_iter or ref <= 3):
-            assert got == ref, (got, ref)
+        if lo == hi:
+            if ref == max_iter or ref <= 3:
+                assert got == ref, (got, ref)
+            else:
+                assert lo - 1 <= got <= hi + 1, (got, ref, ref_pert)
+        elif ver_ref > 0.5:
+            assert lo - 1 <= got <= max_iter, (got, ref, ref_pert)
         else:
             assert lo - 1 <= got <= hi + 1, (got, ref, ref_pert)
     elif ref == max_iter or ref <= 3:
