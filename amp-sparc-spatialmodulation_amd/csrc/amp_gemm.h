@@ -75,6 +75,14 @@ __host__ __device__ __forceinline__ size_t x3_index(int o, int j, int f, int J) 
     return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 6 + f) * 64 + lane) * 8 + (kk & 7);
 }
 
+// The same for the fp16x2 form (gemm_h2): four planes per (tile, group), f = 0-1: Re h0 h1,
+// 2-3: Im h0 h1.
+__host__ __device__ __forceinline__ size_t h2_index(int o, int j, int f, int J) {
+    const int kk = j & 31;
+    const int lane = (o & 15) + 16 * (kk >> 3);
+    return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 4 + f) * 64 + lane) * 8 + (kk & 7);
+}
+
 // XCD-aware tile order.  Workgroups are dispatched in linear order (x fastest) round-robin over
 // the 8 XCDs, each with its own 4 MB L2.  The row-block-fastest grid would make every XCD sweep
 // ALL column blocks, i.e. the whole packed weight (8 MB for BAMP's H at cfg5) through each L2.

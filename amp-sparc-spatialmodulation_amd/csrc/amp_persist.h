@@ -230,6 +230,153 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
     }
 }
 
+// ---- split-precision complex GEMM (fp16x2) ----
+// v 2^e = h0 + h1 with fp16 pieces (round-to-nearest-even; 22 significant bits), so a product
+// keeps the three terms h0g0 h0g1 h1g0 (the dropped h1g1 is <= 2^-22 of it) on
+// v_mfma_f32_16x16x32_f16 with f32 accumulation, and the power-of-two scales come off exactly in
+// the epilogue.  fp16's exponent range is the price: the operator is scaled by 2^H2_EX (entries of
+// magnitude < 4; the SVD factors of vamp.py have |v| <= 1), every A row by its own 2^e that puts
+// the row's max |value| in [2^13, 2^14) (h2_row_exp).  Against bf16x3: 8 bytes per complex
+// operator entry instead of 12 and 12 MFMAs per complex tile-group instead of 24
+// (tools/ubench/gemm_h2_ubench.hip at cfg4: 10.4k vs 18.6k cycles per GEMM, max |error| 8.8e-7 vs
+// a sequential f32 sum's 1.4e-6 and bf16x3's 1.3e-6 on the same data).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+constexpr int H2_EX = 14;   // operator scale exponent (amp_weights.hip WPACKH2)
+
+// The exponent e that puts m 2^e (m = a row's max |value|) in [2^13, 2^14); 0 for 0 / inf / NaN.
+__device__ __forceinline__ int h2_row_exp(float m) {
+    if (!(m > 0.f) || !__builtin_isfinite(m)) return 0;
+    return 14 - __builtin_amdgcn_frexp_expf(m);
+}
+
+// Two (scaled) values -> their two packed fp16 pieces (x in the low half).  A non-finite first
+// piece keeps a zero residual.
+__device__ __forceinline__ void split2x2(float x, float y, unsigned& p0, unsigned& p1) {
+    const f32x2_t v = {x, y};
+    const f16x2_t h0 = __builtin_convertvector(v, f16x2_t);
+    const f32x2_t b = __builtin_convertvector(h0, f32x2_t);
+    f32x2_t r = v - b;
+    r.x = __builtin_isfinite(b.x) ? r.x : 0.0f;
+    r.y = __builtin_isfinite(b.y) ? r.y : 0.0f;
+    const f16x2_t h1 = __builtin_convertvector(r, f16x2_t);
+    p0 = __builtin_bit_cast(unsigned, h0);
+    p1 = __builtin_bit_cast(unsigned, h1);
+}
+
+// Scalar form (weight builder): the two pieces of x 2^e.
+__device__ __forceinline__ void split2(float x, int e, unsigned& p0, unsigned& p1) {
+    unsigned q0, q1;
+    split2x2(__builtin_amdgcn_ldexpf(x, e), 0.0f, q0, q1);
+    p0 = q0 & 0xffffu; p1 = q1 & 0xffffu;
+}
+
+// Eight consecutive complex values of one row (already scaled) -> the four fp16 planes
+// (Re h0 h1, Im h0 h1) of an h2 A operand: plane f, row `row`, elements j0 .. j0+7.
+__device__ __forceinline__ void h2_store8(unsigned short* sP, int ldx, int row, int j0, const float (&re)[8],
+                                          const float (&im)[8]) {
+    u32x4 q[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        unsigned a0, a1, b0, b1;
+        split2x2(re[2 * h], re[2 * h + 1], a0, a1);
+        split2x2(im[2 * h], im[2 * h + 1], b0, b1);
+        q[0][h] = a0; q[1][h] = a1; q[2][h] = b0; q[3][h] = b1;
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + j0) = q[f];
+}
+
+// x3_store_acc for the h2 planes (values already scaled).
+__device__ __forceinline__ void h2_store_acc(unsigned short* sP, int ldx, int o, const float (&vr)[4],
+                                             const float (&vi)[4]) {
+    const int lane = threadIdx.x & 63;
+    const bool odd = (lane & 1) != 0;
+    float gr[2], gi[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        gr[h] = dpp_swap_pair(odd ? vr[h] : vr[2 + h]);
+        gi[h] = dpp_swap_pair(odd ? vi[h] : vi[2 + h]);
+    }
+    const int row0 = 4 * (lane >> 4) + (odd ? 2 : 0);
+    unsigned short* p = sP + row0 * ldx + (o & ~1);
+    const int pl = 16 * ldx;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float mr = odd ? vr[2 + h] : vr[h], mi = odd ? vi[2 + h] : vi[h];
+        unsigned q[4];
+        split2x2(odd ? gr[h] : mr, odd ? mr : gr[h], q[0], q[1]);
+        split2x2(odd ? gi[h] : mi, odd ? mi : gi[h], q[2], q[3]);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) *reinterpret_cast<unsigned*>(p + f * pl + h * ldx) = q[f];
+    }
+}
+
+__device__ __forceinline__ f16x8 as_f16x8(u32x4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// gemm_x3's contract on the h2 planes: A = four fp16 planes in LDS (Re h0 h1, Im h0 h1), X packed
+// by h2_index (amp_gemm.h) as four planes per (tile, group).  The accumulators hold the product
+// of the SCALED operands (A 2^e_row, X 2^H2_EX): the caller takes the scales off.
+template <int NT, int G, int R = 1>
+__device__ __forceinline__ void gemm_h2(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
+                                        f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
+    constexpr int RR = G < R ? G : R;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { cr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; ci[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 4 * 1024, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = lane * 16;
+    u32x4 ring[RR][NT][4];
+#pragma unroll
+    for (int d = 0; d < RR; ++d)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 4 + f) * 1024, 0);
+    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * (lane >> 4);
+    const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+    u32x4 an[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int d = g % RR;
+        u32x4 a[4], na[2];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) a[f] = an[f];
+        if (g + 1 < G) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * (g + 1));
+        }
+#pragma unroll
+        for (int f = 0; f < 2; ++f) na[f] = a[2 + f] ^ sgn;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const u32x4* w = ring[d][t];   // w[0] / w[1]: Re h0 / h1, w[2] / w[3]: Im h0 / h1
+#define AMP_MH(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(x), as_f16x8(y), acc, 0, 0, 0)
+            // smallest terms first: Cr = Ar.Xr - Ai.Xi, Ci = Ar.Xi + Ai.Xr
+            AMP_MH(cr[t], a[0], w[1]);  AMP_MH(ci[t], a[0], w[3]);
+            AMP_MH(cr[t], a[1], w[0]);  AMP_MH(ci[t], a[1], w[2]);
+            AMP_MH(cr[t], na[0], w[3]); AMP_MH(ci[t], a[2], w[1]);
+            AMP_MH(cr[t], na[1], w[2]); AMP_MH(ci[t], a[3], w[0]);
+            AMP_MH(cr[t], a[0], w[0]);  AMP_MH(ci[t], a[0], w[2]);
+            AMP_MH(cr[t], na[0], w[2]); AMP_MH(ci[t], a[2], w[0]);
+#undef AMP_MH
+        }
+        if (g + RR < G) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+                    ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + RR) * 4 + f) * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Grid barrier: arrival counter + abort word in pbar (zeroed before the launch).  The
 // workgroup's payload stores precede it in program order (thread 0 stores them or the
 // barrier below orders them); agent-scope release on arrival, acquire after the wait.

@@ -58,9 +58,9 @@ struct VampK {
     DecWG* dwg;                 // [nwg] per-workgroup records
     amp_counts* counts;         // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
-    int x3;                      // persistent engine GEMMs on the bf16x3 engine (Wx1 / Wx2)
-    const void* Wx1;             // Vh X3-packed (x3_index, O = k, J = N)
-    const void* Wx2;             // V  X3-packed (O = N, J = k)
+    int x3;                      // persistent engine GEMMs: 0 f32 MFMA, 1 bf16x3, 2 fp16x2 (Wx1 / Wx2)
+    const void* Wx1;             // Vh X3- / H2-packed (x3_index / h2_index, O = k, J = N)
+    const void* Wx2;             // V  X3- / H2-packed (O = N, J = k)
     XState* xs;                  // trial-sharded exchange words (amp_vamp_run_sharded)
     float* dump;                 // diagnostic per-iteration state dump (amp_vamp_debug_dump), else null
     Const c;

@@ -405,6 +405,25 @@ bool gemm_f32_requested() {
     return v;
 }
 
+// AMP_VAMP_GEMM=x3 keeps the bf16x3 form where AUTO would pick fp16x2 (A/B runs)
+static bool gemm_x3_requested() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_VAMP_GEMM");
+        return e && e[0] == 'x';
+    }();
+    return v;
+}
+
+// The persistent engine's GEMM arithmetic for a shape whose planes fit (amp_vamp_args.gemm):
+// 0 f32 MFMA, 1 bf16x3, 2 fp16x2.  AUTO: fp16x2 (the fastest, f32-level accuracy), unless the
+// environment asks for f32 or bf16x3.
+static int vamp_gemm_mode(int gemm, bool fits) {
+    if (gemm == AMP_GEMM_H2) return 2;
+    if (gemm == AMP_GEMM_X3) return 1;
+    if (gemm == AMP_GEMM_F32 || !fits || gemm_f32_requested()) return 0;
+    return gemm_x3_requested() ? 1 : 2;
+}
+
 static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64) {
     int rc = check_dims(d, c);
     if (rc) return rc;
@@ -439,11 +458,12 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
-    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_X3, "amp_vamp: gemm %d", a->gemm);
+    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_H2, "amp_vamp: gemm %d", a->gemm);
     const bool x3_fits = vamp_persist_x3_fits(d->N, a->k, d->L);
-    AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || x3_fits, "amp_vamp: the bf16x3 engine needs k == N, N %% 64 == 0 and "
-                "its LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
-    P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && x3_fits && !gemm_f32_requested())) ? 1 : 0;
+    AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2) || x3_fits,
+                "amp_vamp: the split-precision engines need k == N, N %% 64 == 0 and "
+                "their LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
+    P.x3 = vamp_gemm_mode(a->gemm, x3_fits);
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.dump = debug_dump_ptr();
     return AMP_OK;
@@ -536,10 +556,11 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     const bool yk = P.ytil_in_kernel != 0;
     CWeightJob j[3];
     if (P.x3) {
-        //   q = Vh r~    (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N   (bf16x3 planes)
-        j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wx1, P.N, P.k, WPACKX3};
+        const int pk = P.x3 == 2 ? WPACKH2 : WPACKX3;
+        //   q = Vh r~    (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N   (bf16x3 / fp16x2 planes)
+        j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wx1, P.N, P.k, pk};
         //   V (x~ - q)   (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
-        j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wx2, P.k, P.N, WPACKX3};
+        j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wx2, P.k, P.N, pk};
     } else {
     //   q = Vh r~        (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N
     j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wq1, 2 * P.N, 2 * P.k, WPACK16};
@@ -641,10 +662,11 @@ int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const 
 }
 
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
-    if (!d || k <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_X3) return AMP_E_ARG;
+    if (!d || k <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_H2) return AMP_E_ARG;
     const bool fits = vamp_persist_x3_fits(d->N, k, d->L);
-    if (gemm == AMP_GEMM_X3) return fits ? AMP_GEMM_X3 : AMP_E_ARG;
-    return (gemm == AMP_GEMM_AUTO && fits && !gemm_f32_requested()) ? AMP_GEMM_X3 : AMP_GEMM_F32;
+    if ((gemm == AMP_GEMM_X3 || gemm == AMP_GEMM_H2) && !fits) return AMP_E_ARG;
+    static const int code[3] = {AMP_GEMM_F32, AMP_GEMM_X3, AMP_GEMM_H2};
+    return code[vamp_gemm_mode(gemm, fits)];
 }
 
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine) {

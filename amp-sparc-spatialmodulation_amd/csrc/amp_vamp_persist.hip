@@ -98,6 +98,7 @@ bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs) {
 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_x3.hip
+int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_h2.hip
 
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
@@ -115,6 +116,7 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) {
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
+    if (P.x3 == 2) return persist_dispatch_h2(P, dc, st);
     if (P.x3) return persist_dispatch_x3(P, dc, st);
     if (persist_waves() == 4) {
         switch (P.N) {

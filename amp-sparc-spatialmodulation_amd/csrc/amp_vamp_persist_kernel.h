@@ -169,7 +169,10 @@ __global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, 
 // same 16 NT real columns as the f32 form), the operators are the X3-packed Vh / V (Wx1 / Wx2).
 // OCC: workgroups per CU the register allocation is bounded for (__launch_bounds__' minimum
 // waves per SIMD = OCC * NWV / 4); 2 only for the side-by-side cfg2 epochs (N = 64).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1>
+// H2 (with X3): the split-precision GEMMs in the fp16x2 form (gemm_h2: four A planes, the operators
+// h2-packed); every A row (r~, then w) is scaled by its own power of two (h2_row_exp) before the
+// split and the accumulators are scaled back by 2^-(e_row + H2_EX).
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
     static_assert(!X3 || (NWV == 4 && NT % 2 == 0), "X3: four waves, whole complex tiles");
     constexpr int PWG = 64 * NWV;
@@ -180,6 +183,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
     __shared__ double s_d[PWG / 64][4];
+    __shared__ float s_hmax[PWG / 64][PBM];   // H2: per-wave row maxima of the A operand
+    __shared__ int s_hexp[PBM];               // H2: r~ row exponents (for GEMM1's epilogue)
     const PLayout Y = playout(P.N, P.k, P.L, X3);
     float* sA = lds + Y.offA;
     float* sR = lds + Y.offR;
@@ -284,7 +289,55 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         const float* vprev = lds + ((t & 1) ? Y.offV0 : Y.offV1);
         float* vnew = lds + ((t & 1) ? Y.offV1 : Y.offV0);
         // 1. A <- r~ (vamp.py:91; t = 0: dxdr 0, normScalar 1)
-        if constexpr (X3) {
+        if constexpr (H2) {
+            // r~ rows in registers (item e: row e % PBM == tid % PBM, 8 complex values), the
+            // row's max |value| over the workgroup, then the scaled split
+            constexpr int IPT = (NT + 3) / 4;             // items per thread: PBM N / 8 / PWG
+            const int row = tid % PBM;
+            float re[IPT][8], im[IPT][8];
+            float m = 0.f;
+#pragma unroll
+            for (int i = 0; i < IPT; ++i) {
+                const int e = tid + i * PWG;
+                const int j0 = 8 * (e / PBM);
+                const bool ok = e < PBM * (N >> 3);
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    float4 x = make_float4(0.f, 0.f, 0.f, 0.f), q = x;
+                    if (ok) {
+                        x = *reinterpret_cast<const float4*>(sX + row * ldr + 2 * j0 + 4 * h);
+                        q = *reinterpret_cast<const float4*>(sR + row * ldr + 2 * j0 + 4 * h);
+                    }
+                    re[i][2 * h] = (x.x - cur.dxdr_prev * q.x) * cur.ns_prev;
+                    im[i][2 * h] = (x.y - cur.dxdr_prev * q.y) * cur.ns_prev;
+                    re[i][2 * h + 1] = (x.z - cur.dxdr_prev * q.z) * cur.ns_prev;
+                    im[i][2 * h + 1] = (x.w - cur.dxdr_prev * q.w) * cur.ns_prev;
+                }
+#pragma unroll
+                for (int h = 0; h < 8; ++h) m = fmaxf(m, fmaxf(fabsf(re[i][h]), fabsf(im[i][h])));
+            }
+            m = fmaxf(m, __shfl_xor(m, 16));
+            m = fmaxf(m, __shfl_xor(m, 32));
+            if (lane < PBM) s_hmax[wave][lane] = m;
+            __syncthreads();
+            float mr = s_hmax[0][row];
+#pragma unroll
+            for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][row]);
+            const int ex = h2_row_exp(mr);
+            if (tid < PBM) s_hexp[tid] = ex;
+#pragma unroll
+            for (int i = 0; i < IPT; ++i) {
+                const int e = tid + i * PWG;
+                if (e < PBM * (N >> 3)) {
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) {
+                        re[i][h] = __builtin_amdgcn_ldexpf(re[i][h], ex);
+                        im[i][h] = __builtin_amdgcn_ldexpf(im[i][h], ex);
+                    }
+                    h2_store8(sP, ldx, row, 8 * (e / PBM), re[i], im[i]);
+                }
+            }
+        } else if constexpr (X3) {
             for (int e = tid; e < PBM * (N >> 3); e += PWG) {   // 8 complex values per item
                 // consecutive items walk the 16 rows (row stride 2N + 4 floats): each group of 16
                 // lanes reads 16 different bank quads (item-major rows put 4 lanes on each)
@@ -315,13 +368,73 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
         f32x4 acc[NT];
         f32x4 cr[NC], ci[NC];
-        if constexpr (X3)
+        if constexpr (H2)
+            gemm_h2<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
+        else if constexpr (X3)
             gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx1, cc0, cr, ci);
         else
             gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
+        float hsc[4];                                 // H2: 2^-(e_row + H2_EX) of this lane's rows
+        int hew[4];                                   // H2: the w rows' exponents
+        if constexpr (H2) {
+            // w = scale (y~ + vr q) - q for every tile of this wave, its rows' max |w| to LDS; the
+            // barrier below also ends every wave's reads of the r~ planes
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + H2_EX));
+            float mrow[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t2 = 0; t2 < NC; ++t2) {
+                const float sc = 1.0f / (s2c[t2] + cur.vr);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float qr = cr[t2][r] * hsc[r], qi = ci[t2][r] * hsc[r];
+                    cr[t2][r] = sc * (yt[2 * t2][r] + cur.vr * qr) - qr;
+                    ci[t2][r] = sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi;
+                    mrow[r] = fmaxf(mrow[r], fmaxf(fabsf(cr[t2][r]), fabsf(ci[t2][r])));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int sh = 1; sh < 16; sh <<= 1) mrow[r] = fmaxf(mrow[r], __shfl_xor(mrow[r], sh));
+            }
+            if ((lane & 15) == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s_hmax[wave][4 * (lane >> 4) + r] = mrow[r];
+            }
+        }
         __syncthreads();
         stamp(t, 2);
-        if constexpr (X3) {
+        if constexpr (H2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float mr = s_hmax[0][4 * (lane >> 4) + r];
+#pragma unroll
+                for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][4 * (lane >> 4) + r]);
+                hew[r] = h2_row_exp(mr);
+            }
+#pragma unroll
+            for (int t2 = 0; t2 < NC; ++t2) {
+                const int o = 16 * (cc0 + t2) + (lane & 15);
+                float wr[4], wi[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    wr[r] = __builtin_amdgcn_ldexpf(cr[t2][r], hew[r]);
+                    wi[r] = __builtin_amdgcn_ldexpf(ci[t2][r], hew[r]);
+                }
+                h2_store_acc(sP, ldx, o, wr, wi);
+                if (P.dump) {
+                    float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 0) * PBM * twoN;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o] = cr[t2][r];
+                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = ci[t2][r];
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(hew[r] + H2_EX));
+        } else if constexpr (X3) {
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lane & 15);
@@ -358,7 +471,15 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         stamp(t, 3);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
         if constexpr (X3) {
-            gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx2, cc0, cr, ci);
+            if constexpr (H2) {
+                gemm_h2<NC, G3>(sP, ldx, P.Wx2, cc0, cr, ci);
+#pragma unroll
+                for (int t2 = 0; t2 < NC; ++t2)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
+            } else {
+                gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx2, cc0, cr, ci);
+            }
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lane & 15);
@@ -551,9 +672,9 @@ static inline int den_u() {
 
 // Launch path: persist_grid_launch (amp_host.h): a plain launch after an explicit co-residency
 // check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1>
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC, H2>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
     // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
@@ -577,23 +698,23 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
     return persist_grid_launch("vamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
-template <int NT, int NWV, bool X3, int OCC = 1>
+template <int NT, int NWV, bool X3, int OCC = 1, bool H2 = false>
 static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV, 4, X3, OCC>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC>(P, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC, H2>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC, H2>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV, 4, X3, OCC, H2>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC, H2>(P, dc, st);
     case 16:
         // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8;
         // f32 engine only: 4 and 8 spill beside the bf16x3 GEMM's registers)
-        if constexpr (X3) return persist_launch_t<NT, 16, NWV, AMP_X3_DU, X3, OCC>(P, dc, st);
+        if constexpr (X3) return persist_launch_t<NT, 16, NWV, AMP_X3_DU, X3, OCC, H2>(P, dc, st);
         switch (den_u()) {
         case 4: return persist_launch_t<NT, 16, NWV, 4, X3>(P, dc, st);
         case 8: return persist_launch_t<NT, 16, NWV, 8, X3>(P, dc, st);
         default: return persist_launch_t<NT, 16, NWV, 2, X3>(P, dc, st);
         }
-    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC>(P, dc, st);
+    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC, H2>(P, dc, st);
     }
 }
 

@@ -142,6 +142,33 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         }
         return;
     }
+    if (J.packed == WPACKH2) {
+        // fp16x2 planes of X 2^H2_EX (amp_persist.h gemm_h2): kap = J, ncp = O (complex counts).
+        // |x| >= 4 leaves fp16's range: the piece is then inf, so the GEMM's result is non-finite
+        // (never silently wrong); the SVD factors of vamp.py have |x| <= 1.
+        unsigned short* w2 = reinterpret_cast<unsigned short*>(J.wt);
+        const long tot = (long)J.ncp * J.kap;
+        for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+            const int o = (int)(e / J.kap), j = (int)(e % J.kap);
+            float xr = 0.f, xi = 0.f;
+            if (o < J.O && j < J.J) {
+                const float2 v = J.src[o * J.so + j * J.sj];
+                xr = v.x;
+                xi = J.conj ? -v.y : v.y;
+                if (J.rowscale) {
+                    const float s = J.rowscale[o];
+                    xr = s * xr;
+                    xi = s * xi;
+                }
+            }
+            unsigned p[4];
+            split2(xr, H2_EX, p[0], p[1]);
+            split2(xi, H2_EX, p[2], p[3]);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) w2[h2_index(o, j, f, J.kap)] = (unsigned short)p[f];
+        }
+        return;
+    }
     const long total = (long)(J.ncp / 2) * (J.kap / 2);
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / (J.kap / 2)), j = (int)(e % (J.kap / 2));
@@ -169,13 +196,14 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     long most = 0;
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
-        AMP_REQUIRE((J.packed == WPACKX3 ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
+        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2;
+        AMP_REQUIRE((planar ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
                          (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||
-                         (J.packed == WPACKX3 && J.kap % 32 == 0 && J.ncp % 16 == 0)),
+                         (planar && J.kap % 32 == 0 && J.ncp % 16 == 0)),
                     "build_cweights: job %d kap %d / ncp %d not tiled for layout %d", i, J.kap, J.ncp, J.packed);
         P.j[i] = J;
-        most = std::max(most, J.packed == WPACKX3 ? (long)J.ncp * J.kap : (long)(J.ncp / 2) * (J.kap / 2));
+        most = std::max(most, planar ? (long)J.ncp * J.kap : (long)(J.ncp / 2) * (J.kap / 2));
     }
     P.zero = zero;
     P.nzero = zero ? nzero : 0;

@@ -286,7 +286,8 @@ def main():
         kern, flops_launch = 'vamp_k2 (GEMM2 + Onsager update + section denoiser)', flops_mv
         kms = {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}
     achieved = flops_launch / (ms[1] * 1e-3) / 1e12
-    x3 = persistent and nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) == nat.GEMM_X3
+    gmode = nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) if persistent else nat.GEMM_F32
+    gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2'}.get(gmode, 'f32')
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -317,13 +318,15 @@ def main():
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),
                      'kernel': kern, 'flop_per_launch': flops_launch,
-                     'gemm': 'bf16x3' if x3 else 'f32'},
+                     'gemm': gname},
     }
-    if x3:
-        # the f32 products run as six bf16 MFMA products each (amp_persist.h gemm_x3): the matrix
-        # cores' own rate is 6x the f32-equivalent one, against the dense bf16 peak
-        out['roofline']['bf16_issued'] = {'achieved': 6 * achieved, 'peak': BF16_MFMA_PEAK_TFLOPS,
-                                          'frac': 6 * achieved / BF16_MFMA_PEAK_TFLOPS}
+    if gname != 'f32':
+        # the f32 products run as six bf16 (bf16x3) or three fp16 (fp16x2) MFMA products each
+        # (amp_persist.h gemm_x3 / gemm_h2): the matrix cores' own rate against the dense peak of
+        # that input type (bf16 and fp16 have the same dense peak on gfx950)
+        mult = 6 if gname == 'bf16x3' else 3
+        out['roofline'][gname[:4] + '_issued'] = {'achieved': mult * achieved, 'peak': BF16_MFMA_PEAK_TFLOPS,
+                                                 'frac': mult * achieved / BF16_MFMA_PEAK_TFLOPS}
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args.config, args.ebn0, args.seed, args.cpu_sample)
     print(json.dumps(out), flush=True)

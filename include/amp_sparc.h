@@ -89,7 +89,7 @@ typedef struct amp_vamp_args {
     int32_t k;          /* min(n, N) */
     int32_t max_iter;   /* config.N_Layers */
     int32_t engine;     /* amp_vamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT */
-    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 */
+    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 / _H2 */
     double noise_var;   /* Na/Nr/SNR (vamp.py:179) */
     double sparsity;    /* Na/Nt (vamp.py:155) */
     void* r;            /* out c64 [B][N]: decision input T.r (vamp.py:187) */
@@ -112,10 +112,18 @@ typedef struct amp_vamp_args {
  *  X3    split precision: every f32 operand as three bf16 pieces, six bf16 MFMA products per
  *        product (terms below 2^-24 relative dropped), f32 accumulation — the f32 GEMM's
  *        accuracy at 2.7x the MFMA rate (needs k == N, N % 64 == 0 and 160 KB of LDS);
- *  AUTO  X3 where it fits, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32). */
+ *  H2    split precision in fp16: every A row scaled by its own power of two, every value as two
+ *        fp16 pieces (22 significant bits), three fp16 MFMA products per product, f32
+ *        accumulation, the scales taken off exactly — f32-level accuracy (max error below a
+ *        sequential f32 sum's) with 2/3 of X3's operator bytes and half its MFMAs; the operators
+ *        must have entries of magnitude < 4 (SVD factors: <= 1; larger entries give non-finite
+ *        results, never silently wrong ones); same shape constraints as X3;
+ *  AUTO  H2 where the planes fit, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32,
+ *        AMP_VAMP_GEMM=x3 picks X3). */
 #define AMP_GEMM_AUTO 0
 #define AMP_GEMM_F32 1
 #define AMP_GEMM_X3 2
+#define AMP_GEMM_H2 3
 
 #define AMP_ENGINE_AUTO 0
 #define AMP_ENGINE_LAUNCHES 1
@@ -124,8 +132,8 @@ typedef struct amp_vamp_args {
 /* The engine amp_vamp_run will use for this shape on the current device (LAUNCHES or
  * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
-/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_X3 or AMP_GEMM_F32
- * (AMP_E_ARG when `gemm` is AMP_GEMM_X3 and the shape does not fit it). */
+/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_H2, AMP_GEMM_X3 or
+ * AMP_GEMM_F32 (AMP_E_ARG when `gemm` is AMP_GEMM_X3 / _H2 and the shape does not fit it). */
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
  * phase into trace (device, nwg * max_iter * 10 + 2 * nwg uint64; layout in amp_vamp.hip). */

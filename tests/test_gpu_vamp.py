@@ -214,16 +214,17 @@ VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk'
 
 
 ENGINES = {'launches': 1, 'persistent': 2}   # amp_native.ENGINE_*
-# (engine, persistent GEMM arithmetic): 'persistent' = the product default (bf16x3 where it fits)
-VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1)}
+# (engine, persistent GEMM arithmetic): 'persistent' = the product default (fp16x2 where it fits),
+# 'persistent-x3' the bf16x3 form, 'persistent-f32' the f32-MFMA form
+VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 'persistent-x3': (2, 2)}
 
 
 @pytest.mark.parametrize('variant', sorted(VARIANTS))
 @pytest.mark.parametrize('name,key', VAMP_POINTS)
 def test_vamp_curve_point(device, name, key, variant):
     """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar),
-    for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible) and both
-    GEMM arithmetics of the persistent engine (split bf16x3, the default, and f32 MFMA)."""
+    for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible) and the three
+    GEMM arithmetics of the persistent engine (split fp16x2, the default; split bf16x3; f32 MFMA)."""
     from vamp import VAMP
     ent = CURVES[name]
     ref = ent['points'][key]
@@ -270,10 +271,10 @@ def test_vamp_engines_agree(device, ebn0):
 @pytest.mark.parametrize('name', ['cfg4_vamp_16qam', 'cfg2_vamp_qpsk'])
 @pytest.mark.parametrize('iters', [1, 3])
 def test_vamp_x3_gemm_matches_f32(device, name, iters):
-    """The split-precision bf16x3 persistent GEMMs against the f32-MFMA ones, both measured
-    against the numpy oracle (f32 BLAS GEMMs in yet another summation order): after 1 and 3
-    iterations r of the x3 engine is as close to the oracle as the f32 engine's (tolerance: 4x
-    the f32 engine's own deviation, floored at 2e-6 of max|r|)."""
+    """The split-precision persistent GEMMs (bf16x3 and fp16x2) against the f32-MFMA ones, all
+    measured against the numpy oracle (f32 BLAS GEMMs in yet another summation order): after 1
+    and 3 iterations r of each split engine is as close to the oracle as the f32 engine's
+    (tolerance: 4x the f32 engine's own deviation, floored at 2e-6 of max|r|)."""
     from vamp import VAMP
     import amp_native as nat
     ent = CURVES[name]
@@ -281,7 +282,8 @@ def test_vamp_x3_gemm_matches_f32(device, name, iters):
     inp = _regen_inputs(cfg, 0, 8.0)
     assert nat.lib().amp_vamp_select_engine(cfg.dims(), ent['Nt'], nat.ENGINE_AUTO) == nat.ENGINE_PERSISTENT
     r = {}
-    for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+    assert nat.lib().amp_vamp_select_gemm(cfg.dims(), ent['Nt'], nat.GEMM_AUTO) == nat.GEMM_H2
+    for gemm in (nat.GEMM_F32, nat.GEMM_X3, nat.GEMM_H2):
         T = VAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm).detect(inp['U'], inp['s'], inp['Vh'], inp['y'],
                                                                      inp['SNR'])
         r[gemm] = T.r.clone().cpu().numpy()[..., 0]
@@ -291,7 +293,9 @@ def test_vamp_x3_gemm_matches_f32(device, name, iters):
     scale = float(np.abs(o).max())
     e32 = float(np.abs(r[nat.GEMM_F32] - o).max())
     ex3 = float(np.abs(r[nat.GEMM_X3] - o).max())
+    eh2 = float(np.abs(r[nat.GEMM_H2] - o).max())
     assert ex3 <= max(4 * e32, 2e-6 * scale), (ex3, e32, scale)
+    assert eh2 <= max(4 * e32, 2e-6 * scale), (eh2, e32, scale)
 
 
 def _check_T(got, ref, max_iter, ver_ref=0.0, ref_pert=None):
