@@ -121,6 +121,7 @@ SIGNATURES = {
     'amp_scamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_scamp_select_engine': (C.c_int, [_D, _I]),
     'amp_scamp_run': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
+    'amp_scamp_detect_count': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), C.POINTER(AmpVampDecideArgs), _P]),
     'amp_scamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),
     'amp_scamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _I, _P]),
     'amp_scamp_finalize': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P]),

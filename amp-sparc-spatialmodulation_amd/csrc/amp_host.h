@@ -202,6 +202,7 @@ struct CWeightJob {
     float* wt;
     int kap, ncp;
     int packed;
+    int ex = 14;        // WPACKH2: the operator's scale exponent (amp_persist.h H2_EX; SCAMP: SH2_EX)
 };
 // Up to 4 jobs in ONE launch; the same launch zeroes `nzero` words at `zero` (or none).
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);

@@ -243,6 +243,7 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 constexpr int H2_EX = 14;   // operator scale exponent (amp_weights.hip WPACKH2)
+constexpr int YH2_EX = 10;  // the y~ operator s Uh (entries s_o |U| < 64; the singular values are O(1))
 
 // The exponent e that puts m 2^e (m = a row's max |value|) in [2^13, 2^14); 0 for 0 / inf / NaN.
 __device__ __forceinline__ int h2_row_exp(float m) {

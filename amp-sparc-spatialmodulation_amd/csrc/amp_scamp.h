@@ -4,11 +4,17 @@
 
 #include <algorithm>
 
+#include "amp_decide.h"
 #include "amp_denoise.h"
 #include "amp_gemm.h"
 #include "amp_host.h"
 
 namespace amp {
+
+// fp16x2 persistent GEMMs (amp_scamp_persist_kernel.h, H2): the operator A is packed as A 2^SH2_EX,
+// so its entries must stay below 64 in magnitude (the channel's are ~CN(0, 1/Nr)).
+constexpr int SH2_EX = 10;
+
 
 constexpr int SRWG = 1024;
 constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in registers / LDS
@@ -63,6 +69,13 @@ struct ScampK {
     const int* bandA;
     const int* bandB;
     XState* xs;            // trial-sharded exchange words (amp_scamp_run_sharded)
+    // fused decision (amp_scamp_detect_count: decide_epilogue at the end of scamp_persist)
+    int dec_on, ibits;
+    const float2* xtrue;   // [B][N] transmitted x
+    const long long* sym;  // [B*L] gray labels
+    const long long* idx;  // [B*L] flat nonzero indices
+    DecWG* dwg;            // [nwg] per-workgroup records
+    amp_counts* counts;    // out
     Const c;
 };
 
@@ -78,6 +91,7 @@ struct ScampWs {
     double* pxch;
     int *bandA, *bandB;
     XState* xs;
+    DecWG* dwg;
     size_t bytes;
 };
 
@@ -124,6 +138,7 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.bandA = cv.take<int>((size_t)2 * (P.ncpA / 128));
     w.bandB = cv.take<int>((size_t)2 * (P.ncpB / P.bn));
     w.xs = cv.take<XState>(1);
+    w.dwg = cv.take<DecWG>((size_t)nwg);
     w.bytes = cv.off;
     return w;
 }
@@ -140,6 +155,6 @@ __device__ __forceinline__ float scamp_gamma(const ScampK& P, const float* psi_r
 
 bool scamp_persist_eligible(const amp_dims* d, int ncu);
 bool scamp_persist_x3_fits(const amp_dims* d);
-int scamp_persist_launch(const ScampK& P, const Const64& c64, hipStream_t st);
+int scamp_persist_launch(const ScampK& P, const DecConst& dc, hipStream_t st);
 
 }  // namespace amp

@@ -546,6 +546,15 @@ static bool scamp_gemm_f32_requested() {
     return v;
 }
 
+// AMP_SCAMP_GEMM=h2: AMP_GEMM_AUTO picks the fp16x2 persistent GEMMs instead of bf16x3 (A/B runs)
+static bool scamp_gemm_h2_requested() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_SCAMP_GEMM");
+        return e && e[0] == 'h';
+    }();
+    return v;
+}
+
 // Block-banded A (Lin > 1 or Lout > 1): the GEMMs skip the reduction blocks of each column tile
 // that hold only zeros (weight_kband over the packed weights, once per forward).  Off with
 // AMP_BAND_GEMM=0 (A/B runs).
@@ -589,12 +598,20 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.gen = 0;
     P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
+    P.dec_on = 0; P.ibits = 0; P.xtrue = nullptr; P.sym = nullptr; P.idx = nullptr; P.counts = nullptr;
+    P.dwg = w.dwg;
     P.c = to_const(c);
     c64 = to_const64(c);
-    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_X3, "amp_scamp: gemm %d", a->gemm);
+    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_H2, "amp_scamp: gemm %d", a->gemm);
     const bool fits = scamp_persist_x3_fits(d);
-    AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || fits, "amp_scamp: the bf16x3 engine's LDS carve exceeds 160 KB");
-    P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && fits && !scamp_gemm_f32_requested())) ? 1 : 0;
+    AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2) || fits,
+                "amp_scamp: the split-precision engine's LDS carve exceeds 160 KB");
+    // 0 f32 MFMA, 1 bf16x3, 2 fp16x2.  AUTO keeps bf16x3 for SCAMP: with fp16x2 one cfg3 golden
+    // (QPSK, 7 dB, seed 1) never meets the psi allclose exit (T 20 vs the reference's 6, VER / SER
+    // equal): at nMSE 1e-9 psi is ~1e-9 and torch.allclose's atol 1e-8 decides, which the
+    // fp16x2 products' 2^-22 terms move.  AMP_SCAMP_GEMM=f32 / h2 for A/B runs.
+    P.x3 = a->gemm == AMP_GEMM_H2 ? 2 : a->gemm == AMP_GEMM_X3 ? 1 : a->gemm == AMP_GEMM_F32 || !fits ? 0
+         : scamp_gemm_f32_requested() ? 0 : scamp_gemm_h2_requested() ? 2 : 1;
     return AMP_OK;
 }
 
@@ -605,10 +622,11 @@ static int scamp_persist_prepare(ScampK& P, const amp_scamp_args* a, hipStream_t
     P.gen = ++gen;
     CWeightJob j[2];
     if (P.x3) {
-        //   A x     (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N   (bf16x3 planes)
-        j[0] = CWeightJob{(const float2*)a->A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wx1, P.N, P.n, WPACKX3};
+        const int pk = P.x3 == 2 ? WPACKH2 : WPACKX3;
+        //   A x     (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N   (bf16x3 / fp16x2 planes)
+        j[0] = CWeightJob{(const float2*)a->A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wx1, P.N, P.n, pk, SH2_EX};
         //   A^H s   (scamp.py:57)   X[o][j] = conj(A[j][o]),  o < N, j < n
-        j[1] = CWeightJob{(const float2*)a->A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.Wx2, P.n, P.N, WPACKX3};
+        j[1] = CWeightJob{(const float2*)a->A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.Wx2, P.n, P.N, pk, SH2_EX};
         return build_cweights(j, 2, P.pbar, 64, st);
     }
     //   A x       (scamp.py:47)   X[o][j] = A[o][j],        o < n, j < N
@@ -685,6 +703,8 @@ static int scamp_finalize_impl(const ScampK& P, hipStream_t st) {
     return AMP_OK;
 }
 
+__global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out);   // amp_vamp_persist.hip
+
 }  // namespace amp
 
 extern "C" {
@@ -727,12 +747,42 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
                 "and ceil(B/16) = %d <= %d CUs", cdiv(d->B, 16), device_cu_count());
     if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
         if ((rc = scamp_persist_prepare(P, a, st))) return rc;
-        return scamp_persist_launch(P, c64, st);
+        DecConst dc;
+        static_cast<Const64&>(dc) = c64;   // no decision in this launch: only the float64 table is read
+        return scamp_persist_launch(P, dc, st);
     }
     if ((rc = scamp_prepare_impl(P, a, st))) return rc;
     for (int t = 0; t < P.max_iter; ++t)
         if ((rc = scamp_iterate_impl(P, c64, t, st))) return rc;
     return scamp_finalize_impl(P, st);
+}
+
+int amp_scamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a,
+                           const amp_vamp_decide_args* dec, void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts, "amp_scamp_detect_count: null pointer argument");
+    AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_scamp_detect_count: ibits_trunc out of range");
+    AMP_REQUIRE(d->Lin * d->Na * d->M == d->N, "amp_scamp_detect_count: inconsistent dims");
+    AMP_REQUIRE(a->engine != AMP_ENGINE_LAUNCHES && scamp_persist_eligible(d, device_cu_count()),
+                "amp_scamp_detect_count: needs the persistent engine ((2N, 2n) in {(128, 256), (256, 512), "
+                "(256, 256)}, M <= 64, ceil(B/16) = %d <= %d CUs)", cdiv(d->B, 16), device_cu_count());
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = scamp_persist_prepare(P, a, st))) return rc;
+    P.dec_on = 1;
+    P.ibits = dec->ibits_trunc;
+    P.xtrue = (const float2*)dec->x;
+    P.sym = (const long long*)dec->sym;
+    P.idx = (const long long*)dec->idx;
+    P.counts = (amp_counts*)dec->counts;
+    DecConst dc = to_decconst(c);
+    static_cast<Const64&>(dc) = c64;
+    if ((rc = scamp_persist_launch(P, dc, st))) return rc;
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);
+    AMP_LAUNCH_CHECK("vamp_decide_fold (scamp)");
+    return AMP_OK;
 }
 
 int amp_scamp_prepare(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream) {

@@ -40,9 +40,11 @@ bool scamp_persist_eligible(const amp_dims* d, int ncu) {
 }
 
 // NT1 = 2n / 64 column tiles per wave (GEMM1, K = 2N = 16 G1); NT2 = 2N / 64 (GEMM2, K = 2n)
-int scamp_persist_launch_x3(const ScampK& P, const Const64& c64, hipStream_t st);   // amp_scamp_persist_x3.hip
+int scamp_persist_launch_x3(const ScampK& P, const DecConst& c64, hipStream_t st);   // amp_scamp_persist_x3.hip
+int scamp_persist_launch_h2(const ScampK& P, const DecConst& c64, hipStream_t st);   // amp_scamp_persist_h2.hip
 
-int scamp_persist_launch(const ScampK& P, const Const64& c64, hipStream_t st) {
+int scamp_persist_launch(const ScampK& P, const DecConst& c64, hipStream_t st) {
+    if (P.x3 == 2) return scamp_persist_launch_h2(P, c64, st);
     if (P.x3) return scamp_persist_launch_x3(P, c64, st);
     const int twoN = 2 * P.N, twon = 2 * P.n;
     if (twoN == 128 && twon == 256) return spersist_launch_s<4, 8, 2, 16, false>(P, c64, st);

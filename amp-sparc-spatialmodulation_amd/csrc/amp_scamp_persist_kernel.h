@@ -5,6 +5,7 @@
 
 #include <stdlib.h>
 
+#include "amp_decide_fused.h"
 #include "amp_persist.h"
 #include "amp_scamp.h"
 
@@ -90,14 +91,19 @@ __device__ __forceinline__ float block_psi(const float* xrow, int lc, int Nt, in
 
 // X3: both GEMMs on the split-precision bf16x3 engine (amp_persist.h gemm_x3); the wave's complex
 // column tiles are NT1/2 (GEMM1) and NT2/2 (GEMM2), the same real columns as the f32 form.
-template <int NT1, int G1, int NT2, int G2, int KK, bool X3>
-__global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
+// H2 (with X3): the fp16x2 form (gemm_h2): every A row (x, then s = z / phi) scaled by its own
+// power of two before the split, the accumulators scaled back by 2^-(e_row + SH2_EX).
+template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false>
+__global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
     constexpr int PWG = 256, NW = 4;
+    const Const64& c64 = dc;   // the rare path's float64 table; dc also the fused decision's (dec_on)
     constexpr int NC1 = X3 ? NT1 / 2 : 1, NC2 = X3 ? NT2 / 2 : 1;
     static_assert(!X3 || (NT1 % 2 == 0 && NT2 % 2 == 0), "X3: whole complex tiles");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
     __shared__ double s_d[NW][4];
+    __shared__ float s_hmax[NW][SPB];   // H2: per-wave row maxima of the A operand
+    __shared__ int s_hexp[SPB];         // H2: x row exponents (for GEMM1's epilogue)
     const int N = P.N, n = P.n, L = P.L, M = P.M, Lin = P.Lin, Lout = P.Lout, Nt = P.Nt, Nr = P.Nr;
     const SLayout Y = slayout(N, n, L, Lin, Lout, X3);
     const int ldx = Y.ldx, ldz = Y.ldz;
@@ -178,7 +184,51 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
         // 2. GEMM1 A x (A operand: the x rows as they lie) ; z = y - A x + b z ; s = z / phi
         f32x4 acc1[NT1];
         f32x4 cr1[NC1], ci1[NC1];
-        if constexpr (X3) {
+        if constexpr (H2) {
+            // x rows in registers (item e: row e % SPB == tid % SPB), each row's max |x| over the
+            // workgroup, then the scaled split into the four fp16 planes
+            constexpr int IPT = (G1 + 15) / 16;              // items per thread: SPB N / 8 / PWG, N = G1 * 8
+            const int row = tid % SPB;
+            float re[IPT][8], im[IPT][8];
+            float m = 0.f;
+#pragma unroll
+            for (int i = 0; i < IPT; ++i) {
+                const int e = tid + i * PWG;
+                const bool ok = e < SPB * (N >> 3);
+                const int j0 = 8 * (e / SPB);
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (ok) v = *reinterpret_cast<const float4*>(sX + row * ldx + 2 * j0 + 4 * h);
+                    re[i][2 * h] = v.x; im[i][2 * h] = v.y; re[i][2 * h + 1] = v.z; im[i][2 * h + 1] = v.w;
+                }
+#pragma unroll
+                for (int h = 0; h < 8; ++h) m = fmaxf(m, fmaxf(fabsf(re[i][h]), fabsf(im[i][h])));
+            }
+            m = fmaxf(m, __shfl_xor(m, 16));
+            m = fmaxf(m, __shfl_xor(m, 32));
+            if (lane < SPB) s_hmax[wave][lane] = m;
+            __syncthreads();
+            float mr = s_hmax[0][row];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) mr = fmaxf(mr, s_hmax[w][row]);
+            const int ex = h2_row_exp(mr);
+            if (tid < SPB) s_hexp[tid] = ex;
+#pragma unroll
+            for (int i = 0; i < IPT; ++i) {
+                const int e = tid + i * PWG;
+                if (e < SPB * (N >> 3)) {
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) {
+                        re[i][h] = __builtin_amdgcn_ldexpf(re[i][h], ex);
+                        im[i][h] = __builtin_amdgcn_ldexpf(im[i][h], ex);
+                    }
+                    h2_store8(sP, ldp1, row, 8 * (e / SPB), re[i], im[i]);
+                }
+            }
+            __syncthreads();
+            gemm_h2<NC1, G1 / 4>(sP, ldp1, P.Wx1, cc1, cr1, ci1);
+        } else if constexpr (X3) {
             for (int e = tid; e < SPB * (N >> 3); e += PWG) {   // x rows -> bf16 planes, 8 per item
                 // consecutive items walk the 16 rows (stride 2N + 4 floats): conflict-free reads
                 const int row = e % SPB, j0 = 8 * (e / SPB);
@@ -195,8 +245,63 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
         } else {
             gemm16<NT1, G1>(sX, ldx, P.Wq1, ct1, acc1);
         }
+        float hsc[4];   // H2: 2^-(e_row + SH2_EX) of this lane's rows (x rows, then s rows)
+        if constexpr (H2) {
+            // z and s = z / phi of every tile of this wave (s kept in cr1 / ci1), the rows' max |s|
+            // to LDS; the barrier below also ends every wave's reads of the x planes
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + SH2_EX));
+        }
         __syncthreads();   // tau / b / phi published; every wave done reading x
-        if constexpr (X3) {
+        if constexpr (H2) {
+            float mrow[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t2 = 0; t2 < NC1; ++t2) {
+                const int o = 16 * (cc1 + t2) + (lane & 15);
+                const int lo = o / Nr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 4 * (lane >> 4) + r;
+                    const int b = row * ldz + 2 * o;
+                    const float bz = sB[row * Lout + lo], ip = sIph[row * Lout + lo];
+                    const float zr = (yt[2 * t2][r] - cr1[t2][r] * hsc[r]) + bz * sZ[b];
+                    const float zi = (yt[2 * t2 + 1][r] - ci1[t2][r] * hsc[r]) + bz * sZ[b + 1];
+                    sZ[b] = zr; sZ[b + 1] = zi;
+                    cr1[t2][r] = zr * ip; ci1[t2][r] = zi * ip;
+                    mrow[r] = fmaxf(mrow[r], fmaxf(fabsf(cr1[t2][r]), fabsf(ci1[t2][r])));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int sh = 1; sh < 16; sh <<= 1) mrow[r] = fmaxf(mrow[r], __shfl_xor(mrow[r], sh));
+            }
+            if ((lane & 15) == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s_hmax[wave][4 * (lane >> 4) + r] = mrow[r];
+            }
+            __syncthreads();
+            int hes[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float mr = s_hmax[0][4 * (lane >> 4) + r];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) mr = fmaxf(mr, s_hmax[w][4 * (lane >> 4) + r]);
+                hes[r] = h2_row_exp(mr);
+                hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(hes[r] + SH2_EX));
+            }
+#pragma unroll
+            for (int t2 = 0; t2 < NC1; ++t2) {
+                const int o = 16 * (cc1 + t2) + (lane & 15);
+                float sr[4], si[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sr[r] = __builtin_amdgcn_ldexpf(cr1[t2][r], hes[r]);
+                    si[r] = __builtin_amdgcn_ldexpf(ci1[t2][r], hes[r]);
+                }
+                h2_store_acc(sP, ldp2, o, sr, si);
+            }
+        } else if constexpr (X3) {
 #pragma unroll
             for (int t2 = 0; t2 < NC1; ++t2) {
                 const int o = 16 * (cc1 + t2) + (lane & 15);
@@ -233,7 +338,15 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
         f32x4 acc2[NT2];
         if constexpr (X3) {
             f32x4 cr2[NC2], ci2[NC2];
-            gemm_x3<NC2, G2 / 4>(sP, ldp2, P.Wx2, cc2, cr2, ci2);
+            if constexpr (H2) {
+                gemm_h2<NC2, G2 / 4>(sP, ldp2, P.Wx2, cc2, cr2, ci2);
+#pragma unroll
+                for (int t2 = 0; t2 < NC2; ++t2)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { cr2[t2][r] *= hsc[r]; ci2[t2][r] *= hsc[r]; }
+            } else {
+                gemm_x3<NC2, G2 / 4>(sP, ldp2, P.Wx2, cc2, cr2, ci2);
+            }
 #pragma unroll
             for (int t2 = 0; t2 < NC2; ++t2) {
                 const int o = 16 * (cc2 + t2) + (lane & 15);
@@ -395,13 +508,19 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, Const64 c64) {
         s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
         *P.status = s;
     }
+    if (P.dec_on) {
+        // fused MAP decision + counters on xmap (scamp.py:107 -> loss.py:67-179): the s / plane region
+        // holds the truth rows (n >= N: rows of ldx floats fit), the z region the labels
+        __syncthreads();
+        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldx, row0, row0, nrows, sS, sZ, scr);
+    }
 }
 
 int device_cu_count();
 
-template <int NT1, int G1, int NT2, int G2, int KK, bool X3>
-static int spersist_launch_t(const ScampK& P, const Const64& c64, hipStream_t st) {
-    const void* fn = (const void*)scamp_persist<NT1, G1, NT2, G2, KK, X3>;
+template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false>
+static int spersist_launch_t(const ScampK& P, const DecConst& dc, hipStream_t st) {
+    const void* fn = (const void*)scamp_persist<NT1, G1, NT2, G2, KK, X3, H2>;
     const size_t lds = (size_t)slayout(P.N, P.n, P.L, P.Lin, P.Lout, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query: once per instantiation and LDS size
     static size_t attr_lds = 0;
@@ -418,20 +537,20 @@ static int spersist_launch_t(const ScampK& P, const Const64& c64, hipStream_t st
     // persist_grid_launch (amp_host.h): plain launch after the co-residency check, or the
     // cooperative one; every barrier spin is bounded (2 s) as the backstop
     ScampK Pc = P;
-    Const64 cc = c64;
+    DecConst cc = dc;
     void* args[] = {(void*)&Pc, (void*)&cc};
     return persist_grid_launch("scamp_persist", fn, P.nwg, 256, lds, per_cu, args, st);
 }
 
-template <int NT1, int G1, int NT2, int G2, bool X3>
-static int spersist_launch_s(const ScampK& P, const Const64& c64, hipStream_t st) {
+template <int NT1, int G1, int NT2, int G2, bool X3, bool H2 = false>
+static int spersist_launch_s(const ScampK& P, const DecConst& c64, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return spersist_launch_t<NT1, G1, NT2, G2, 1, X3>(P, c64, st);
-    case 2: return spersist_launch_t<NT1, G1, NT2, G2, 2, X3>(P, c64, st);
-    case 4: return spersist_launch_t<NT1, G1, NT2, G2, 4, X3>(P, c64, st);
-    case 8: return spersist_launch_t<NT1, G1, NT2, G2, 8, X3>(P, c64, st);
-    case 16: return spersist_launch_t<NT1, G1, NT2, G2, 16, X3>(P, c64, st);
-    default: return spersist_launch_t<NT1, G1, NT2, G2, 64, X3>(P, c64, st);
+    case 1: return spersist_launch_t<NT1, G1, NT2, G2, 1, X3, H2>(P, c64, st);
+    case 2: return spersist_launch_t<NT1, G1, NT2, G2, 2, X3, H2>(P, c64, st);
+    case 4: return spersist_launch_t<NT1, G1, NT2, G2, 4, X3, H2>(P, c64, st);
+    case 8: return spersist_launch_t<NT1, G1, NT2, G2, 8, X3, H2>(P, c64, st);
+    case 16: return spersist_launch_t<NT1, G1, NT2, G2, 16, X3, H2>(P, c64, st);
+    default: return spersist_launch_t<NT1, G1, NT2, G2, 64, X3, H2>(P, c64, st);
     }
 }
 

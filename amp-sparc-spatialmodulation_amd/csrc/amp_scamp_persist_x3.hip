@@ -5,7 +5,7 @@
 
 namespace amp {
 
-int scamp_persist_launch_x3(const ScampK& P, const Const64& c64, hipStream_t st) {
+int scamp_persist_launch_x3(const ScampK& P, const DecConst& c64, hipStream_t st) {
     const int twoN = 2 * P.N, twon = 2 * P.n;
     if (twoN == 128 && twon == 256) return spersist_launch_s<4, 8, 2, 16, true>(P, c64, st);
     if (twoN == 256 && twon == 512) return spersist_launch_s<8, 16, 4, 32, true>(P, c64, st);

@@ -274,6 +274,7 @@ bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs = 1);
 int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu);
 bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
+bool vamp_persist_ytil_h2(const VampK& P);
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);
 int device_cu_count();
 float* debug_dump_ptr();   // amp_vamp_debug_dump's buffer (null: off)

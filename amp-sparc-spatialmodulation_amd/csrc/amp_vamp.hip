@@ -20,6 +20,7 @@
 #include <mutex>
 #include <vector>
 
+#include "amp_persist.h"
 #include "amp_vamp.h"
 
 namespace amp {
@@ -537,14 +538,15 @@ static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t
 
 // Persistent engine: ONE launch builds the 16x16x4-packed operators (Vh, V), the y~ operator
 // s Uh and zeroes the barrier words; the Tracker's initial state and the iteration-0 scalars
-// are formed inside vamp_persist.  y~ = (s Uh) y comes from gemm_store by default: forming it
-// inside vamp_persist (AMP_YTIL_IN_KERNEL=1, n == 2N) saves ~20 us per forward but sums in
-// another order, which flips the allclose early exit of a cfg2 QPSK 9 dB golden (T 4 vs the
-// reference's 3; the exit there is decided by float32 rounding of y~).
-static bool ytil_in_kernel_requested() {
-    static const bool v = [] {
+// are formed inside vamp_persist.  y~ = (s Uh) y: on the fp16x2 engine inside vamp_persist's
+// prologue (n == 2N; AMP_YTIL_IN_KERNEL=0 keeps the separate gemm_store launch), on the other
+// arithmetics from gemm_store (the f32 engine can form it in-kernel with AMP_YTIL_IN_KERNEL=1: ~20
+// us per forward, but its 16x16x4 summation order flipped the allclose early exit of a cfg2 QPSK
+// 9 dB golden, T 4 vs the reference's 3).
+static int ytil_in_kernel_env() {
+    static const int v = [] {
         const char* e = getenv("AMP_YTIL_IN_KERNEL");
-        return e && e[0] == '1';
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
     return v;
 }
@@ -552,7 +554,11 @@ static bool ytil_in_kernel_requested() {
 static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st) {
     static std::atomic<unsigned> gen{0};
     P.gen = ++gen;
-    P.ytil_in_kernel = (!P.x3 && ytil_in_kernel_requested() && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
+    const int env = ytil_in_kernel_env();
+    if (P.x3 == 2)
+        P.ytil_in_kernel = (env != 0 && vamp_persist_ytil_h2(P)) ? 1 : 0;
+    else
+        P.ytil_in_kernel = (!P.x3 && env == 1 && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
     const bool yk = P.ytil_in_kernel != 0;
     CWeightJob j[3];
     if (P.x3) {
@@ -568,8 +574,10 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     j[1] = CWeightJob{(const float2*)a->Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)P.Wq2, 2 * P.k, 2 * P.N, WPACK16};
     }
     //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
-    j[2] = yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
-              : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
+    j[2] = (yk && P.x3 == 2)
+               ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, P.n, P.k, WPACKH2, YH2_EX}
+           : yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
+                : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
     int rc = build_cweights(j, 3, P.pbar, PBAR_WORDS, st);
     if (rc || yk) return rc;
     rc = vamp_attrs();

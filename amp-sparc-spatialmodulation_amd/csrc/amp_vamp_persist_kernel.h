@@ -6,6 +6,7 @@
 
 #include <stdlib.h>
 
+#include "amp_decide_fused.h"
 #include "amp_persist.h"
 #include "amp_vamp.h"
 
@@ -45,123 +46,6 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
     y.total = o;
     return y;
 }
-
-// Fused MAP decision + error counters (Loss.error_rate, loss.py:67-179, via amp_decide.h) on
-// this workgroup's rows while r (the decision input, vamp.py:187) and xmmse are still in LDS;
-// per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
-// mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
-// row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
-// (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
-template <int PWG, int KK>
-__device__ void decide_epilogue(const VampK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
-                                int lrow0, int nrows, float* sT, void* lab_lds, void* scr) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int M = P.M, L = P.L, N = P.N;
-    const int S = nrows * L;
-    // one coalesced bulk load of this workgroup's truth rows and labels into LDS (a per-section
-    // global load inside the decision loop left every round waiting on HBM latency)
-    long long* lsym = reinterpret_cast<long long*>(lab_lds);
-    long long* lidx = lsym + S;
-    unsigned char* mism = reinterpret_cast<unsigned char*>(lidx + S);
-    {
-        // PBM rows of 2N floats = PBM * N / 2 float4: all loads in flight before the LDS stores
-        constexpr int CH = 8;
-        const int tot = nrows * (N >> 1);
-        for (int e0 = 0; e0 < tot; e0 += PWG * CH) {
-            float4 v[CH];
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    v[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.xtrue) +
-                                                            (size_t)(row0 + row) * 2 * N + c4);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    *reinterpret_cast<float4*>(sT + row * ldr + c4) = v[u];
-                }
-            }
-        }
-    }
-    for (int e = tid; e < S; e += PWG) {
-        lsym[e] = P.sym[(size_t)row0 * L + e];
-        lidx[e] = P.idx[(size_t)row0 * L + e];
-    }
-    __syncthreads();
-    const long long ibmask = dec_ibmask(P.ibits);
-    DecPart q = decpart_zero();
-    // one section per group of DG = 4 lanes (two DPP steps per reduction), float32 prefilter
-    constexpr int DG = 4;
-    const int g = lane % DG;
-    for (int base = wave * (64 / DG); base < S; base += (PWG / 64) * (64 / DG)) {   // wave-uniform
-        const int ls = base + lane / DG;
-        const bool act = ls < S;
-        const int lsc = act ? ls : S - 1;
-        const int row = lsc / L, l = lsc - row * L;
-        const float* rp = sR + row * ldr + 2 * l * M;
-        const float* xp = sX + row * ldr + 2 * l * M;
-        const float* tp = sT + row * ldr + 2 * l * M;
-        auto ld = [&](int m, float2& xv, float2& xt, float2& xe) {
-            xv = *reinterpret_cast<const float2*>(rp + 2 * m);
-            xe = *reinterpret_cast<const float2*>(xp + 2 * m);
-            xt = *reinterpret_cast<const float2*>(tp + 2 * m);
-        };
-        int bi, mm;
-        double se;
-        decide_section<KK, DG, true>(dc, M, g, ld, bi, mm, se);
-        if (act && g == 0) {
-            const long long s = (long long)(lrow0 + row) * L + l;
-            mism[lsc] = (unsigned char)mm;
-            count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
-        }
-    }
-    __syncthreads();
-    // channel uses (Na sections each) and trials with any mismatch (loss.py:133-136, 150)
-    long long ver = 0, verf = 0, verm = 0, verL = 0, fer = 0;
-    for (int row = tid; row < nrows; row += PWG) {
-        int trial = 0;
-        for (int lin = 0; lin < P.Lin; ++lin) {
-            int cu = 0;
-            for (int a = 0; a < P.Na; ++a) cu |= mism[row * L + lin * P.Na + a];
-            ver += cu;
-            if (lin == 0) verf += cu;
-            if (lin == P.Lin / 2) verm += cu;
-            if (lin == P.Lin - 1) verL += cu;
-            trial |= cu;
-        }
-        fer += trial;
-    }
-    q.ier = group_sum(q.ier, 64); q.ser = group_sum(q.ser, 64); q.iber = group_sum(q.iber, 64);
-    q.sber = group_sum(q.sber, 64);
-    q.mse = group_sum(q.mse, 64); q.msef = group_sum(q.msef, 64); q.msem = group_sum(q.msem, 64);
-    q.mseL = group_sum(q.mseL, 64);
-    ver = group_sum(ver, 64); verf = group_sum(verf, 64); verm = group_sum(verm, 64); verL = group_sum(verL, 64);
-    fer = group_sum(fer, 64);
-    DecWG* sw = reinterpret_cast<DecWG*>(scr);
-    if (lane == 0) {
-        DecWG w;
-        w.p = q; w.ver = ver; w.verf = verf; w.verm = verm; w.verL = verL; w.fer = fer;
-        w.pad[0] = w.pad[1] = w.pad[2] = 0;
-        sw[wave] = w;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        DecWG o = sw[0];
-        for (int v = 1; v < PWG / 64; ++v) {
-            decpart_add(o.p, sw[v].p);
-            o.ver += sw[v].ver; o.verf += sw[v].verf; o.verm += sw[v].verm; o.verL += sw[v].verL; o.fer += sw[v].fer;
-        }
-        P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
-                                 // an agent-scope release writes back the L2 and cost ~90 us)
-    }
-}
-
-__global__ __launch_bounds__(1024) void vamp_decide_fold(const DecWG* w, int n, amp_counts* out);
 
 // dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
 // X3: both per-iteration GEMMs on the split-precision bf16x3 engine (gemm_x3): the A operand
@@ -216,7 +100,63 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         const float sv = P.s[col >> 1];
         s2c[t] = sv * sv;                                   // vamp.py:17
     }
-    if (X3) {
+    if (H2 && P.ytil_in_kernel) {
+      if constexpr (H2) {
+        // y~ = (s Uh) y (vamp.py:22) for this workgroup's rows on the fp16x2 GEMM (n == 2N): the y
+        // rows scaled per row and split into four planes over the A / R / X region (free until
+        // the Tracker's state is formed below), the operator s Uh h2-packed with exponent YH2_EX
+        constexpr int IPY = NT / 2;                   // items per thread: PBM n / 8 / PWG, n = 64 NT
+        const int n = P.n, ldy = n + 8;
+        const int row = tid % PBM;
+        float re[IPY][8], im[IPY][8];
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < IPY; ++i) {
+            const int e = tid + i * PWG;
+            const int j0 = 8 * (e / PBM);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 2 * n + 2 * j0 + 4 * h);
+                re[i][2 * h] = v.x; im[i][2 * h] = v.y; re[i][2 * h + 1] = v.z; im[i][2 * h + 1] = v.w;
+            }
+#pragma unroll
+            for (int h = 0; h < 8; ++h) m = fmaxf(m, fmaxf(fabsf(re[i][h]), fabsf(im[i][h])));
+        }
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        if (lane < PBM) s_hmax[wave][lane] = m;
+        __syncthreads();
+        float mr = s_hmax[0][row];
+#pragma unroll
+        for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][row]);
+        const int ex = h2_row_exp(mr);
+        if (tid < PBM) s_hexp[tid] = ex;
+#pragma unroll
+        for (int i = 0; i < IPY; ++i) {
+            const int e = tid + i * PWG;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                re[i][h] = __builtin_amdgcn_ldexpf(re[i][h], ex);
+                im[i][h] = __builtin_amdgcn_ldexpf(im[i][h], ex);
+            }
+            h2_store8(sP, ldy, row, 8 * (e / PBM), re[i], im[i]);
+        }
+        __syncthreads();
+        f32x4 yr[NC], yi[NC];
+        gemm_h2<NC, 2 * G3>(sP, ldy, P.Wq0, cc0, yr, yi);   // K = n = 2N: 2 G3 groups of 32
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float sc = __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + YH2_EX));
+#pragma unroll
+            for (int t = 0; t < NC; ++t) {
+                yt[2 * t][r] = yr[t][r] * sc;
+                yt[2 * t + 1][r] = yi[t][r] * sc;
+            }
+        }
+        __syncthreads();   // the planes region becomes the Tracker's state
+      }
+    } else if (X3) {
 #pragma unroll
         for (int t = 0; t < NC; ++t) {
             const int o = 16 * (cc0 + t) + (lane & 15);

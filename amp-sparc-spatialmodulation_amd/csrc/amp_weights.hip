@@ -143,9 +143,10 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         return;
     }
     if (J.packed == WPACKH2) {
-        // fp16x2 planes of X 2^H2_EX (amp_persist.h gemm_h2): kap = J, ncp = O (complex counts).
-        // |x| >= 4 leaves fp16's range: the piece is then inf, so the GEMM's result is non-finite
-        // (never silently wrong); the SVD factors of vamp.py have |x| <= 1.
+        // fp16x2 planes of X 2^ex (amp_persist.h gemm_h2): kap = J, ncp = O (complex counts).
+        // |x| 2^ex >= 65520 leaves fp16's range: the piece is then inf, so the GEMM's result is
+        // non-finite (never silently wrong); VAMP's SVD factors have |x| <= 1 (ex = 14), SCAMP's
+        // channel entries are ~CN(0, 1/Nr) (ex = 10: |x| < 64).
         unsigned short* w2 = reinterpret_cast<unsigned short*>(J.wt);
         const long tot = (long)J.ncp * J.kap;
         for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
@@ -162,8 +163,8 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
                 }
             }
             unsigned p[4];
-            split2(xr, H2_EX, p[0], p[1]);
-            split2(xi, H2_EX, p[2], p[3]);
+            split2(xr, J.ex, p[0], p[1]);
+            split2(xi, J.ex, p[2], p[3]);
 #pragma unroll
             for (int f = 0; f < 4; ++f) w2[h2_index(o, j, f, J.kap)] = (unsigned short)p[f];
         }

@@ -17,7 +17,7 @@ from torch import nn
 import amp_native as nat
 from config import Config
 from loss import Loss
-from vamp import LazyResult, ShardHook, _c64, block_denoise
+from vamp import _FUSED_DECIDE, LazyResult, ShardHook, _c64, block_denoise
 
 
 class _Buffers:
@@ -170,10 +170,15 @@ class SCAMP(LazyResult, nn.Module):
             res, host = self._result_slot(T.y.device)
             T.res = res
             T.args.status = nat.dptr(res)
-            T._call('amp_scamp_run')
-            # decision on T.xmap (scamp.py:107); counters next to the status record
-            self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
             persistent = nat.lib().amp_scamp_select_engine(C.byref(T.dims), self.engine) == nat.ENGINE_PERSISTENT
+            if persistent and _FUSED_DECIDE and self.L.decision_mode == 'sparc':
+                # forward + decision on T.xmap (scamp.py:107) + counters in one launch sequence
+                dec = self.L.decide_args(x, symbol, index, out=res[64:])
+                T._call('amp_scamp_detect_count', C.byref(dec))
+            else:
+                T._call('amp_scamp_run')
+                # decision on T.xmap (scamp.py:107); counters next to the status record
+                self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
             rescue = (lambda: self._rescue_forward(W, A, y, SNR, x, symbol, index)) if persistent else None
             self._arm(self.L, res, host, 'amp_scamp_run', rescue)          # + L.dump(), scamp.py:99
         self._keep = T

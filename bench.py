@@ -278,16 +278,19 @@ def main():
               'amp_vamp_profile')
     N, k = Nt, min(Nt, Nr)
     flops_mv = 8.0 * Bp * N * k                    # complex [N x k] . [k] per trial = 8 real flop / CMAC
+    gmode = nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) if persistent else nat.GEMM_F32
+    gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2'}.get(gmode, 'f32')
+    # the fp16x2 engine forms y~ = (s Uh) y in its prologue when n == 2N (amp_vamp.hip): those
+    # 8 B n k flops per trial belong to the launch then
+    ytil_in = persistent and gname == 'fp16x2' and Nr == 2 * Nt and os.environ.get('AMP_YTIL_IN_KERNEL') != '0'
     if persistent:
-        kern, flops_launch = 'vamp_persist (whole iteration loop: 2 GEMMs + LMMSE + Onsager + denoiser per iteration)', \
-            2.0 * flops_mv * T
+        kern, flops_launch = 'vamp_persist (whole iteration loop: 2 GEMMs + LMMSE + Onsager + denoiser per iteration' + \
+            (', y~ GEMM in the prologue)' if ytil_in else ')'), 2.0 * flops_mv * T + (8.0 * Bp * Nr * k if ytil_in else 0.0)
         kms = {'prepare': ms[0], 'vamp_persist': ms[1], 'forward': ms[3]}
     else:
         kern, flops_launch = 'vamp_k2 (GEMM2 + Onsager update + section denoiser)', flops_mv
         kms = {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}
     achieved = flops_launch / (ms[1] * 1e-3) / 1e12
-    gmode = nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) if persistent else nat.GEMM_F32
-    gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2'}.get(gmode, 'f32')
     if rank != 0:
         if dist:
             tdist.destroy_process_group()

@@ -265,7 +265,7 @@ typedef struct amp_scamp_args {
     const void* y;      /* c64 [B][n] */
     int32_t max_iter;
     int32_t engine;     /* amp_scamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT (as for VAMP) */
-    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 (as for VAMP) */
+    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 / _H2 (as for VAMP) */
     int32_t pad;
     double noise_var;   /* Na/Nr/SNR (scamp.py:98) */
     void* xmap;         /* out c64 [B][N] (scamp.py:107) */
@@ -286,6 +286,13 @@ size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
  *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
 int amp_scamp_select_engine(const amp_dims* d, int32_t engine);
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+/* SCAMP.forward + Loss.error_rate in one call (scamp.py:77-107 then loss.py:67-179), as
+ * amp_vamp_detect_count: the persistent engine's forward with the MAP decision on xmap
+ * (scamp.py:107) fused into the same launch (each workgroup decides the rows it holds in LDS; one
+ * fold launch after it), counters identical to amp_map_decide_count's.  AMP_E_ARG when the shape
+ * is not persistent-eligible (use amp_scamp_run + amp_map_decide_count). */
+int amp_scamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a,
+                           const amp_vamp_decide_args* dec, void* stream);
 /* amp_scamp_run (launch engine) on one rank's slice of a trial-sharded batch (the protocol of
  * amp_vamp_run_sharded, the hook of amp_set_allreduce_hook): max|xi| / min section max
  * (scamp.py:64), the psi allclose count (scamp.py:105) and the rare path's exact values
