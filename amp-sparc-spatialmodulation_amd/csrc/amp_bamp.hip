@@ -21,6 +21,12 @@ constexpr int BRWG = 1024;
 
 struct alignas(16) BampIter {
     int32_t stopped, T, fixed, fixed_all;
+    // exact float64 fix-up of iteration T-1 pending (set by bamp_r, done by bamp_fix_sec, settled
+    // by bamp_fin): the exact batch max |xi| G, the float32 estimate's slack, the allclose count
+    // before the fix-up
+    double G, slack;
+    uint32_t notclose;
+    int32_t active, pad[2];
 };
 
 struct BampK {
@@ -283,10 +289,31 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     part_block_store(pa, P.parts + (size_t)t * P.nblk + blockIdx.y * gridDim.x + blockIdx.x, lds + C::CTILE_FLOATS);
 }
 
-// reduction, exact float64 fix-up, allclose decision (bamp.py:140)
+// Iteration record t+1 (bamp.py:140): early exit when no var moved beyond allclose.
+__device__ __forceinline__ void bamp_finish(const BampK& P, int t, uint32_t notclose, int fixed) {
+    BampIter nx{};
+    nx.stopped = notclose == 0 ? 1 : 0;
+    nx.T = t + 1;
+    nx.fixed = fixed;
+    nx.fixed_all = (fixed < 0) ? 1 : 0;
+    P.iters[t + 1] = nx;
+    if (nx.stopped || t + 1 == P.max_iter) {
+        amp_status s;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+        *P.status = s;
+    }
+}
+
+// Reduction and allclose decision (bamp.py:140).  The rare exact-float64 path (a section's
+// normaliser out of the float64 range against the batch-global shift, amp_denoise.h) is spread
+// over the grid as SCAMP's is: this workgroup only settles the exact batch max |xi| G over the
+// candidate sections and leaves a pending record; bamp_fix_sec recomputes the out-of-range
+// sections (a grid kernel: at 64-QAM on a failing detector most sections of the batch take this
+// path every iteration, 314 ms per cfg5 detection when one workgroup recomputed them all), and
+// bamp_fin adds the per-block counts and decides the early exit.
 __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
-    __shared__ unsigned s_nc[BRWG / 64];
     __shared__ double s_d[BRWG / 64];
     const BampIter cur = P.iters[t];
     if (cur.stopped) {
@@ -294,58 +321,100 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
         return;
     }
     PartAcc pa = part_reduce_all(P.parts + (size_t)t * P.nblk, P.nblk, lds);
-    int fixed = 0;
     if (part_allnan(pa)) {
         if (!cur.fixed_all) nan_fill(P.xm, bvar(P, t), (size_t)P.B * P.N);
-        pa.notclose = 1;
-        fixed = -1;
+        if (threadIdx.x == 0) bamp_finish(P, t, 1u, -1);
     } else if (part_danger(pa)) {
-        float* vn = bvar(P, t);
-        const float* vp = bvar(P, t + 1);
+        const double slack = logit_slack(pa.maxabs);
         const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
         const float* cov = P.cov;
-        float2* x2 = reinterpret_cast<float2*>(P.xm);
         const int M = P.M;
-        int dnc = 0;
-        auto ldf = [=](int sct) {
+        double gm = 0.0;
+        for (int sct = threadIdx.x; sct < P.B * P.L; sct += blockDim.x) {
+            if ((double)P.secabs[sct] < pa.maxabs - slack) continue;
             const size_t o0 = (size_t)sct * M;
-            return [=](int m, float& rr, float& ri, float& it) {
+            auto ld = [=](int m, float& rr, float& ri, float& it) {
                 const float2 v = xp2[o0 + m];
                 rr = v.x; ri = v.y; it = 1.0f / (cov[o0 + m] * 0.5f);
             };
-        };
-        auto stf = [&](int sct) {
-            const size_t o0 = (size_t)sct * M;
-            return [&, o0](int m, float xr, float xi, float var) {
-                const size_t o = o0 + m;
-                dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(vn[o], vp[o]) ? 0 : 1);
-                x2[o] = make_float2(xr, xi);
-                vn[o] = var;
-            };
-        };
-        double G;
-        fixed = fixup_sections<true>(P.B * P.L, M, P.secmax, P.secabs, pa.maxabs, c64, ldf, stf, &G, s_d);
-        dnc = group_sum(dnc, 64);
-        if ((threadIdx.x & 63) == 0) s_nc[threadIdx.x >> 6] = (unsigned)dnc;
-        __syncthreads();
-        unsigned nc = 0;
-        for (int w = 0; w < BRWG / 64; ++w) nc += s_nc[w];
-        pa.notclose += nc;
-    }
-    if (threadIdx.x == 0) {
-        BampIter nx;
-        nx.stopped = pa.notclose == 0 ? 1 : 0;
-        nx.T = t + 1;
-        nx.fixed = fixed;
-        nx.fixed_all = (fixed < 0) ? 1 : 0;
-        P.iters[t + 1] = nx;
-        if (nx.stopped || t + 1 == P.max_iter) {
-            amp_status s;
-            s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
-            s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
-            *P.status = s;
+            gm = fmax(gm, section_absmax_f64(ld, M, c64));
         }
+        gm = group_max(gm, 64);
+        if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = gm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double G = 0.0;
+            for (int w = 0; w < BRWG / 64; ++w) G = fmax(G, s_d[w]);
+            BampIter nx{};
+            nx.stopped = 0; nx.T = t + 1; nx.fixed = 0; nx.fixed_all = 0;
+            nx.G = G; nx.slack = slack; nx.notclose = pa.notclose; nx.active = 1;
+            P.iters[t + 1] = nx;
+        }
+    } else if (threadIdx.x == 0) {
+        bamp_finish(P, t, pa.notclose, 0);
     }
+}
+
+// per-block counts of bamp_fix_sec, written over iteration t's partials (consumed by bamp_r):
+// slot i = {sections fixed, allclose delta} of block i
+__device__ __forceinline__ int2* bamp_fix_counts(const BampK& P, int t) {
+    return reinterpret_cast<int2*>(P.parts + (size_t)t * P.nblk);
+}
+
+__device__ __forceinline__ int bamp_block_sum_int(int v, int* s_i) {
+    v = group_sum(v, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_i[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_i[w];
+    return tot;
+}
+
+// the out-of-range sections of a pending record, recomputed with the reference's exact float64
+// op sequence (exact_section_f64): xmmse, var and the allclose delta against the previous var
+__global__ __launch_bounds__(AMP_WG) void bamp_fix_sec(BampK P, Const64 c64, int t) {
+    __shared__ int s_i[AMP_WG / 64];
+    const BampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
+    float2* x2 = reinterpret_cast<float2*>(P.xm);
+    const float* cov = P.cov;
+    float* vn = bvar(P, t);
+    const float* vp = bvar(P, t + 1);
+    const int M = P.M;
+    int cnt = 0, dnc = 0;
+    for (int sct = blockIdx.x * blockDim.x + threadIdx.x; sct < P.B * P.L; sct += gridDim.x * blockDim.x) {
+        if (!((double)P.secmax[sct] - pend.G < AMP_DANGER + pend.slack)) continue;
+        const size_t o0 = (size_t)sct * M;
+        auto ld = [=](int m, float& rr, float& ri, float& it) {
+            const float2 v = xp2[o0 + m];
+            rr = v.x; ri = v.y; it = 1.0f / (cov[o0 + m] * 0.5f);
+        };
+        auto st = [&](int m, float xr, float xi, float var) {
+            const size_t o = o0 + m;
+            dnc += (torch_close(var, vp[o]) ? 0 : 1) - (torch_close(vn[o], vp[o]) ? 0 : 1);
+            x2[o] = make_float2(xr, xi);
+            vn[o] = var;
+        };
+        exact_section_f64<true>(ld, st, M, c64, pend.G);
+        ++cnt;
+    }
+    cnt = bamp_block_sum_int(cnt, s_i);
+    dnc = bamp_block_sum_int(dnc, s_i);
+    if (threadIdx.x == 0) bamp_fix_counts(P, t)[blockIdx.x] = make_int2(cnt, dnc);
+}
+
+__global__ __launch_bounds__(AMP_WG) void bamp_fin(BampK P, int t, int nfix) {
+    __shared__ int s_i[AMP_WG / 64];
+    const BampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    const int2* c = bamp_fix_counts(P, t);
+    int fixed = 0, dnc = 0;
+    for (int i = threadIdx.x; i < nfix; i += blockDim.x) { fixed += c[i].x; dnc += c[i].y; }
+    fixed = bamp_block_sum_int(fixed, s_i);
+    dnc = bamp_block_sum_int(dnc, s_i);
+    if (threadIdx.x == 0) bamp_finish(P, t, (uint32_t)((int)pend.notclose + dnc), fixed);
 }
 
 // Tracker (bamp.py:13-25): xmmse = 0, var(prev) = 1, z = y, u = 0 + sigma2 -> 1/u.
@@ -354,7 +423,7 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
 // not-close count (bamp.py:140) and max|xi| / min section max (bamp.py:70) after xr1, the rare
 // path's exact max|xi| after xr2 and its recomputed sections' deltas after xr3.
 __device__ inline void bamp_record(const BampK& P, int t, bool stop, int fixed) {
-    BampIter nx;
+    BampIter nx{};
     nx.stopped = stop ? 1 : 0;
     nx.T = t + 1;
     nx.fixed = fixed;
@@ -507,7 +576,7 @@ __global__ void bamp_init_kernel(BampK P) {
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        BampIter it;
+        BampIter it{};
         it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0;
         P.iters[0] = it;
     }
@@ -647,6 +716,11 @@ static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStrea
     hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
     launch_kb2(P, c64, gr, t, st);
     hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
+    // the rare path's grid fix-up: no-ops unless bamp_r left a pending record (nfix blocks'
+    // counts fit the iteration's nblk partial slots)
+    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
+    hipLaunchKernelGGL(bamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(bamp_fin, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
     AMP_LAUNCH_CHECK("bamp iteration");
     return AMP_OK;
 }

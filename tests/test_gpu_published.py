@@ -54,11 +54,10 @@ def test_scamp_published_isi_point(device):
     assert abs(fer - p) <= 4.5 * s_fer, (fer, p, s_fer)
     assert abs(ver - PUBLISHED['ver']) <= 4.5 * s_ver, (ver, PUBLISHED['ver'], s_ver)
     # the early exit is batch-global (torch.allclose over every trial's psi, scamp.py:105): over
-    # B = 512 trials it runs at least as long as the published B = 1 mean, and at this shape it
-    # usually runs to the 200-iteration cap (so does the reference: T = 200 at B = 256 and
-    # B = 1, seed 0; REF_RUNS below)
+    # B = 512 trials the reference runs to the 200-iteration cap (REF_RUNS below: T = 200 at
+    # B = 256 and at B = 512 for seeds 0 and 1), so most epochs here must too (8 of 8 measured)
     print('published-shape T per epoch:', Ts)
-    assert PUBLISHED['T'] * 0.5 <= float(np.mean(Ts)) <= 200, Ts
+    assert sum(1 for T in Ts if T == 200) >= 6, Ts
 
 
 # The reference's own SCAMP at this shape, one epoch on its own generators (host replica here),
