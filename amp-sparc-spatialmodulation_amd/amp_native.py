@@ -68,7 +68,7 @@ class AmpBampArgs(C.Structure):
     _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('denoiser', C.c_int32),
                 ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p),
                 ('status', C.c_void_p), ('ws', C.c_void_p), ('ws_bytes', C.c_size_t),
-                ('P0', C.c_float), ('Ps', C.c_float)]
+                ('P0', C.c_float), ('Ps', C.c_float), ('gemm', C.c_int32), ('pad', C.c_int32)]
 
 
 class AmpScampArgs(C.Structure):

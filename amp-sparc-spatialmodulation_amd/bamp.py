@@ -44,7 +44,7 @@ class Tracker:
     """Device state of one BAMP forward (bamp.py:12-25): xmap, xmmse, var and the workspace holding
     the H, H^H, |H|^2, |H|^2^T operators and z, u, cov of the running iteration."""
 
-    def __init__(self, H, y, sigma2: float, config: Config, bufs: _Buffers | None = None):
+    def __init__(self, H, y, sigma2: float, config: Config, bufs: _Buffers | None = None, gemm: int = nat.GEMM_AUTO):
         self.config = config
         B = config.B
         n, N = H.shape[-2], H.shape[-1]
@@ -65,6 +65,7 @@ class Tracker:
         # bamp.py:38-41: 'random' mode denoises element-wise (random_denoiser, bamp.py:79-88)
         a.denoiser = 1 if config.mode == 'random' else 0
         a.P0, a.Ps = float(np.float32(config.P0)), float(np.float32(config.Ps))
+        a.gemm = gemm                                                     # amp_bamp_args.gemm
         a.xmap, a.xmmse, a.var = nat.dptr(self.buf.xmap), nat.dptr(self.buf.xmmse), nat.dptr(self.buf.var)
         a.status = nat.dptr(self.buf.res)
         a.ws, a.ws_bytes = nat.dptr(self.buf.ws), self.buf.ws.numel()
@@ -141,9 +142,13 @@ class BAMPLayer(nn.Module):
 
 
 class BAMP(LazyResult, nn.Module):
-    def __init__(self, config: Config) -> None:
+    """``gemm``: the GEMM arithmetic, nat.GEMM_AUTO (fp16x2 where the shape tiles, else f32
+    MFMA), GEMM_F32 or GEMM_H2 (amp_sparc.h amp_bamp_args.gemm)."""
+
+    def __init__(self, config: Config, gemm: int = nat.GEMM_AUTO) -> None:
         super().__init__()
         self.config = config
+        self.gemm = gemm
         self.E = config.Na / config.Nr                                    # bamp.py:102
         self.layers = nn.ModuleList([BAMPLayer(config, i) for i in range(config.N_Layers)])
         self.L = Loss(config)
@@ -166,7 +171,7 @@ class BAMP(LazyResult, nn.Module):
     def detect(self, H: torch.Tensor, y: torch.Tensor, SNR: float) -> Tracker:
         """All iterations on the device, asynchronous (no host sync)."""
         with torch.cuda.device(y.device):
-            T = Tracker(H, y, self.E / SNR, self.config, self._bufs)
+            T = Tracker(H, y, self.E / SNR, self.config, self._bufs, self.gemm)
             T._call('amp_bamp_run')
         self._keep = T
         return T
@@ -174,7 +179,7 @@ class BAMP(LazyResult, nn.Module):
     def forward(self, H: torch.Tensor, y: torch.Tensor, SNR: float, x: torch.Tensor, symbols, indices) -> Loss:
         """bamp.py:116-143; the counters resolve lazily (see LazyResult)."""
         with torch.cuda.device(y.device):
-            T = Tracker(H, y, self.E / SNR, self.config, self._bufs)
+            T = Tracker(H, y, self.E / SNR, self.config, self._bufs, self.gemm)
             res, host = self._result_slot(T.y.device)
             T.res = res
             T.args.status = nat.dptr(res)

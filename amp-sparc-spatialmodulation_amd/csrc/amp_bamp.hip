@@ -13,6 +13,7 @@
 
 #include "amp_denoise.h"
 #include "amp_gemm.h"
+#include "amp_gemm_h2.h"
 #include "amp_host.h"
 
 namespace amp {
@@ -60,19 +61,39 @@ struct BampK {
     Const c;
     int elementwise;                       // random_denoiser (bamp.py:79-88) instead of the block one
     float P0, Ps;
+    // fp16x2 GEMMs (amp_gemm_h2.h): the four operators h2-packed into the weight buffers above
+    // (real |H|^2 two planes, complex H / H^H four), each GEMM's A rows split into `ap` first
+    int h2, rows_pad;
+    unsigned short* ap;    // [4 planes][rows_pad][max(N, n)] fp16
+    int* rexp;             // [rows_pad] row exponents
 };
+
+// BAMP's fp16x2 operator scale exponent: |H|^2 and |H| below 64 (the channel's entries are
+// ~CN(0, 1/Nr)); larger entries overflow their fp16 piece, so the result is non-finite
+constexpr int BH2_EX = 10;
+
+// the fp16x2 GEMMs need whole 64-wide reduction groups and output tiles (no band skipping)
+static inline bool bamp_h2_shape(const amp_dims* d) {
+    return d->N % 64 == 0 && d->n % 64 == 0 && d->Lin == 1 && d->Lout == 1;
+}
 
 // BAMPLayer.random_denoiser (bamp.py:79-88) for one entry, in the reference's dtypes: G(0) in
 // float32 (r - 0 stays complex64), G(a_k) in float64 (complex64 - complex128), norm / exp / var
 // in float64 (the float32 prior scalars promoted), complex128 / float64 as a reciprocal multiply.
 // c64: torch.tensor(config.symbols), complex128 (bamp.py:37).
+// KK: the table size as a compile-time bound (points k >= c64.K skipped): the loop is unrolled so
+// the by-value kernel-argument table is only read at constant offsets (a runtime-indexed loop made
+// the compiler copy the whole table into scratch memory at every kernel entry: ~900 B per lane).
+template <int KK>
 __device__ __forceinline__ void bamp_bayes_elem(const BampK& P, const Const64& c64, float rr, float ri, float cov,
                                                 float& xr, float& xi, float& var) {
     const float a0 = hypotf(rr, ri);
     const float g0 = expf(-(a0 * a0) / cov);
     const double cd = (double)cov;
     double gs = 0.0, sr = 0.0, si = 0.0, s2 = 0.0;
-    for (int k = 0; k < c64.K; ++k) {
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+        if (k >= c64.K) break;
         const double a = hypot((double)rr - c64.re[k], (double)ri - c64.im[k]);
         const double g = exp(-(a * a) / cd);
         const double ak = hypot(c64.re[k], c64.im[k]);
@@ -93,6 +114,8 @@ __device__ __forceinline__ void bamp_bayes_elem(const BampK& P, const Const64& c
 
 struct BampWs {
     float *Wabs2, *WH, *Wabs2T, *WHH, *v, *z, *invu, *s, *cov, *var1;
+    unsigned short* ap;
+    int* rexp;
     int* band[4];
     XState* xs;
     float *secmax, *secabs;
@@ -135,6 +158,13 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.band[2] = cv.take<int>((size_t)2 * (P.ncpB1 / 128));
     w.band[3] = cv.take<int>((size_t)2 * (P.ncpB2 / P.bn));
     w.xs = cv.take<XState>(1);
+    w.ap = nullptr;
+    w.rexp = nullptr;
+    if (bamp_h2_shape(d)) {
+        const size_t rp = (size_t)round_up(d->B, GBM);
+        w.ap = cv.take<unsigned short>(4 * rp * std::max(d->N, d->n));
+        w.rexp = cv.take<int>(rp);
+    }
     w.bytes = cv.off;
     return w;
 }
@@ -149,10 +179,13 @@ __device__ __forceinline__ int bke(const BampK& P, int w, int cb) { return P.ban
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = xcd_tile();
+    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds, bkb(P, 0, tile.cb),
-                   bke(P, 0, tile.cb));
+    if (P.h2)
+        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds);
+    else
+        gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds,
+                       bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -165,11 +198,14 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
 __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = xcd_tile();
+    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds, bkb(P, 1, tile.cb),
-                   bke(P, 1, tile.cb));
+    if (P.h2)
+        gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds);
+    else
+        gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds, bkb(P, 1, tile.cb),
+                       bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
         const int rho = e >> 6, cp = e & 63;           // complex column pair
@@ -194,10 +230,13 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
 __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = xcd_tile();
+    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds, bkb(P, 2, tile.cb),
-                   bke(P, 2, tile.cb));
+    if (P.h2)
+        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds);
+    else
+        gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds, bkb(P, 2, tile.cb),
+                       bke(P, 2, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -244,11 +283,14 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     using C = GemmCfg<BN>;
-    const GemmTile tile = xcd_tile();
+    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds, bkb(P, 3, tile.cb),
-                  bke(P, 3, tile.cb));
+    if (P.h2)
+        gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds);
+    else
+        gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds, bkb(P, 3, tile.cb),
+                      bke(P, 3, tile.cb));
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
         const int rho = e / BN, cc = e % BN;
@@ -276,7 +318,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
                 const size_t o = (size_t)(row0 + rho) * P.N + col0 / 2 + cc;
                 const float2 v = *reinterpret_cast<const float2*>(lds + rho * C::LDC + 2 * cc);
                 float xr, xi, var;
-                bamp_bayes_elem(P, c64, v.x, v.y, P.cov[o], xr, xi, var);
+                bamp_bayes_elem<KK>(P, c64, v.x, v.y, P.cov[o], xr, xi, var);
                 *reinterpret_cast<float2*>(P.xm + 2 * o) = make_float2(xr, xi);
                 vn[o] = var;
                 pa.sumvar += (double)var;
@@ -590,19 +632,32 @@ __global__ void bamp_output_kernel(BampK P) {
         P.var0[e] = P.var1[e];
 }
 
+// dynamic LDS of every BAMP GEMM launch: the f32 tile's A block or the fp16x2 tile's four staged
+// planes, whichever is larger (either arithmetic runs from the same instantiation)
+constexpr size_t BLDS = h2_tile_lds<256, true>() > GemmCfg<256>::LDS_BYTES ? h2_tile_lds<256, true>()
+                                                                             : GemmCfg<256>::LDS_BYTES;
+static_assert(BLDS <= 80 * 1024, "two BAMP GEMM workgroups per CU");
+static int bamp_lds_attr(const void* fn) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BLDS);
+    if (e != hipSuccess) {
+        set_error("hipFuncSetAttribute: %s", hipGetErrorString(e));
+        return AMP_E_LAUNCH;
+    }
+    return AMP_OK;
+}
 template <int KK>
 static int bamp_kb2_attrs() {
-    int rc = set_lds_attr<128>((const void*)bamp_kb2<128, KK>);
-    return rc ? rc : set_lds_attr<256>((const void*)bamp_kb2<256, KK>);
+    int rc = bamp_lds_attr((const void*)bamp_kb2<128, KK>);
+    return rc ? rc : bamp_lds_attr((const void*)bamp_kb2<256, KK>);
 }
 
 template <int KK>
 static void launch_kb2_kk(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
     if (P.bn == 128)
-        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P,
+        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BLDS, st, P,
                            c64, t);
     else
-        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), GemmCfg<256>::LDS_BYTES, st, P,
+        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), BLDS, st, P,
                            c64, t);
 }
 
@@ -622,9 +677,9 @@ static int g_bamp_rc = 0;
 
 static int bamp_attrs() {
     std::call_once(g_bamp_once, [] {
-        g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka1);
-        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_ka2);
-        if (!g_bamp_rc) g_bamp_rc = set_lds_attr<128>((const void*)bamp_kb1);
+        g_bamp_rc = bamp_lds_attr((const void*)bamp_ka1);
+        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_ka2);
+        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_kb1);
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<1>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<2>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<4>();
@@ -681,6 +736,20 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.elementwise = a->denoiser;
     P.P0 = a->P0;
     P.Ps = a->Ps;
+    // GEMM arithmetic: fp16x2 (AUTO where the shape tiles, AMP_BAMP_GEMM=f32 keeps f32) or f32 MFMA
+    AMP_REQUIRE(a->gemm == AMP_GEMM_AUTO || a->gemm == AMP_GEMM_F32 || a->gemm == AMP_GEMM_H2,
+                "amp_bamp_run: gemm %d (AUTO, F32 or H2)", a->gemm);
+    const bool h2ok = bamp_h2_shape(d);
+    AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || h2ok, "amp_bamp_run: the fp16x2 GEMMs need N %% 64 == 0, n %% 64 == 0 and "
+                "Lin = Lout = 1 (N = %d, n = %d)", d->N, d->n);
+    static const bool f32_env = [] {
+        const char* e = getenv("AMP_BAMP_GEMM");
+        return e && e[0] == 'f';
+    }();
+    P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && !f32_env)) ? 1 : 0;
+    P.rows_pad = round_up(d->B, GBM);
+    P.ap = w.ap;
+    P.rexp = w.rexp;
     c64 = to_const64(c);
     return AMP_OK;
 }
@@ -689,11 +758,22 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
 static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t st) {
     int rc;
     const float2* H = (const float2*)a->H;
+    if (P.h2) {
+        // the four operators as fp16x2 planes (exponent BH2_EX) in ONE launch: |H|^2 (O = n, J = N),
+        // H (O = n, J = N), |H|^2^T (O = N, J = n), H^H (O = N, J = n)
+        CWeightJob j[4];
+        j[0] = CWeightJob{H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wabs2, P.N, P.n, WPACKH2_ABS2, BH2_EX};
+        j[1] = CWeightJob{H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WH, P.N, P.n, WPACKH2, BH2_EX};
+        j[2] = CWeightJob{H, 1, P.N, 0, nullptr, P.N, P.n, (float*)P.Wabs2T, P.n, P.N, WPACKH2_ABS2, BH2_EX};
+        j[3] = CWeightJob{H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.n, P.N, WPACKH2, BH2_EX};
+        if ((rc = build_cweights(j, 4, nullptr, 0, st))) return rc;
+    } else {
     // weights, once per forward (Tracker: adj, abs2, abs2T, bamp.py:17-19)
     if ((rc = build_abs2_weight(H, P.N, 1, P.n, P.N, (float*)P.Wabs2, P.kapA1, P.ncpA1, st))) return rc;
     if ((rc = build_cweight(H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WH, P.kapA2, P.ncpA2, st))) return rc;
     if ((rc = build_abs2_weight(H, 1, P.N, P.N, P.n, (float*)P.Wabs2T, P.kapB1, P.ncpB1, st))) return rc;
     if ((rc = build_cweight(H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.kapB2, P.ncpB2, st))) return rc;
+    }
     if (P.band[0]) {
         const float* wts[4] = {P.Wabs2, P.WH, P.Wabs2T, P.WHH};
         const int kaps[4] = {P.kapA1, P.kapA2, P.kapB1, P.kapB2}, ncps[4] = {P.ncpA1, P.ncpA2, P.ncpB1, P.ncpB2};
@@ -708,13 +788,34 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
     return AMP_OK;
 }
 
+// the four GEMM launches of one BAMPLayer.forward (bamp.py:59-64), each preceded on the fp16x2
+// path by the split of its A rows (var, xmmse, 1/u, s) into the plane buffer
+static void bamp_split(const BampK& P, const float* a, int lda, int K, bool cpx, int t, hipStream_t st) {
+    const int* stop = &P.iters[t].stopped;
+    if (cpx)
+        hipLaunchKernelGGL(h2_split_rows_kernel<true>, dim3(P.rows_pad / 4), dim3(256), 0, st, a, lda, P.B, P.rows_pad,
+                           K, P.ap, P.rexp, stop);
+    else
+        hipLaunchKernelGGL(h2_split_rows_kernel<false>, dim3(P.rows_pad / 4), dim3(256), 0, st, a, lda, P.B,
+                           P.rows_pad, K, P.ap, P.rexp, stop);
+}
+
+static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st) {
+    const int gr = cdiv(P.B, GBM);
+    // the host reads bvar(P, t + 1) as the device does: (t + 1) & 1 picks var1, else var0
+    if (P.h2) bamp_split(P, ((t + 1) & 1) ? P.var1 : P.var0, P.N, P.N, false, t, st);
+    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    if (P.h2) bamp_split(P, P.xm, 2 * P.N, P.N, true, t, st);
+    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    if (P.h2) bamp_split(P, P.invu, P.n, P.n, false, t, st);
+    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    if (P.h2) bamp_split(P, P.s, 2 * P.n, P.n, true, t, st);
+    launch_kb2(P, c64, gr, t, st);
+}
+
 // One BAMPLayer.forward (bamp.py:48-64) + the allclose test of bamp.py:140 (no-op once stopped).
 static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStream_t st) {
-    const int gr = cdiv(P.B, GBM);
-    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    launch_kb2(P, c64, gr, t, st);
+    bamp_gemms(P, c64, t, st);
     hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
     // the rare path's grid fix-up: no-ops unless bamp_r left a pending record (nfix blocks'
     // counts fit the iteration's nblk partial slots)
@@ -726,11 +827,7 @@ static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStrea
 }
 
 static int bamp_iterate_sharded(const BampK& P, const Const64& c64, int t, hipStream_t st, bool& hook_failed) {
-    const int gr = cdiv(P.B, GBM);
-    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
-    launch_kb2(P, c64, gr, t, st);
+    bamp_gemms(P, c64, t, st);
     hipLaunchKernelGGL(bamp_xr1, dim3(1), dim3(BRWG), 0, st, P, t);
     AMP_LAUNCH_CHECK("bamp_xr1");
     // every hook call is made on every rank even after one failed: the ranks' collectives stay
@@ -820,7 +917,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_random_denoise_kernel(BampK P, Co
     for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < count;
          e += (long long)gridDim.x * blockDim.x) {
         float xr, xi, v;
-        bamp_bayes_elem(P, c64, r[e].x, r[e].y, cov[e], xr, xi, v);
+        bamp_bayes_elem<AMP_MAX_K>(P, c64, r[e].x, r[e].y, cov[e], xr, xi, v);
         xm[e] = make_float2(xr, xi);
         var[e] = v;
     }

@@ -690,6 +690,15 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
     constexpr int gpw = 64 / G;
     const int gid = lane / G, g = lane % G;
     const int nw = blockDim.x >> 6;
+    // the table in LDS: the rolled loops below index it at runtime, which on the by-value kernel
+    // argument made the compiler copy the whole Const into scratch memory at every kernel entry
+    __shared__ float s_cre[KK], s_cim[KK];
+    __syncthreads();
+    if (threadIdx.x == 0) {   // constant offsets into the kernel argument (scalar loads)
+#pragma unroll
+        for (int k = 0; k < KK; ++k) { s_cre[k] = kval(c.re[k]); s_cim[k] = kval(c.im[k]); }
+    }
+    __syncthreads();
     DenStat S;
     for (int base = wave * gpw; base < nsec; base += nw * gpw) {   // wave-uniform trip count
         const int sec = base + gid;
@@ -703,7 +712,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
         for (int k0 = 0; k0 < KK; k0 += 8) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float x = fmaf(ur, c.re[k0 + j], ui * c.im[k0 + j]);
+                const float x = fmaf(ur, s_cre[k0 + j], ui * s_cim[k0 + j]);
                 lmax = fmaxf(lmax, x);
                 lmin = fminf(lmin, x);
             }
@@ -714,7 +723,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
         for (int k0 = 0; k0 < KK; k0 += 8) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float cr = c.re[k0 + j], ci = c.im[k0 + j];
+                const float cr = s_cre[k0 + j], ci = s_cim[k0 + j];
                 const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
                 zm += e;
                 a = fmaf(cr, e, a);
@@ -732,7 +741,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
             for (int k0 = 0; k0 < KK; k0 += 8) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float cr = c.re[k0 + j], ci = c.im[k0 + j];
+                    const float cr = s_cre[k0 + j], ci = s_cim[k0 + j];
                     const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
                     const float dr = xr - cr, di = xi - ci;
                     vs = fmaf(fmaf(dr, dr, di * di), e, vs);

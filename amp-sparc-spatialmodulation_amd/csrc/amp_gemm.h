@@ -102,6 +102,20 @@ __device__ __forceinline__ GemmTile xcd_tile() {
     return GemmTile{pos % nr, pos / nr};
 }
 
+// Row-block-major variant (the fp16x2 tiles, amp_gemm_h2.h): XCD x walks a contiguous run of
+// tiles row block by row block, every column block of one row block in turn, so each XCD reads
+// its rows' A planes once (they stay in its L2 while the column blocks pass) and serves the whole
+// operator from its L2 (4 MB at cfg5's H as fp16x2 planes).  Also a bijection.
+__device__ __forceinline__ GemmTile xcd_tile_rows() {
+    constexpr int NXCD = 8;
+    const int nr = gridDim.x, nc = gridDim.y, total = nr * nc;
+    const int id = blockIdx.y * nr + blockIdx.x;
+    const int x = id % NXCD, q = id / NXCD;
+    const int base = total / NXCD, rem = total % NXCD;
+    const int pos = x * base + min(x, rem) + q;
+    return GemmTile{pos / nc, pos % nc};
+}
+
 // Plain A operand: rows of `lda` floats, `ka` valid columns (zero beyond, and for rows >= rows).
 struct ALoadPlain {
     const float* __restrict__ a;

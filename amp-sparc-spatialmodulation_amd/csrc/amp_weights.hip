@@ -5,6 +5,7 @@
 
 #include "amp_gemm.h"
 #include "amp_host.h"
+#include "amp_gemm_h2.h"
 #include "amp_persist.h"
 
 namespace amp {
@@ -170,6 +171,26 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         }
         return;
     }
+    if (J.packed == WPACKH2_ABS2) {
+        // fp16x2 planes of the real |X|^2 (torch's complex abs, the correctly rounded hypot, then
+        // an f32 square: bamp.py:18 `H.abs()**2`), scaled by 2^ex (gemm_tile_h2, amp_gemm_h2.h)
+        unsigned short* w2 = reinterpret_cast<unsigned short*>(J.wt);
+        const long tot = (long)J.ncp * J.kap;
+        for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+            const int o = (int)(e / J.kap), j = (int)(e % J.kap);
+            float v = 0.f;
+            if (o < J.O && j < J.J) {
+                const float2 z = J.src[o * J.so + j * J.sj];
+                const float a = (float)sqrt((double)z.x * z.x + (double)z.y * z.y);
+                v = a * a;
+            }
+            unsigned p0, p1;
+            split2(v, J.ex, p0, p1);
+            w2[h2r_index(o, j, 0, J.kap)] = (unsigned short)p0;
+            w2[h2r_index(o, j, 1, J.kap)] = (unsigned short)p1;
+        }
+        return;
+    }
     const long total = (long)(J.ncp / 2) * (J.kap / 2);
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / (J.kap / 2)), j = (int)(e % (J.kap / 2));
@@ -197,7 +218,7 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     long most = 0;
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
-        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2;
+        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2;
         AMP_REQUIRE((planar ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
                          (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||

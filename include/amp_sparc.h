@@ -234,6 +234,11 @@ typedef struct amp_bamp_args {
     void* ws;
     size_t ws_bytes;
     float P0, Ps;       /* Config.P0 / Config.Ps as float32 (bamp.py:36), denoiser 1 only */
+    int32_t gemm;       /* GEMM arithmetic: AMP_GEMM_AUTO (fp16x2 where N % 64 == 0, n % 64 == 0 and
+                           Lin = Lout = 1, else f32; environment AMP_BAMP_GEMM=f32 keeps f32),
+                           AMP_GEMM_F32 or AMP_GEMM_H2 (amp_gemm_h2.h: every GEMM's A rows split once
+                           into per-row scaled fp16 pieces; |H| must stay below 64) */
+    int32_t pad;
 } amp_bamp_args;
 
 size_t amp_bamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
