@@ -74,6 +74,22 @@ __device__ __forceinline__ void gemm16(const float* sA, int lda, const float* __
     }
 }
 
+// ---- A-plane layout of the split-precision engines (bf16x3: six planes, fp16x2: four) ----
+// Plane f, row r (16 rows per plane), element j at (16 f + r) ldx + (j ^ 8 (r & m)): no row pad
+// (ldx = K, pl_ldx), the 16-byte chunks of row r XOR-permuted by r & m, m + 1 = the lowest set bit
+// of K / 8 capped at 16 (the permutation stays inside aligned blocks of m + 1 chunks).  The
+// 16x16x32 fragment reads (lanes l and l + 16: rows l & 15, chunks c and c + 1), the 8-row
+// 16-byte stores and the accumulator word stores then all hit distinct banks for K = 64 ... 512
+// (the 16-byte row pad of rounds 1-2 left every fragment read 2-way in half its lane groups:
+// tools/ubench/lds_phase_ubench.hip).
+__host__ __device__ inline int pl_ldx(int K) { return K; }
+__device__ __forceinline__ int pl_mask(int ldx) {
+    const int n = ldx >> 3;
+    const int b = n & -n;
+    return (b < 16 ? b : 16) - 1;
+}
+__device__ __forceinline__ int pl_col(int row, int j, int m) { return j ^ ((row & m) << 3); }
+
 // ---- split-precision complex GEMM (bf16x3) ----
 // x = x0 + x1 + x2 with bf16 pieces (round-to-nearest-even; each residual is exact in f32), so
 // a product a.b keeps the six terms a0b0 a0b1 a1b0 a0b2 a1b1 a2b0 (dropped terms <= 2^-24 |ab|)
@@ -112,8 +128,9 @@ __device__ __forceinline__ void x3_store8(unsigned short* sP, int ldx, int row, 
         split3x2(im[2 * h], im[2 * h + 1], b0, b1, b2);
         q[0][h] = a0; q[1][h] = a1; q[2][h] = a2; q[3][h] = b0; q[4][h] = b1; q[5][h] = b2;
     }
+    const int c = pl_col(row, j0, pl_mask(ldx));
 #pragma unroll
-    for (int f = 0; f < 6; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + j0) = q[f];
+    for (int f = 0; f < 6; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + c) = q[f];
 }
 
 __device__ __forceinline__ float dpp_swap_pair(float v) {   // lane l <-> l ^ 1 (quad_perm [1,0,3,2])
@@ -134,16 +151,17 @@ __device__ __forceinline__ void x3_store_acc(unsigned short* sP, int ldx, int o,
         gi[h] = dpp_swap_pair(odd ? vi[h] : vi[2 + h]);
     }
     const int row0 = 4 * (lane >> 4) + (odd ? 2 : 0);
-    unsigned short* p = sP + row0 * ldx + (o & ~1);
+    const int m = pl_mask(ldx);
     const int pl = 16 * ldx;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+        unsigned short* p = sP + (row0 + h) * ldx + pl_col(row0 + h, o & ~1, m);
         const float mr = odd ? vr[2 + h] : vr[h], mi = odd ? vi[2 + h] : vi[h];
         unsigned q[6];
         split3x2(odd ? gr[h] : mr, odd ? mr : gr[h], q[0], q[1], q[2]);
         split3x2(odd ? gi[h] : mi, odd ? mi : gi[h], q[3], q[4], q[5]);
 #pragma unroll
-        for (int f = 0; f < 6; ++f) *reinterpret_cast<unsigned*>(p + f * pl + h * ldx) = q[f];
+        for (int f = 0; f < 6; ++f) *reinterpret_cast<unsigned*>(p + f * pl) = q[f];
     }
 }
 
@@ -183,11 +201,15 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
 #pragma unroll
             for (int f = 0; f < 6; ++f)
                 ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 6 + f) * 1024, 0);
-    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * (lane >> 4);
+    // A fragment of group g: row lane & 15, chunk 4 g + (lane >> 4), permuted (pl_col): element
+    // 8 ((4 g + q) ^ sw) = ((32 g) ^ s32) + 8 (q ^ (sw & 3)), s32 = 32 (sw >> 2) (one v_xad per g)
+    const int sw = (lane & 15) & pl_mask(ldx);
+    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * ((lane >> 4) ^ (sw & 3));
+    const int s32 = 32 * (sw >> 2);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
     u32x4 an[6];
 #pragma unroll
-    for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+    for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + s32 + f * 16 * ldx);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int d = g % RR;
@@ -196,7 +218,8 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
         for (int f = 0; f < 6; ++f) a[f] = an[f];
         if (g + 1 < G) {
 #pragma unroll
-            for (int f = 0; f < 6; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * (g + 1));
+            for (int f = 0; f < 6; ++f)
+                an[f] = *reinterpret_cast<const u32x4*>(ap + ((32 * (g + 1)) ^ s32) + f * 16 * ldx);
         }
 #pragma unroll
         for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
@@ -284,8 +307,9 @@ __device__ __forceinline__ void h2_store8(unsigned short* sP, int ldx, int row, 
         split2x2(im[2 * h], im[2 * h + 1], b0, b1);
         q[0][h] = a0; q[1][h] = a1; q[2][h] = b0; q[3][h] = b1;
     }
+    const int c = pl_col(row, j0, pl_mask(ldx));
 #pragma unroll
-    for (int f = 0; f < 4; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + j0) = q[f];
+    for (int f = 0; f < 4; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + c) = q[f];
 }
 
 // x3_store_acc for the h2 planes (values already scaled).
@@ -300,16 +324,17 @@ __device__ __forceinline__ void h2_store_acc(unsigned short* sP, int ldx, int o,
         gi[h] = dpp_swap_pair(odd ? vi[h] : vi[2 + h]);
     }
     const int row0 = 4 * (lane >> 4) + (odd ? 2 : 0);
-    unsigned short* p = sP + row0 * ldx + (o & ~1);
+    const int m = pl_mask(ldx);
     const int pl = 16 * ldx;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+        unsigned short* p = sP + (row0 + h) * ldx + pl_col(row0 + h, o & ~1, m);
         const float mr = odd ? vr[2 + h] : vr[h], mi = odd ? vi[2 + h] : vi[h];
         unsigned q[4];
         split2x2(odd ? gr[h] : mr, odd ? mr : gr[h], q[0], q[1]);
         split2x2(odd ? gi[h] : mi, odd ? mi : gi[h], q[2], q[3]);
 #pragma unroll
-        for (int f = 0; f < 4; ++f) *reinterpret_cast<unsigned*>(p + f * pl + h * ldx) = q[f];
+        for (int f = 0; f < 4; ++f) *reinterpret_cast<unsigned*>(p + f * pl) = q[f];
     }
 }
 
@@ -337,11 +362,15 @@ __device__ __forceinline__ void gemm_h2(const unsigned short* sP, int ldx, const
 #pragma unroll
             for (int f = 0; f < 4; ++f)
                 ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 4 + f) * 1024, 0);
-    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * (lane >> 4);
+    // A fragment of group g: row lane & 15, chunk 4 g + (lane >> 4), permuted (pl_col): element
+    // 8 ((4 g + q) ^ sw) = ((32 g) ^ s32) + 8 (q ^ (sw & 3)), s32 = 32 (sw >> 2) (one v_xad per g)
+    const int sw = (lane & 15) & pl_mask(ldx);
+    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * ((lane >> 4) ^ (sw & 3));
+    const int s32 = 32 * (sw >> 2);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
     u32x4 an[4];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+    for (int f = 0; f < 4; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + s32 + f * 16 * ldx);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int d = g % RR;
@@ -350,7 +379,8 @@ __device__ __forceinline__ void gemm_h2(const unsigned short* sP, int ldx, const
         for (int f = 0; f < 4; ++f) a[f] = an[f];
         if (g + 1 < G) {
 #pragma unroll
-            for (int f = 0; f < 4; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx + 32 * (g + 1));
+            for (int f = 0; f < 4; ++f)
+                an[f] = *reinterpret_cast<const u32x4*>(ap + ((32 * (g + 1)) ^ s32) + f * 16 * ldx);
         }
 #pragma unroll
         for (int f = 0; f < 2; ++f) na[f] = a[2 + f] ^ sgn;

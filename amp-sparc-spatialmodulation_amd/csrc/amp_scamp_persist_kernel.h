@@ -21,8 +21,8 @@ struct SLayout {
 };
 
 // X3: the GEMM A operands (x for GEMM1, s = z / phi for GEMM2) as six bf16 planes of 16 rows x
-// (K + 8) in the region of the f32 s rows (one operand at a time)
-__host__ __device__ inline int sx3_plane_floats(int K) { return 6 * 16 * (K + 8) / 2; }
+// K (amp_persist.h's XOR-permuted layout) in the region of the f32 s rows (one operand at a time)
+__host__ __device__ inline int sx3_plane_floats(int K) { return 6 * 16 * pl_ldx(K) / 2; }
 
 __host__ __device__ inline SLayout slayout(int N, int n, int L, int Lin, int Lout, bool x3 = false) {
     SLayout y;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
     const int ct1 = wave * NT1, ct2 = wave * NT2;
     const int cc1 = wave * NC1, cc2 = wave * NC2;
     unsigned short* sP = reinterpret_cast<unsigned short*>(sS);
-    const int ldp1 = N + 8, ldp2 = n + 8;      // X3 plane row strides (bf16) of the GEMM1 / GEMM2 operands
+    const int ldp1 = pl_ldx(N), ldp2 = pl_ldx(n);      // X3 plane row strides (bf16) of the GEMM1 / GEMM2 operands
     float yt[NT1][4];
 #pragma unroll
     for (int t2 = 0; t2 < NT1; ++t2) {

@@ -60,10 +60,10 @@ bool vamp_persist_ytil_in_kernel(const VampK& P) {
     return P.n == 2 * P.N && PBM * (2 * P.n + 4) <= playout(P.N, P.k, P.L).offV0;
 }
 
-// the fp16x2 y~ prologue: n == 2N and the four y planes (16 rows x (n + 8) fp16) within the A / R / X
+// the fp16x2 y~ prologue: n == 2N and the four y planes (16 rows x n fp16) within the A / R / X
 // region of the split-precision carve
 bool vamp_persist_ytil_h2(const VampK& P) {
-    return P.n == 2 * P.N && P.k == P.N && 2 * PBM * (P.n + 8) <= playout(P.N, P.k, P.L, true).offV0;
+    return P.n == 2 * P.N && P.k == P.N && 2 * PBM * pl_ldx(P.n) <= playout(P.N, P.k, P.L, true).offV0;
 }
 
 bool vamp_persist_x3_fits(int N, int k, int L) {

@@ -17,22 +17,24 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
 #endif
 
-// LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the 16-row ds_read_b128 and the
-// accumulator stores conflict-free (row r and r+4 land 16 banks apart).
+// LDS carve (floats).  Row strides 2N+4 / max(2N,2k)+4 keep the f32 engine's 16-row ds_read_b128
+// and accumulator stores conflict-free (row r and r+4 land 16 banks apart); the split-precision
+// engines read r / x~ as complex pairs (ds_read_b64 of rows 4 apart) and take 2N+8 (rows r and r+4
+// 32 banks apart: the two 16-lane halves of a 32-lane group on disjoint banks).
 struct PLayout {
     int lda, ldr;
     int offA, offR, offX, offV0, offV1, offSM, offSA, offScr, total;
 };
 
-// bf16x3 A planes (X3 engine): six planes of 16 rows x (N + 8) bf16 (16-byte pad: the 16 rows of
-// one fragment read land on distinct banks)
-__host__ __device__ inline int x3_ldx(int N) { return N + 8; }
+// split-precision A planes (X3 engine): six (bf16x3) or four (fp16x2) planes of 16 rows x N 16-bit
+// pieces in the XOR-permuted layout of amp_persist.h (pl_col)
+__host__ __device__ inline int x3_ldx(int N) { return pl_ldx(N); }
 __host__ __device__ inline int x3_plane_floats(int N) { return 6 * 16 * x3_ldx(N) / 2; }
 
 __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false) {
     PLayout y;
     y.lda = (2 * N > 2 * k ? 2 * N : 2 * k) + 4;
-    y.ldr = 2 * N + 4;
+    y.ldr = 2 * N + (x3 ? 8 : 4);
     int o = 0;
     y.offA = o; o += (x3 && x3_plane_floats(N) > PBM * y.lda) ? x3_plane_floats(N) : PBM * y.lda;
     y.offR = o; o += PBM * y.ldr;
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         // rows scaled per row and split into four planes over the A / R / X region (free until
         // the Tracker's state is formed below), the operator s Uh h2-packed with exponent YH2_EX
         constexpr int IPY = NT / 2;                   // items per thread: PBM n / 8 / PWG, n = 64 NT
-        const int n = P.n, ldy = n + 8;
+        const int n = P.n, ldy = pl_ldx(n);
         const int row = tid % PBM;
         float re[IPY][8], im[IPY][8];
         float m = 0.f;

@@ -4,6 +4,10 @@
 launch engines: time per forward and the block-banded GEMMs' effect.  Run once as is and once
 with AMP_BAND_GEMM=0 (the dense GEMMs) to compare; inputs from the reference's generators
 (host replica, seed 0), resident in HBM.  Prints one JSON line per detector.
+Roofline: the operator has Lin Lh nonzero Nr x Nt blocks (channel.py:89-91); per trial-iteration
+SCAMP does two complex mat-vecs on them (A x, A^H s: 8 flop per complex MAC) and BAMP two complex
+plus two real (|A|^2 var, |A|^2^T (1/u): 2 flop per MAC), priced against the fp32 MFMA peak
+(157.3 TFLOP/s, MI355X_MICROARCH.md).
   python tools/isi_bench.py [B] [iterations]"""
 import json
 import os
@@ -56,10 +60,15 @@ def main():
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / reps * 1e3
         T = int(L.loss['T'])
+        nz = 32 * 3 * 32 * 128                      # Lin Lh Nr Nt nonzero complex entries
+        flop = nz * (2 * 8 if algo == 'scamp' else 2 * 8 + 2 * 2)
+        tf = flop * B / (ms / T * 1e-3) / 1e12
         print(json.dumps({'algo': algo, 'shape': 'Nt=128 Na=8 Nr=32 Lin=32 Lh=3 QPSK (N=4096, n=1088)', 'B': B,
                           'EbN0': 6.0, 'band_gemm': band, 'T': T, 'fer': float(L.loss['fer']),
                           'ver': float(L.loss['ver']), 'ser': float(L.loss['ser']), 'ms_per_forward': round(ms, 3),
-                          'ms_per_iteration': round(ms / T, 4)}), flush=True)
+                          'ms_per_iteration': round(ms / T, 4),
+                          'nz_mflop_per_trial_iteration': round(flop / 1e6, 3), 'tflops_nonzero': round(tf, 2),
+                          'frac_fp32_peak': round(tf / 157.3, 4)}), flush=True)
     nat.unload()
 
 
