@@ -14,7 +14,7 @@ import torch   # noqa: F401  (loads torch's HIP runtime first: one runtime per p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
-LIB_PATH = os.path.join(HERE, 'lib', 'libampsparc.so')
+LIB_PATH = os.environ.get('AMP_LIB_PATH') or os.path.join(HERE, 'lib', 'libampsparc.so')   # AMP_LIB_PATH: A/B builds
 
 AMP_MAX_K = 64      # include/amp_sparc.h (K in {1, 2, 4, 8, 16, 64})
 

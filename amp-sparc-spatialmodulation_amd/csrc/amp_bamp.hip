@@ -14,6 +14,8 @@
 #include "amp_denoise.h"
 #include "amp_gemm.h"
 #include "amp_gemm_h2.h"
+#include <vector>
+#include <cstdio>
 #include "amp_host.h"
 
 namespace amp {
@@ -72,9 +74,10 @@ struct BampK {
 // ~CN(0, 1/Nr)); larger entries overflow their fp16 piece, so the result is non-finite
 constexpr int BH2_EX = 10;
 
-// the fp16x2 GEMMs need whole 64-wide reduction groups and output tiles (no band skipping)
+// the fp16x2 GEMMs need whole 64-wide reduction groups and output tiles (a block-banded H reduces
+// over each tile's h2_kband range)
 static inline bool bamp_h2_shape(const amp_dims* d) {
-    return d->N % 64 == 0 && d->n % 64 == 0 && d->Lin == 1 && d->Lout == 1;
+    return d->N % 64 == 0 && d->n % 64 == 0;
 }
 
 // BAMPLayer.random_denoiser (bamp.py:79-88) for one entry, in the reference's dtypes: G(0) in
@@ -182,7 +185,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     if (P.h2)
-        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds);
+        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds, bkb(P, 0, tile.cb),
+                                       bke(P, 0, tile.cb));
     else
         gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds,
                        bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
@@ -202,7 +206,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     if (P.h2)
-        gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds);
+        gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds, bkb(P, 1, tile.cb),
+                                       bke(P, 1, tile.cb));
     else
         gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds, bkb(P, 1, tile.cb),
                        bke(P, 1, tile.cb));
@@ -233,7 +238,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     if (P.h2)
-        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds);
+        gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds, bkb(P, 2, tile.cb),
+                                       bke(P, 2, tile.cb));
     else
         gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds, bkb(P, 2, tile.cb),
                        bke(P, 2, tile.cb));
@@ -287,7 +293,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     if (P.h2)
-        gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds);
+        gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds, bkb(P, 3, tile.cb),
+                               bke(P, 3, tile.cb));
     else
         gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds, bkb(P, 3, tile.cb),
                       bke(P, 3, tile.cb));
@@ -740,8 +747,8 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     AMP_REQUIRE(a->gemm == AMP_GEMM_AUTO || a->gemm == AMP_GEMM_F32 || a->gemm == AMP_GEMM_H2,
                 "amp_bamp_run: gemm %d (AUTO, F32 or H2)", a->gemm);
     const bool h2ok = bamp_h2_shape(d);
-    AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || h2ok, "amp_bamp_run: the fp16x2 GEMMs need N %% 64 == 0, n %% 64 == 0 and "
-                "Lin = Lout = 1 (N = %d, n = %d)", d->N, d->n);
+    AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || h2ok, "amp_bamp_run: the fp16x2 GEMMs need N %% 64 == 0 and n %% 64 == 0 "
+                "(N = %d, n = %d)", d->N, d->n);
     static const bool f32_env = [] {
         const char* e = getenv("AMP_BAMP_GEMM");
         return e && e[0] == 'f';
@@ -774,7 +781,24 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
     if ((rc = build_abs2_weight(H, 1, P.N, P.N, P.n, (float*)P.Wabs2T, P.kapB1, P.ncpB1, st))) return rc;
     if ((rc = build_cweight(H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.kapB2, P.ncpB2, st))) return rc;
     }
-    if (P.band[0]) {
+    if (P.band[0] && P.h2) {
+        // per column tile: real |H|^2 (two planes, 8 16-tiles per 128 outputs), complex H (four, 4)
+        if ((rc = h2_kband(P.Wabs2, 2, P.N / 32, 8, P.ncpA1 / 128, P.n / 16, const_cast<int*>(P.band[0]), st))) return rc;
+        if ((rc = h2_kband(P.WH, 4, P.N / 32, 4, P.ncpA2 / 128, P.n / 16, const_cast<int*>(P.band[1]), st))) return rc;
+        if ((rc = h2_kband(P.Wabs2T, 2, P.n / 32, 8, P.ncpB1 / 128, P.N / 16, const_cast<int*>(P.band[2]), st))) return rc;
+        if ((rc = h2_kband(P.WHH, 4, P.n / 32, P.bn / 32, P.ncpB2 / P.bn, P.N / 16, const_cast<int*>(P.band[3]), st))) return rc;
+        if (getenv("AMP_DEBUG_BAND")) {   // diagnostic: the ranges as formed (synchronises the stream)
+            const int nt[4] = {P.ncpA1 / 128, P.ncpA2 / 128, P.ncpB1 / 128, P.ncpB2 / P.bn};
+            for (int i = 0; i < 4; ++i) {
+                std::vector<int> h(2 * nt[i]);
+                hipMemcpyAsync(h.data(), P.band[i], h.size() * 4, hipMemcpyDeviceToHost, st);
+                hipStreamSynchronize(st);
+                fprintf(stderr, "band[%d]:", i);
+                for (int k = 0; k < nt[i]; ++k) fprintf(stderr, " %d-%d", h[2 * k], h[2 * k + 1]);
+                fprintf(stderr, "\n");
+            }
+        }
+    } else if (P.band[0]) {
         const float* wts[4] = {P.Wabs2, P.WH, P.Wabs2T, P.WHH};
         const int kaps[4] = {P.kapA1, P.kapA2, P.kapB1, P.kapB2}, ncps[4] = {P.ncpA1, P.ncpA2, P.ncpB1, P.ncpB2};
         const int bns[4] = {128, 128, 128, P.bn};

@@ -12,7 +12,10 @@
 //    scale exponent H2_EX;
 //  * products h0g0 + h0g1 + h1g0 on v_mfma_f32_16x16x32_f16 (two row blocks of 16 trials per wave
 //    share each weight fragment), f32 accumulation, the scales taken off exactly in the epilogue.
-// The A planes are staged through LDS in chunks of H2KC elements; the weights stream from L2.
+// The A planes are staged through LDS in chunks of H2KC elements, in amp_persist.h's XOR-permuted
+// plane layout (pl_col: the fragment reads and the staging stores hit distinct banks); the weights
+// stream from L2.  A block-banded operator (the ISI channel) reduces each tile over [kb, ke) only
+// (h2_kband).
 #pragma once
 
 #include "amp_gemm.h"
@@ -21,7 +24,12 @@
 namespace amp {
 
 constexpr int H2KC = 256;           // A elements (complex or real) per staged chunk
-constexpr int H2LDK = H2KC + 8;     // LDS row stride of a staged plane (fp16; 16-byte pad)
+#ifdef AMP_H2_PAD_LAYOUT
+constexpr int H2SWM = 0;            // A/B builds: the 16-byte row pad of the first version
+#else
+constexpr int H2SWM = 15;           // chunk permutation mask (pl_col)
+#endif
+constexpr int H2LDK = H2KC + (H2SWM ? 0 : 8);   // LDS row stride of a staged plane (fp16)
 
 // bytes of LDS gemm_tile_h2<BN, CPX> needs (the staged planes; the C tile aliases them)
 template <int BN, bool CPX>
@@ -96,10 +104,12 @@ __global__ __launch_bounds__(256) void h2_split_rows_kernel(const float* __restr
 // GemmCfg<BN>::LDC).  planes / rexp: h2_split_rows_kernel's output for K elements per row
 // (rows_pad rows, K % 64 == 0); wq: the h2-packed operator (J = K) with scale exponent wex, ncp
 // (complex or real outputs) a multiple of 16.  Each wave owns NT output tiles of 16 (complex: BN / 128, real: BN / 64).
+// [kb, ke): the reduction range holding every nonzero weight of this column tile (multiples of
+// 64; h2_kband), default all of it.
 template <int BN, bool CPX>
 __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ planes, int rows_pad,
                                              const int* __restrict__ rexp, int K, const void* __restrict__ wq,
-                                             int wex, int row0, int col0, float* lds) {
+                                             int wex, int row0, int col0, float* lds, int kb = 0, int ke = -1) {
     using Cg = GemmCfg<BN>;
     constexpr int PL = CPX ? 4 : 2;                  // planes
     constexpr int NT = CPX ? BN / 128 : BN / 64;      // 16-wide output tiles per wave
@@ -114,6 +124,8 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
     // this wave's first output tile and its weight stream (one buffer resource, SGPR offsets)
     const int ct0 = (CPX ? col0 / 2 : col0) / 16 + wave * NT;
     const int G = K >> 5;                               // groups of 32 reduction elements
+    if (ke < 0) ke = K;
+    const int gl1 = (ke > kb ? ke >> 5 : 1) - 1;        // last group of the range (refill clamp)
     const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (char*)const_cast<void*>(wq) + (size_t)ct0u * G * PL * 1024, (short)0, 0x7ffffff0, 0x00020000);
@@ -133,7 +145,9 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
         (void)gg;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const unsigned short* ap = sP + (16 * b + (lane & 15)) * H2LDK + 32 * gl + 8 * (lane >> 4);
+            // chunk 4 gl + (lane >> 4) of row lane & 15, permuted (pl_col, m = 15)
+            const int sw = lane & 15 & H2SWM;
+            const unsigned short* ap = sP + (16 * b + (lane & 15)) * H2LDK + 8 * ((lane >> 4) ^ (sw & 3)) + ((32 * gl) ^ (32 * (sw >> 2)));
             u32x4 a[PL];
 #pragma unroll
             for (int f = 0; f < PL; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * GBM * H2LDK);
@@ -157,11 +171,13 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
             }
         }
     };
-    wload(wA, 0);
-    if (G > 1) wload(wB, 1);
-    for (int kc0 = 0; kc0 < K; kc0 += H2KC) {
-        const int kc = min(H2KC, K - kc0);
-        if (kc0 > 0) __syncthreads();                   // every wave done with the previous chunk
+    if (ke > kb) {
+        wload(wA, kb >> 5);
+        wload(wB, min((kb >> 5) + 1, gl1));
+    }
+    for (int kc0 = kb; kc0 < ke; kc0 += H2KC) {
+        const int kc = min(H2KC, ke - kc0);
+        if (kc0 > kb) __syncthreads();                  // every wave done with the previous chunk
         // stage PL planes x 32 rows x kc elements (16-byte loads, all in flight before the stores)
         {
             const int q8 = kc >> 3;                     // 16-byte units per plane row
@@ -181,7 +197,7 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
                 const int e = tid + i * AMP_WG;
                 if (e < tot) {
                     const int f = e / (GBM * q8), rem = e - f * GBM * q8, r = rem / q8, c8 = rem - r * q8;
-                    *reinterpret_cast<u32x4*>(sP + (f * GBM + r) * H2LDK + 8 * c8) = v[i];
+                    *reinterpret_cast<u32x4*>(sP + (f * GBM + r) * H2LDK + pl_col(r, 8 * c8, H2SWM)) = v[i];
                 }
             }
         }
@@ -195,19 +211,19 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
 #pragma unroll
             for (int g = 0; g < H2KC / 32; g += 2) {
                 mma_group(g0 + g, g, wA);
-                wload(wA, min(g0 + g + 2, G - 1));
+                wload(wA, min(g0 + g + 2, gl1));
                 __builtin_amdgcn_sched_barrier(0);   // keep the refill behind its group's MFMAs
                 mma_group(g0 + g + 1, g + 1, wB);
-                wload(wB, min(g0 + g + 3, G - 1));
+                wload(wB, min(g0 + g + 3, gl1));
                 __builtin_amdgcn_sched_barrier(0);
             }
         } else {
             for (int g = 0; g < gc; g += 2) {
                 mma_group(g0 + g, g, wA);
-                wload(wA, min(g0 + g + 2, G - 1));
+                wload(wA, min(g0 + g + 2, gl1));
                 __builtin_amdgcn_sched_barrier(0);   // keep the refill behind its group's MFMAs
                 mma_group(g0 + g + 1, g + 1, wB);
-                wload(wB, min(g0 + g + 3, G - 1));
+                wload(wB, min(g0 + g + 3, gl1));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -232,6 +248,39 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
             }
         }
     __syncthreads();
+}
+
+// The reduction range of each column tile of an h2-packed operator (h2_index / h2r_index, PL
+// planes, n16 packed 16-output tiles): grid (column tile, slice of 64 groups), the first / last 32-group holding a nonzero
+// piece (NaN / inf included), met through atomic min / max in band[] (weight_kband_init before,
+// h2_kband_fin after, amp_weights.hip), then widened to whole 64-element pairs: [kb, ke) in reduction elements.
+template <int PL>
+__global__ __launch_bounds__(256) void h2_kband_kernel(const u32x4* __restrict__ wq, int G, int tpt, int gps, int n16,
+                                                       int* __restrict__ band) {
+    __shared__ int s_lo, s_hi;
+    if (threadIdx.x == 0) { s_lo = G; s_hi = -1; }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ga = blockIdx.y * gps, gn = min(gps, G - ga);
+    int lo = G, hi = -1;
+    for (int b = wave; b < tpt * gn; b += blockDim.x >> 6) {   // wave-uniform
+        const int t16 = blockIdx.x * tpt + b / gn, g = ga + b % gn;
+        if (t16 >= n16) continue;                               // past the operator's outputs (tail tile)
+        const size_t base = ((size_t)t16 * G + g) * PL * 64 + lane;
+        unsigned bits = 0u;
+#pragma unroll
+        for (int f = 0; f < PL; ++f) {
+            const u32x4 v = wq[base + (size_t)f * 64];
+            bits |= v.x | v.y | v.z | v.w;
+        }
+        if (__any((bits & 0x7fff7fffu) != 0u)) { lo = min(lo, g); hi = max(hi, g); }
+    }
+    if (lane == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_hi >= 0) {
+        atomicMin(&band[2 * blockIdx.x], s_lo);
+        atomicMax(&band[2 * blockIdx.x + 1], s_hi);
+    }
 }
 
 }  // namespace amp

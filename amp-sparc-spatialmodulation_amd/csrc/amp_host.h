@@ -185,7 +185,15 @@ inline int persist_grid_launch(const char* what, const void* fn, int nwg, int th
 
 // Column tile width of the section-fused GEMMs: a multiple of 2M so no section straddles
 // two workgroups.
-inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
+// AMP_SECTION_BN=256: the wide column tile also where sections fit the narrow one (A/B runs)
+inline bool section_bn_wide_env() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_SECTION_BN");
+        return e && atoi(e) == 256;
+    }();
+    return v;
+}
+inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128 && !section_bn_wide_env()) ? 128 : 256; }
 
 // Expanded-weight builders (amp_weights.hip)
 enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2, WPACKX3 = 3, WPACKH2 = 4, WPACKH2_ABS2 = 5 };
@@ -213,6 +221,7 @@ int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* 
 // (multiples of GBK) that holds all its nonzero entries -> band[2 c], band[2 c + 1] (kb = ke when
 // the tile is all zero).  One pass over the weight (amp_weights.hip).
 int weight_kband(const float* wp, int kap, int ncp, int BN, int* band, hipStream_t st);
+int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* band, hipStream_t st);
 template <int BN>
 int set_lds_attr(const void* fn);
 int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,

@@ -98,7 +98,7 @@ struct ScampWs {
 // 128 columns whenever a section fits (2M <= 128): twice the workgroups of a whole-coupling-
 // block tile (cfg3: 256 instead of 128).  A tile that does not hold whole coupling blocks
 // (2 Nt > BN) leaves psi to scamp_psi.
-inline int scamp_bn(const amp_dims* d) { return (2 * d->M <= 128) ? 128 : 256; }
+inline int scamp_bn(const amp_dims* d) { return section_bn(d); }
 inline int scamp_psi_nblk(const amp_dims* d) { return std::max(1, std::min(cdiv(d->B * d->Lin, AMP_WG / 64), 2048)); }
 
 inline void scamp_geometry(const amp_dims* d, ScampK& P) {

@@ -30,12 +30,38 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     const float* psi = spsi(P, t + 1);               // psi of iteration t-1 (ones at t = 0)
     const float* phi_old = sphi(P, t + 1);           // +inf at t = 0 (scamp.py:19)
     float* phi_new = sphi(P, t);
+    // gamma of each (trial, output block) the tile touches, formed once (the same float32 sum as
+    // scamp_gamma) instead of once per element: Lin MACs of global loads per element had made the
+    // epilogue, not the GEMM, the cost of a Lin > 1 tile
+    // The rows' psi and the W rows come into LDS first (coalesced), so the serial float32 sums
+    // read LDS, not a chain of dependent global loads.
+    const int lo0 = (col0 >> 1) / P.Nr, nlo = (min((col0 >> 1) + 63, P.n - 1)) / P.Nr - lo0 + 1;
+    const int Lin = P.Lin;
+    float* sg = lds + C::CTILE_FLOATS;                 // [GBM][nlo] gamma
+    float* sp = sg + GBM * nlo;                        // [GBM][Lin] psi rows
+    float* sw = sp + GBM * Lin;                        // [nlo][Lin] W rows lo0 ..
+    const bool per_block = C::CTILE_FLOATS + GBM * nlo + GBM * Lin + nlo * Lin <= C::A_FLOATS;
+    if (per_block) {
+        for (int e = threadIdx.x; e < GBM * Lin; e += AMP_WG) {
+            const int row = row0 + e / Lin;
+            sp[e] = row < P.B ? psi[(size_t)row0 * Lin + e] : 0.f;
+        }
+        for (int e = threadIdx.x; e < nlo * Lin; e += AMP_WG) sw[e] = P.W[(size_t)lo0 * Lin + e];
+        __syncthreads();
+        for (int e = threadIdx.x; e < GBM * nlo; e += AMP_WG) {
+            const int rho = e / nlo, j = e - rho * nlo;
+            float g = 0.f;                             // scamp_gamma's sum, in its order
+            for (int lc = 0; lc < Lin; ++lc) g += sw[j * Lin + lc] * sp[rho * Lin + lc];
+            sg[e] = g / (float)Lin;
+        }
+        __syncthreads();
+    }
     for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
         const int rho = e >> 6, cp = e & 63;
         const int row = row0 + rho, i = (col0 >> 1) + cp;
         if (row < P.B && i < P.n) {
             const int lo = i / P.Nr;
-            const float gma = scamp_gamma(P, psi + (size_t)row * P.Lin, lo);
+            const float gma = per_block ? sg[rho * nlo + lo - lo0] : scamp_gamma(P, psi + (size_t)row * P.Lin, lo);
             const float b = gma / phi_old[(size_t)row * P.Lout + lo];
             const size_t oc = (size_t)row * twon + 2 * i;
             const float ar = lds[rho * C::LDC + 2 * cp], ai = lds[rho * C::LDC + 2 * cp + 1];
@@ -52,8 +78,8 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
 
 struct ScampDenoisePolicy {
     const float* tile;
-    const float* tau_tile;   // LDS [32][Lin] tau of the tile's rows
-    int ldc, spr, M, N, Nt, L, row0, colc0, Lin;
+    const float* tau_tile;   // LDS [32][Lin] tau of the tile's rows and blocks lc0 .. lc0 + Lin - 1
+    int ldc, spr, M, N, Nt, L, row0, colc0, Lin, lc0;
     float* xm;
     float* secmax;
     float* secabs;
@@ -62,7 +88,7 @@ struct ScampDenoisePolicy {
         const int cc = sj * M + m;
         const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * cc);
         rr = v.x; ri = v.y;
-        it = 1.0f / (tau_tile[rho * Lin + (colc0 + cc) / Nt] * 0.5f);   // tau_use / 2 (scamp.py:63)
+        it = 1.0f / (tau_tile[rho * Lin + (colc0 + cc) / Nt - lc0] * 0.5f);   // tau_use / 2 (scamp.py:63)
     }
     __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float, PartAcc&) const {
         const int rho = sec / spr, sj = sec - rho * spr;
@@ -90,26 +116,47 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     const int lc0 = (col0 / 2) / P.Nt, nlc = max(1, (ncols / 2) / P.Nt);   // coupling blocks in this tile
-    float* tau_t = lds + C::CTILE_FLOATS;                                    // [32][Lin]
+    // tau of the blocks this tile covers only (blocks lc0 .. lc0 + ntc - 1): each is written to
+    // P.tau by the tile that holds its first column
+    const int ntc = (col0 / 2 + ncols / 2 - 1) / P.Nt - lc0 + 1;
+    float* tau_t = lds + C::CTILE_FLOATS;                                    // [32][ntc]
     const float* phi = sphi(P, t);
-    for (int e = threadIdx.x; e < GBM * P.Lin; e += AMP_WG) {
-        const int rho = e / P.Lin, lc = e % P.Lin;
+    // the rows' 1 / phi and the W columns lc0 .. into LDS first (coalesced): the serial float32
+    // sums then read LDS instead of a chain of dependent global loads
+    const int Lout = P.Lout;
+    float* siph = tau_t + GBM * ntc;                                         // [32][Lout] 1 / phi
+    float* swc = siph + GBM * Lout;                                          // [ntc][Lout] W columns
+    const bool staged = C::CTILE_FLOATS + GBM * ntc + GBM * Lout + ntc * Lout <= C::A_FLOATS;
+    if (staged) {
+        for (int e = threadIdx.x; e < GBM * Lout; e += AMP_WG)
+            siph[e] = e / Lout < nrows ? 1.0f / phi[(size_t)row0 * Lout + e] : 0.f;
+        for (int e = threadIdx.x; e < ntc * Lout; e += AMP_WG) {
+            const int j = e / Lout, lo = e - j * Lout;
+            swc[e] = P.W[lo * P.Lin + lc0 + j];
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < GBM * ntc; e += AMP_WG) {
+        const int rho = e / ntc, lc = lc0 + e - rho * ntc;
         float tv = 0.f;
         if (rho < nrows) {
             float acc = 0.f;   // (W^T (1/phi))[lc] in float32
-            for (int lo = 0; lo < P.Lout; ++lo)
-                acc += P.W[lo * P.Lin + lc] * (1.0f / phi[(size_t)(row0 + rho) * P.Lout + lo]);
+            if (staged)
+                for (int lo = 0; lo < Lout; ++lo) acc += swc[(lc - lc0) * Lout + lo] * siph[rho * Lout + lo];
+            else
+                for (int lo = 0; lo < P.Lout; ++lo)
+                    acc += P.W[lo * P.Lin + lc] * (1.0f / phi[(size_t)(row0 + rho) * P.Lout + lo]);
             tv = ((1.0f / acc) * (float)P.L) / (float)P.Nr;          // L / x = recip(x) * L ; / Mr
-            if (tile.cb == 0) P.tau[(size_t)(row0 + rho) * P.Lin + lc] = tv;
+            if (lc * P.Nt >= col0 / 2) P.tau[(size_t)(row0 + rho) * P.Lin + lc] = tv;
         }
-        tau_t[rho * P.Lin + lc] = tv;
+        tau_t[e] = tv;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
         const int rho = e / BN, cc = e % BN;
         if (rho < nrows && cc < ncols) {
             const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
-            const float tv = tau_t[rho * P.Lin + ((col0 + cc) >> 1) / P.Nt];
+            const float tv = tau_t[rho * ntc + ((col0 + cc) >> 1) / P.Nt - lc0];
             const float xp = P.xm[o] + tv * lds[rho * C::LDC + cc];
             P.xmap[o] = xp;
             lds[rho * C::LDC + cc] = xp;
@@ -118,7 +165,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     __syncthreads();
     ScampDenoisePolicy pol;
     pol.tile = lds; pol.tau_tile = tau_t; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.Nt = P.Nt; pol.L = P.L;
-    pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2; pol.Lin = P.Lin;
+    pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2; pol.Lin = ntc; pol.lc0 = lc0;
     pol.xm = P.xm; pol.secmax = P.secmax; pol.secabs = P.secabs;
     PartAcc pa;
     denoise_sections<false, KK>(pol, nrows * pol.spr, P.M, P.c, pa);

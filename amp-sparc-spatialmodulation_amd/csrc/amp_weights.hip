@@ -275,19 +275,28 @@ __global__ __launch_bounds__(AMP_WG) void gemm_store_kernel(const float* __restr
     }
 }
 
-// One workgroup per BN-column tile; each wave takes (column group, reduction group) blocks of the
-// packed layout (64 float4 = one lane each, wcol in gemm_tile) and keeps the first / last group
-// holding a nonzero value (NaN / inf count as nonzero: they must reach the product).
-__global__ __launch_bounds__(256) void weight_kband_kernel(const float4* __restrict__ wp, int G, int cgs,
+// Grid (column tile, reduction slice): each wave takes (column group, reduction group) blocks of
+// the packed layout (64 float4 = one lane each, wcol in gemm_tile) within its slice and keeps the
+// first / last group holding a nonzero value (NaN / inf count as nonzero: they must reach the
+// product); the slices meet in band[] through atomic min / max (vector atomics), bracketed by an
+// init and a conversion launch.  (One workgroup per tile had taken 225 us per operator at the
+// ISI shape: 17 workgroups walking 8 MB.)
+__global__ __launch_bounds__(256) void weight_kband_init(int* __restrict__ band, int ntiles, int G) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) { band[2 * t] = G; band[2 * t + 1] = -1; }
+}
+
+__global__ __launch_bounds__(256) void weight_kband_kernel(const float4* __restrict__ wp, int G, int cgs, int gps,
                                                            int* __restrict__ band) {
     __shared__ int s_lo, s_hi;
     if (threadIdx.x == 0) { s_lo = G; s_hi = -1; }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cg0 = blockIdx.x * cgs;
+    const int ga = blockIdx.y * gps, gn = min(gps, G - ga);
     int lo = G, hi = -1;
-    for (int b = wave; b < cgs * G; b += blockDim.x >> 6) {   // wave-uniform
-        const int cg = cg0 + b / G, g = b % G;
+    for (int b = wave; b < cgs * gn; b += blockDim.x >> 6) {   // wave-uniform
+        const int cg = cg0 + b / gn, g = ga + b % gn;
         const float4 v = wp[((size_t)cg * G + g) * 64 + lane];
         const bool nz = (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f) | (v.x != v.x) | (v.y != v.y) |
                         (v.z != v.z) | (v.w != v.w);
@@ -295,21 +304,58 @@ __global__ __launch_bounds__(256) void weight_kband_kernel(const float4* __restr
     }
     if (lane == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int gpk = GBK / 8;                           // reduction groups per GBK
-        const int kb = s_hi < 0 ? 0 : (s_lo / gpk) * GBK;
-        const int ke = s_hi < 0 ? 0 : ((s_hi + gpk) / gpk) * GBK;
-        band[2 * blockIdx.x] = kb;
-        band[2 * blockIdx.x + 1] = ke;
+    if (threadIdx.x == 0 && s_hi >= 0) {
+        atomicMin(&band[2 * blockIdx.x], s_lo);
+        atomicMax(&band[2 * blockIdx.x + 1], s_hi);
     }
+}
+
+__global__ __launch_bounds__(256) void weight_kband_fin(int* __restrict__ band, int ntiles) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const int lo = band[2 * t], hi = band[2 * t + 1];
+    const int gpk = GBK / 8;                               // reduction groups per GBK
+    band[2 * t] = hi < 0 ? 0 : (lo / gpk) * GBK;
+    band[2 * t + 1] = hi < 0 ? 0 : ((hi + gpk) / gpk) * GBK;
 }
 
 int weight_kband(const float* wp, int kap, int ncp, int BN, int* band, hipStream_t st) {
     AMP_REQUIRE(kap % GBK == 0 && ncp % BN == 0 && BN % 32 == 0, "weight_kband: kap %d / ncp %d / BN %d", kap, ncp,
                 BN);
-    hipLaunchKernelGGL(weight_kband_kernel, dim3(ncp / BN), dim3(256), 0, st, (const float4*)wp, kap / 8, BN / 32,
-                       band);
+    const int nt = ncp / BN, G = kap / 8;
+    const int gps = 64;                                    // reduction groups per slice: 64 KB per tile-slice
+    hipLaunchKernelGGL(weight_kband_init, dim3(cdiv(nt, 256)), dim3(256), 0, st, band, nt, G);
+    hipLaunchKernelGGL(weight_kband_kernel, dim3(nt, cdiv(G, gps)), dim3(256), 0, st, (const float4*)wp, G, BN / 32,
+                       gps, band);
+    hipLaunchKernelGGL(weight_kband_fin, dim3(cdiv(nt, 256)), dim3(256), 0, st, band, nt);
     AMP_LAUNCH_CHECK("weight_kband");
+    return AMP_OK;
+}
+
+// [lo, hi] 32-groups -> [kb, ke) in reduction elements, whole 64-element pairs
+__global__ __launch_bounds__(256) void h2_kband_fin(int* __restrict__ band, int ntiles) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const int lo = band[2 * t], hi = band[2 * t + 1];
+    band[2 * t] = hi < 0 ? 0 : 32 * (lo & ~1);
+    band[2 * t + 1] = hi < 0 ? 0 : 32 * ((hi | 1) + 1);
+}
+
+// h2_kband_kernel over an h2-packed operator (PL planes, G 32-groups per 16-output tile, tpt
+// 16-output tiles per GEMM column tile, ntiles column tiles, n16 packed 16-output tiles): [kb, ke)
+// per column tile.
+int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* band, hipStream_t st) {
+    AMP_REQUIRE(G % 2 == 0 && (PL == 2 || PL == 4), "h2_kband: G %d / PL %d", G, PL);
+    const int gps = 64;
+    hipLaunchKernelGGL(weight_kband_init, dim3(cdiv(ntiles, 256)), dim3(256), 0, st, band, ntiles, G);
+    if (PL == 4)
+        hipLaunchKernelGGL(h2_kband_kernel<4>, dim3(ntiles, cdiv(G, gps)), dim3(256), 0, st, (const u32x4*)wq, G, tpt,
+                           gps, n16, band);
+    else
+        hipLaunchKernelGGL(h2_kband_kernel<2>, dim3(ntiles, cdiv(G, gps)), dim3(256), 0, st, (const u32x4*)wq, G, tpt,
+                           gps, n16, band);
+    hipLaunchKernelGGL(h2_kband_fin, dim3(cdiv(ntiles, 256)), dim3(256), 0, st, band, ntiles);
+    AMP_LAUNCH_CHECK("h2_kband");
     return AMP_OK;
 }
 
