@@ -95,6 +95,7 @@ SIGNATURES = {
     'amp_vamp2_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_vamp2_run': (C.c_int, [_D, _K, C.POINTER(AmpVamp2Args), _P]),
     'amp_vamp_persist_trace': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P, _P]),
+    'amp_scamp_persist_trace': (C.c_int, [_D, _K, C.POINTER(AmpScampArgs), _P, _P]),
     'amp_vamp_run': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _P]),
     'amp_vamp_iterate': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),

@@ -76,6 +76,7 @@ struct ScampK {
     const long long* idx;  // [B*L] flat nonzero indices
     DecWG* dwg;            // [nwg] per-workgroup records
     amp_counts* counts;    // out
+    unsigned long long* trace;   // diagnostic phase stamps (amp_scamp_persist_trace), else null
     Const c;
 };
 

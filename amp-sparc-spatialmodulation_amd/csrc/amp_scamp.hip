@@ -647,6 +647,7 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.dec_on = 0; P.ibits = 0; P.xtrue = nullptr; P.sym = nullptr; P.idx = nullptr; P.counts = nullptr;
     P.dwg = w.dwg;
+    P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
     AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_H2, "amp_scamp: gemm %d", a->gemm);
@@ -802,6 +803,23 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
     for (int t = 0; t < P.max_iter; ++t)
         if ((rc = scamp_iterate_impl(P, c64, t, st))) return rc;
     return scamp_finalize_impl(P, st);
+}
+
+// Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
+// boundary: trace[(wg * max_iter + t) * 10 + phase] (phases: amp_scamp_persist_kernel.h).
+int amp_scamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* trace,
+                            void* stream) {
+    ScampK P;
+    Const64 c64;
+    int rc = scamp_setup(d, c, a, P, c64);
+    if (rc) return rc;
+    AMP_REQUIRE(trace && scamp_persist_eligible(d, device_cu_count()), "amp_scamp_persist_trace: not eligible / null trace");
+    hipStream_t st = (hipStream_t)stream;
+    if ((rc = scamp_persist_prepare(P, a, st))) return rc;
+    P.trace = (unsigned long long*)trace;
+    DecConst dc;
+    static_cast<Const64&>(dc) = c64;
+    return scamp_persist_launch(P, dc, st);
 }
 
 int amp_scamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a,

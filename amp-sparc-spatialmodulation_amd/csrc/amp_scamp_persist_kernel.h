@@ -156,9 +156,16 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
     const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
     unsigned nbar = 0;
     int fixed = 0, fixed_all = 0, aborted = 0, stopped = 0, T = P.max_iter, last_t = 0;
+    // diagnostic phase stamps (amp_scamp_persist_trace): 0 start, 1 scalars + x planes, 2 GEMM1,
+    // 3 s stored, 4 GEMM2 + xmap, 5 denoiser, 6 psi + publish, 7 gather, 8 iteration end
+    unsigned long long* trc = P.trace;
+    auto stamp = [&](int t, int ph) {
+        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * 10 + ph] = __builtin_amdgcn_s_memtime();
+    };
 
     for (int t = 0; t < P.max_iter; ++t) {
         last_t = t;
+        stamp(t, 0);
         float* psi_prev = lds + ((t & 1) ? Y.offP0 : Y.offP1);
         float* psi_new = lds + ((t & 1) ? Y.offP1 : Y.offP0);
         // 1. coupling scalars per trial (scamp.py:45-53), float32 as amp_scamp.hip forms them
@@ -227,6 +234,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
                 }
             }
             __syncthreads();
+            stamp(t, 1);
             gemm_h2<NC1, G1 / 4>(sP, ldp1, P.Wx1, cc1, cr1, ci1);
         } else if constexpr (X3) {
             for (int e = tid; e < SPB * (N >> 3); e += PWG) {   // x rows -> bf16 planes, 8 per item
@@ -241,8 +249,10 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
                 x3_store8(sP, ldp1, row, j0, re, im);
             }
             __syncthreads();
+            stamp(t, 1);
             gemm_x3<NC1, G1 / 4>(sP, ldp1, P.Wx1, cc1, cr1, ci1);
         } else {
+            stamp(t, 1);
             gemm16<NT1, G1>(sX, ldx, P.Wq1, ct1, acc1);
         }
         float hsc[4];   // H2: 2^-(e_row + SH2_EX) of this lane's rows (x rows, then s rows)
@@ -253,6 +263,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
             for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + SH2_EX));
         }
         __syncthreads();   // tau / b / phi published; every wave done reading x
+        stamp(t, 2);
         if constexpr (H2) {
             float mrow[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -334,6 +345,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
             }
         }
         __syncthreads();
+        stamp(t, 3);
         // 3. GEMM2 A^H s ; xmap = x + tau (A^H s)
         f32x4 acc2[NT2];
         if constexpr (X3) {
@@ -375,6 +387,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         }
         }
         __syncthreads();
+        stamp(t, 4);
         // 4. denoiser -> x, then psi and its allclose count
         SPDenoisePolicy pol{sR, sX, sITau, sM, sA, ldx, M, 31 - __builtin_clz(spr), Nt, Lin};
         PartAcc pa;
@@ -383,6 +396,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         else
             denoise_sections_u<false, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
         __syncthreads();
+        stamp(t, 5);
         unsigned nc = 0;
         for (int b = wave; b < nrows * Lin; b += NW) {        // one wavefront per (row, block)
             const int row = b / Lin, lc = b - row * Lin;
@@ -395,12 +409,14 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         pa.notclose += nc;
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
+        stamp(t, 6);
         // 5. batch-global max|xi| / danger test / allclose count
         PartAcc g;
         if (!part_gather(grs, (unsigned)t * nwg * 32u, nwg, tag, P.pbar + 1, g, scr, &s_flag)) {
             aborted = 1;
             break;
         }
+        stamp(t, 7);
         fixed = 0;
         uint32_t notclose = g.notclose;
         if (part_allnan(g)) {
@@ -484,6 +500,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
             notclose = (uint32_t)((long long)notclose + (long long)b);
         }
         __syncthreads();
+        stamp(t, 8);
         if (notclose == 0) {                                   // scamp.py:105-106
             stopped = 1;
             T = t + 1;

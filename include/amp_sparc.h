@@ -291,6 +291,10 @@ size_t amp_scamp_workspace_bytes(const amp_dims* d, int32_t max_iter);
  *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
 int amp_scamp_select_engine(const amp_dims* d, int32_t engine);
 int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* stream);
+/* Diagnostic (tools/trace_persist.py --config cfg3): one persistent SCAMP forward with s_memtime
+ * stamps per (workgroup, iteration, phase) into `trace` (ceil(B/16) * max_iter * 10 uint64). */
+int amp_scamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_scamp_args* a, void* trace,
+                            void* stream);
 /* SCAMP.forward + Loss.error_rate in one call (scamp.py:77-107 then loss.py:67-179), as
  * amp_vamp_detect_count: the persistent engine's forward with the MAP decision on xmap
  * (scamp.py:107) fused into the same launch (each workgroup decides the rows it holds in LDS; one

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Phase timing of the persistent VAMP engine (amp_vamp_persist_trace): per iteration and
-workgroup s_memtime stamps -> median cycles per phase, barrier skew across workgroups.
+"""Phase timing of the persistent engines (amp_vamp_persist_trace / amp_scamp_persist_trace): per
+iteration and workgroup s_memtime stamps -> median cycles per phase, barrier skew across workgroups.
 
   python tools/trace_persist.py [--config cfg4] [--ebn0 8]
+  python tools/trace_persist.py --config cfg3        (SCAMP, tools/configs_bench.py's cfg3 inputs)
 """
 import argparse
 import ctypes as C
@@ -19,6 +20,52 @@ import torch        # noqa: E402
 PHASES = ['r~ build', 'GEMM1', 'w store', 'GEMM2 + r', 'denoiser', 'partial publish', 'partial gather', 'scalars']
 STRIDE = 10   # stamps per (workgroup, iteration): amp_vamp_persist.hip AMP_TRACE_STRIDE
 ORDER = [0, 1, 2, 3, 4, 8, 5, 6, 7]   # stamp slots in time order
+SPHASES = ['scalars + x planes', 'GEMM1', 's store', 'GEMM2 + xmap', 'denoiser', 'psi + publish',
+           'partial gather', 'danger / exit']
+SORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+
+
+def scamp_trace(cfgname, ebn0):
+    """cfg3-like SCAMP inputs (tools/configs_bench.py), one traced persistent forward."""
+    import amp_native as nat
+    from channel import Channel
+    from config import Config
+    from data import Data
+    from scamp import SCAMP
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    import configs_bench
+    algo, Nt, Na, Nr, B, alph, iters, e0 = configs_bench.CFGS[cfgname]
+    assert algo == 'scamp', cfgname
+    cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
+                 channel_profile='uniform', channel_truncation='tail', device='cpu')
+    np.random.seed(0)
+    torch.manual_seed(0)
+    ch, da = Channel(cfg), Data(cfg)
+    W, A = ch.generate_as_sparc()
+    x, _, _ = da.generate_message()
+    SNR = cfg.snr(ebn0 if ebn0 is not None else e0)
+    y = A @ x + ch.awgn(SNR)
+    cfg.device = 'cuda'
+    dev = torch.device('cuda', 0)
+    W, A, y = (t.to(dev).contiguous() for t in (W, A, y))
+    det = SCAMP(cfg, engine=nat.ENGINE_PERSISTENT)
+    for _ in range(3):
+        det.detect(W, A, y, SNR)
+    T = det.detect(W, A, y, SNR)
+    nwg = (B + 15) // 16
+    tr = torch.zeros(nwg * iters * STRIDE + 2 * nwg, dtype=torch.int64, device=dev)
+    nat.check(nat.lib().amp_scamp_persist_trace(C.byref(T.dims), C.byref(T.const), C.byref(T.args), nat.dptr(tr),
+                                                T.stream), 'trace')
+    torch.cuda.synchronize()
+    Tn = int(T.status().T)
+    st = tr.cpu().numpy()[:nwg * iters * STRIDE].reshape(nwg, iters, STRIDE).astype(np.int64)[:, :Tn, SORDER]
+    d = np.diff(st, axis=2)
+    per_it = np.median(st[:, 1:, 0] - st[:, :-1, 0]) if Tn > 1 else 0
+    print(f'SCAMP {cfgname}: T={Tn}  nwg={nwg}  median cycles per iteration {per_it:.0f}')
+    for i, name in enumerate(SPHASES):
+        v = d[:, 1:, i] if Tn > 1 else d[:, :, i]
+        print(f'  {name:22s} median {np.median(v):9.0f}  p10 {np.percentile(v, 10):9.0f}  p90 {np.percentile(v, 90):9.0f}'
+              f'  ({100 * np.median(v) / per_it:5.1f} %)' if per_it else '')
 
 
 def main():
@@ -28,8 +75,12 @@ def main():
     from vamp import VAMP
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='cfg4')
-    ap.add_argument('--ebn0', type=float, default=8.0)
+    ap.add_argument('--ebn0', type=float, default=None)
     args = ap.parse_args()
+    if args.config.startswith('cfg3'):
+        return scamp_trace(args.config, args.ebn0)
+    if args.ebn0 is None:
+        args.ebn0 = 8.0
     Nt, Na, Nr, B, alph, iters = bench.CONFIGS[args.config]
     cfg = Config(Nt, Na, Nr, 1, 1, batch=B, generator_mode='sparc', iterations=iters, alphabet=alph,
                  channel_profile='uniform', channel_truncation='tail', device='cuda')
