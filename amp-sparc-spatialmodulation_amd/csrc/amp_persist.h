@@ -89,6 +89,15 @@ __device__ __forceinline__ int pl_mask(int ldx) {
     return (b < 16 ? b : 16) - 1;
 }
 __device__ __forceinline__ int pl_col(int row, int j, int m) { return j ^ ((row & m) << 3); }
+// The permuted addresses are cheap to form but loop-invariant, so the compiler would hoist every
+// one of them out of the persistent engines' iteration loop and keep it live across the denoiser
+// (spilling at 512 VGPRs); pl_opaque pins their inputs inside the loop (an empty volatile asm).
+__device__ __forceinline__ int pl_opaque(int x) {
+#ifndef AMP_PL_HOIST
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
 
 // ---- split-precision complex GEMM (bf16x3) ----
 // x = x0 + x1 + x2 with bf16 pieces (round-to-nearest-even; each residual is exact in f32), so
@@ -128,7 +137,7 @@ __device__ __forceinline__ void x3_store8(unsigned short* sP, int ldx, int row, 
         split3x2(im[2 * h], im[2 * h + 1], b0, b1, b2);
         q[0][h] = a0; q[1][h] = a1; q[2][h] = a2; q[3][h] = b0; q[4][h] = b1; q[5][h] = b2;
     }
-    const int c = pl_col(row, j0, pl_mask(ldx));
+    const int c = pl_col(pl_opaque(row), j0, pl_mask(ldx));
 #pragma unroll
     for (int f = 0; f < 6; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + c) = q[f];
 }
@@ -142,7 +151,7 @@ __device__ __forceinline__ float dpp_swap_pair(float v) {   // lane l <-> l ^ 1 
 // odd lane rows +2 / +3 (one DPP swap per sent value; no 16-bit LDS stores).
 __device__ __forceinline__ void x3_store_acc(unsigned short* sP, int ldx, int o, const float (&vr)[4],
                                              const float (&vi)[4]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = pl_opaque((int)threadIdx.x) & 63;
     const bool odd = (lane & 1) != 0;
     float gr[2], gi[2];
 #pragma unroll
@@ -203,8 +212,9 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
                 ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 6 + f) * 1024, 0);
     // A fragment of group g: row lane & 15, chunk 4 g + (lane >> 4), permuted (pl_col): element
     // 8 ((4 g + q) ^ sw) = ((32 g) ^ s32) + 8 (q ^ (sw & 3)), s32 = 32 (sw >> 2) (one v_xad per g)
-    const int sw = (lane & 15) & pl_mask(ldx);
-    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * ((lane >> 4) ^ (sw & 3));
+    const int ln = pl_opaque(lane);
+    const int sw = (ln & 15) & pl_mask(ldx);
+    const unsigned short* ap = sP + (ln & 15) * ldx + 8 * ((ln >> 4) ^ (sw & 3));
     const int s32 = 32 * (sw >> 2);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
     u32x4 an[6];
@@ -307,7 +317,7 @@ __device__ __forceinline__ void h2_store8(unsigned short* sP, int ldx, int row, 
         split2x2(im[2 * h], im[2 * h + 1], b0, b1);
         q[0][h] = a0; q[1][h] = a1; q[2][h] = b0; q[3][h] = b1;
     }
-    const int c = pl_col(row, j0, pl_mask(ldx));
+    const int c = pl_col(pl_opaque(row), j0, pl_mask(ldx));
 #pragma unroll
     for (int f = 0; f < 4; ++f) *reinterpret_cast<u32x4*>(sP + (f * 16 + row) * ldx + c) = q[f];
 }
@@ -315,7 +325,7 @@ __device__ __forceinline__ void h2_store8(unsigned short* sP, int ldx, int row, 
 // x3_store_acc for the h2 planes (values already scaled).
 __device__ __forceinline__ void h2_store_acc(unsigned short* sP, int ldx, int o, const float (&vr)[4],
                                              const float (&vi)[4]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = pl_opaque((int)threadIdx.x) & 63;
     const bool odd = (lane & 1) != 0;
     float gr[2], gi[2];
 #pragma unroll
@@ -364,8 +374,9 @@ __device__ __forceinline__ void gemm_h2(const unsigned short* sP, int ldx, const
                 ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 4 + f) * 1024, 0);
     // A fragment of group g: row lane & 15, chunk 4 g + (lane >> 4), permuted (pl_col): element
     // 8 ((4 g + q) ^ sw) = ((32 g) ^ s32) + 8 (q ^ (sw & 3)), s32 = 32 (sw >> 2) (one v_xad per g)
-    const int sw = (lane & 15) & pl_mask(ldx);
-    const unsigned short* ap = sP + (lane & 15) * ldx + 8 * ((lane >> 4) ^ (sw & 3));
+    const int ln = pl_opaque(lane);
+    const int sw = (ln & 15) & pl_mask(ldx);
+    const unsigned short* ap = sP + (ln & 15) * ldx + 8 * ((ln >> 4) ^ (sw & 3));
     const int s32 = 32 * (sw >> 2);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
     u32x4 an[4];

@@ -398,12 +398,31 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         __syncthreads();
         stamp(t, 5);
         unsigned nc = 0;
-        for (int b = wave; b < nrows * Lin; b += NW) {        // one wavefront per (row, block)
-            const int row = b / Lin, lc = b - row * Lin;
-            const float ps = block_psi(sX + row * ldx, lc, Nt, P.Na);
-            if (lane == 0) {
-                nc += torch_close(ps, psi_prev[b]) ? 0u : 1u;                 // scamp.py:105
-                psi_new[b] = ps;
+        {
+            // psi of every (row, block): groups of GS = min(16, Nt) lanes, 64 / GS blocks per wave
+            // pass, each lane summing every GS-th |x|^2 of its block in float64, then a GS-lane
+            // butterfly (the terms as block_psi forms them; one short reduction per pass instead
+            // of a 64-lane one per block)
+            const int GS = Nt < 16 ? Nt : 16, bpw = 64 / GS, gi = lane / GS, gl = lane - gi * GS;
+            for (int b0 = wave * bpw; b0 < nrows * Lin; b0 += NW * bpw) {   // wave-uniform
+                const int b = b0 + gi;
+                const bool in = b < nrows * Lin;
+                double ssum = 0.0;
+                if (in) {
+                    const int row = b / Lin, lc = b - row * Lin;
+                    const float* xr = sX + row * ldx + 2 * lc * Nt;
+                    for (int m = gl; m < Nt; m += GS) {
+                        const float2 v = *reinterpret_cast<const float2*>(xr + 2 * m);
+                        const float a = (float)sqrt((double)v.x * v.x + (double)v.y * v.y);
+                        ssum += (double)(a * a);
+                    }
+                }
+                for (int off = GS >> 1; off > 0; off >>= 1) ssum += __shfl_xor(ssum, off);
+                if (in && gl == 0) {
+                    const float ps = 1.0f - (float)ssum / (float)P.Na;
+                    nc += torch_close(ps, psi_prev[b]) ? 0u : 1u;             // scamp.py:105
+                    psi_new[b] = ps;
+                }
             }
         }
         pa.notclose += nc;
