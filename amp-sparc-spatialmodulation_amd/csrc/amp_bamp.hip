@@ -816,12 +816,15 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
 // path by the split of its A rows (var, xmmse, 1/u, s) into the plane buffer
 static void bamp_split(const BampK& P, const float* a, int lda, int K, bool cpx, int t, hipStream_t st) {
     const int* stop = &P.iters[t].stopped;
+    // a workgroup per row when four rows per workgroup would leave CUs idle on long rows
+    const int wpr = (P.rows_pad / 4 < 2 * device_cu_count() && K >= 1024) ? 4 : 1;
+    const dim3 grid(P.rows_pad * wpr / 4);
     if (cpx)
-        hipLaunchKernelGGL(h2_split_rows_kernel<true>, dim3(P.rows_pad / 4), dim3(256), 0, st, a, lda, P.B, P.rows_pad,
-                           K, P.ap, P.rexp, stop);
+        hipLaunchKernelGGL(h2_split_rows_kernel<true>, grid, dim3(256), 0, st, a, lda, P.B, P.rows_pad, K, P.ap,
+                           P.rexp, stop, wpr);
     else
-        hipLaunchKernelGGL(h2_split_rows_kernel<false>, dim3(P.rows_pad / 4), dim3(256), 0, st, a, lda, P.B,
-                           P.rows_pad, K, P.ap, P.rexp, stop);
+        hipLaunchKernelGGL(h2_split_rows_kernel<false>, grid, dim3(256), 0, st, a, lda, P.B, P.rows_pad, K, P.ap,
+                           P.rexp, stop, wpr);
 }
 
 static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st) {

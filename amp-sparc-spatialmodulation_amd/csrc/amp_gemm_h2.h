@@ -46,32 +46,43 @@ __host__ __device__ __forceinline__ size_t h2r_index(int o, int j, int f, int J)
 }
 
 // Split rows [0, rows_pad) of a (row stride lda floats; rows >= rows are zero) into fp16 planes
-// planes[f][row][k] (k < K, plane stride rows_pad * K) scaled by 2^rexp[row]: one wavefront per
-// row; complex rows (CPX) hold K interleaved values, real rows K floats.  K % 8 == 0.  `stopped`
-// (optional): the iteration record's stop word, which turns the launch into a no-op.
+// planes[f][row][k] (k < K, plane stride rows_pad * K) scaled by 2^rexp[row]: wpr wavefronts per
+// row (1: four rows per workgroup; 4: a workgroup per row, the long rows of the ISI shape, where
+// one wave per row left half the chip idle), the row max over them through LDS; complex rows
+// (CPX) hold K interleaved values, real rows K floats.  K % 8 == 0.  `stopped` (optional): the
+// iteration record's stop word, which turns the launch into a no-op.
 template <bool CPX>
 __global__ __launch_bounds__(256) void h2_split_rows_kernel(const float* __restrict__ a, int lda, int rows,
                                                             int rows_pad, int K, unsigned short* __restrict__ planes,
-                                                            int* __restrict__ rexp, const int* __restrict__ stopped) {
+                                                            int* __restrict__ rexp, const int* __restrict__ stopped,
+                                                            int wpr) {
+    __shared__ float s_m[4];
     if (stopped && *stopped) return;                     // the detector's loop has stopped (no-op launch)
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows_pad) return;
-    const bool in = row < rows;
-    const float* ar = a + (size_t)row * lda;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int row = blockIdx.x * (4 / wpr) + wave / wpr;
+    const int t = (wave % wpr) * 64 + lane, nt = 64 * wpr;   // this thread within the row's group
+    const bool valid = row < rows_pad;
+    const bool in = valid && row < rows;
+    const float* ar = a + (size_t)(in ? row : 0) * lda;
     constexpr int FPE = CPX ? 2 : 1;                   // floats per element
     float m = 0.f;
     if (in)
-        for (int q = lane; q < K * FPE / 4; q += 64) {
+        for (int q = t; q < K * FPE / 4; q += nt) {
             const float4 v = *reinterpret_cast<const float4*>(ar + 4 * q);
             m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
     m = group_max(m, 64);
+    if (wpr > 1) {                                     // workgroup-uniform
+        if (lane == 0) s_m[wave] = m;
+        __syncthreads();
+        for (int w = 0; w < wpr; ++w) m = fmaxf(m, s_m[(wave / wpr) * wpr + w]);
+    }
+    if (!valid) return;
     const int ex = in ? h2_row_exp(m) : 0;
-    if (lane == 0) rexp[row] = ex;
+    if (t == 0) rexp[row] = ex;
     const size_t ps = (size_t)rows_pad * K;          // plane stride (elements)
     unsigned short* pr = planes + (size_t)row * K;
-    for (int j0 = 8 * lane; j0 < K; j0 += 8 * 64) {   // 8 elements per lane and step
+    for (int j0 = 8 * t; j0 < K; j0 += 8 * nt) {      // 8 elements per thread and step
         float re[8], im[8];
 #pragma unroll
         for (int h = 0; h < 8 / (4 / FPE); ++h) {
