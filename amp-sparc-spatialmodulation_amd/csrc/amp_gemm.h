@@ -37,13 +37,17 @@ constexpr int GKC = 512;      // A chunk staged in LDS
 constexpr int GLDA = GKC + 4; // its row stride (floats): conflict-free ds_read_b128
 constexpr int GRING = 8;      // W groups in flight per wave
 
-template <int BN>
+// KC: the A chunk staged in LDS (GKC; 256 halves the footprint, so four tiles share a CU where
+// the reduction ranges are short: the block-banded ISI operators)
+template <int BN, int KC = GKC>
 struct GemmCfg {
     static_assert(BN == 128 || BN == 256, "BN must be 128 or 256");
+    static_assert(KC % GBK == 0 && KC <= GKC, "KC");
     static constexpr int NACC = BN / 128;                 // 32x32 accumulators per wave
     static constexpr int WN = BN / 4;                     // columns per wave
     static constexpr int LDC = BN + 4;                    // C tile row stride (floats)
-    static constexpr int A_FLOATS = GBM * GLDA;
+    static constexpr int LDA = KC + 4;                    // A chunk row stride (floats)
+    static constexpr int A_FLOATS = GBM * LDA;
     static constexpr int CTILE_FLOATS = GBM * LDC;
     static constexpr int LDS_FLOATS = A_FLOATS;           // C tile + epilogue scratch fit inside
     static_assert(CTILE_FLOATS + 2048 <= A_FLOATS, "epilogue scratch");
@@ -132,10 +136,11 @@ struct ALoadPlain {
 // every nonzero weight of this column tile (multiples of GBK; weight_kband), default all of it:
 // a block-banded operator (the ISI / spatially coupled channel, channel.py:75-95) skips its
 // all-zero blocks.
-template <int BN, class AL>
+template <int BN, class AL, int KC = GKC>
 __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict__ wp, int kap, int row0,
                                           int col0, float* lds, int kb = 0, int ke = -1) {
-    using C = GemmCfg<BN>;
+    using C = GemmCfg<BN, KC>;
+    constexpr int LDA = C::LDA;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, lh = lane >> 5;
     const int G = kap >> 3;   // groups of 8 reduction indices
@@ -152,8 +157,8 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         wcol[j] = reinterpret_cast<const float4*>(wp) + ((size_t)((col0 >> 5) + wave * C::NACC + j) * G) * 64 + lane;
 
     if (ke < 0) ke = kap;
-    for (int kc0 = kb; kc0 < ke; kc0 += GKC) {
-        const int kc = min(GKC, ke - kc0);
+    for (int kc0 = kb; kc0 < ke; kc0 += KC) {
+        const int kc = min(KC, ke - kc0);
         const int q4 = kc >> 2;   // float4 per A row in this chunk
         const int g0 = kc0 >> 3, gc = kc >> 3;   // gc % GRING == 0 (kap % 64 == 0)
         // W ring first: its latency overlaps the A staging
@@ -165,7 +170,7 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         if (kc0 > kb) __syncthreads();   // every wave is done with the previous chunk
         // stage A[row0 .. row0+32) x [kc0, kc0+kc) (the loader forms fused prologues): all loads
         // of a half-batch in flight before its LDS stores
-        constexpr int PER = GBM * (GKC / 4) / AMP_WG;   // float4 per thread for a full chunk
+        constexpr int PER = GBM * (KC / 4) / AMP_WG;    // float4 per thread for a full chunk
         const int nq = GBM * q4;
 #pragma unroll
         for (int h = 0; h < PER; h += PER / 2) {
@@ -180,14 +185,14 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
             for (int i = 0; i < PER / 2; ++i) {
                 const int e = tid + (h + i) * AMP_WG;
                 const int row = e / q4, k4 = e - row * q4;
-                if (e < nq) *reinterpret_cast<float4*>(lds + row * GLDA + 4 * k4) = t4[i];
+                if (e < nq) *reinterpret_cast<float4*>(lds + row * LDA + 4 * k4) = t4[i];
             }
         }
         __syncthreads();
         // Per group: read the NEXT group's A fragment, issue this group's MFMAs, then refill this
         // ring slot GRING groups ahead.  The scheduling barrier pins that order (left alone, the
         // scheduler sinks all refills behind the MFMAs and drains them at once).
-        const float* a_s = lds + li * GLDA + 4 * lh;
+        const float* a_s = lds + li * LDA + 4 * lh;
         float4 acur = *reinterpret_cast<const float4*>(a_s);
         for (int gb = 0; gb < gc; gb += GRING) {
 #pragma unroll

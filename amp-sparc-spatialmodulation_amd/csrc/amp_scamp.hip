@@ -18,6 +18,7 @@
 namespace amp {
 
 // z = y - A xmmse + b z ; phi = sigma2 + gamma ; s = z / phi   (scamp.py:45-51, 57)
+template <int KC>
 __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -25,8 +26,8 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandA ? P.bandA[2 * tile.cb] : 0, ke = P.bandA ? P.bandA[2 * tile.cb + 1] : -1;
-    gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
-    using C = GemmCfg<128>;
+    gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
+    using C = GemmCfg<128, KC>;
     const float* psi = spsi(P, t + 1);               // psi of iteration t-1 (ones at t = 0)
     const float* phi_old = sphi(P, t + 1);           // +inf at t = 0 (scamp.py:19)
     float* phi_new = sphi(P, t);
@@ -104,16 +105,16 @@ struct ScampDenoisePolicy {
 };
 
 // tau = L / (W^T (1/phi)) / Mr ; xmap = xmmse + tau (A^H s) ; xmmse = denoiser ; psi   (scamp.py:53-59)
-template <int BN, int KK>
+template <int BN, int KK, int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    using C = GemmCfg<BN>;
+    using C = GemmCfg<BN, KC>;
     const GemmTile tile = xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandB ? P.bandB[2 * tile.cb] : 0, ke = P.bandB ? P.bandB[2 * tile.cb + 1] : -1;
-    gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
+    gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     const int lc0 = (col0 / 2) / P.Nt, nlc = max(1, (ncols / 2) / P.Nt);   // coupling blocks in this tile
     // tau of the blocks this tile covers only (blocks lc0 .. lc0 + ntc - 1): each is written to
@@ -537,12 +538,35 @@ static int scamp_kb_attrs() {
     return rc ? rc : set_lds_attr<256>((const void*)scamp_kb<256, KK>);
 }
 
+// Block-banded A (the ISI operators): every tile reduces over a few coupling blocks only, so the
+// 256-wide A chunk (half the LDS: four tiles per CU instead of two) costs no extra chunks there.
+// AMP_SCAMP_KC=512 keeps the 512-wide chunk (A/B runs).
+constexpr size_t SKC_LDS = GemmCfg<128, 256>::LDS_BYTES;   // the short-chunk tiles' LDS
+
+static bool scamp_short_chunks(const ScampK& P) {
+    static const bool off = [] {
+        const char* e = getenv("AMP_SCAMP_KC");
+        return e && atoi(e) == 512;
+    }();
+    return P.bandA != nullptr && !off;
+}
+
 template <int KK>
 static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
-    if (P.bn == 128)
+    if (P.bn == 128 && scamp_short_chunks(P))
+        hipLaunchKernelGGL((scamp_kb<128, KK, 256>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SKC_LDS,
+                           st, P, t);
+    else if (P.bn == 128)
         hipLaunchKernelGGL((scamp_kb<128, KK>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), ldsB, st, P, t);
     else
         hipLaunchKernelGGL((scamp_kb<256, KK>), dim3(gr, P.ncpB / 256), dim3(AMP_WG), ldsB, st, P, t);
+}
+
+static void launch_ka(const ScampK& P, int gr, int t, hipStream_t st) {
+    if (scamp_short_chunks(P))
+        hipLaunchKernelGGL(scamp_ka<256>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), SKC_LDS, st, P, t);
+    else
+        hipLaunchKernelGGL(scamp_ka<GKC>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
 }
 
 static void launch_kb(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
@@ -558,7 +582,7 @@ static void launch_kb(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t s
 
 static int scamp_attrs() {
     std::call_once(g_scamp_once, [] {
-        g_scamp_rc = set_lds_attr<128>((const void*)scamp_ka);
+        g_scamp_rc = set_lds_attr<128>((const void*)scamp_ka<GKC>);
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<1>();
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<2>();
         if (!g_scamp_rc) g_scamp_rc = scamp_kb_attrs<4>();
@@ -706,7 +730,7 @@ static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStr
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     // fix-up grid: one slot per block in iteration t's partials (consumed by then)
     const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
-    hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_ka(P, gr, t, st);
     launch_kb(P, gr, ldsB, t, st);
     if (P.psi_split)
         hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
@@ -722,7 +746,7 @@ static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hip
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
-    hipLaunchKernelGGL(scamp_ka, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
+    launch_ka(P, gr, t, st);
     launch_kb(P, gr, ldsB, t, st);
     if (P.psi_split) hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
     hipLaunchKernelGGL(scamp_sxr1, dim3(1), dim3(SRWG), 0, st, P, t);
