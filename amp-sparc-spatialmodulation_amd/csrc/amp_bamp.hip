@@ -743,17 +743,19 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.elementwise = a->denoiser;
     P.P0 = a->P0;
     P.Ps = a->Ps;
-    // GEMM arithmetic: fp16x2 (AUTO where the shape tiles, AMP_BAMP_GEMM=f32 keeps f32) or f32 MFMA
+    // GEMM arithmetic: f32 MFMA (AUTO: the reference's c64 operand precision, bamp.py:59-64) or,
+    // only when asked for (AMP_GEMM_H2, or AUTO with AMP_BAMP_GEMM=h2), the fp16x2 tile (22-bit
+    // operands: narrower than the reference)
     AMP_REQUIRE(a->gemm == AMP_GEMM_AUTO || a->gemm == AMP_GEMM_F32 || a->gemm == AMP_GEMM_H2,
                 "amp_bamp_run: gemm %d (AUTO, F32 or H2)", a->gemm);
     const bool h2ok = bamp_h2_shape(d);
     AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || h2ok, "amp_bamp_run: the fp16x2 GEMMs need N %% 64 == 0 and n %% 64 == 0 "
                 "(N = %d, n = %d)", d->N, d->n);
-    static const bool f32_env = [] {
+    static const bool h2_env = [] {
         const char* e = getenv("AMP_BAMP_GEMM");
-        return e && e[0] == 'f';
+        return e && e[0] == 'h';
     }();
-    P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && !f32_env)) ? 1 : 0;
+    P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && h2_env)) ? 1 : 0;
     P.rows_pad = round_up(d->B, GBM);
     P.ap = w.ap;
     P.rexp = w.rexp;

@@ -406,23 +406,26 @@ bool gemm_f32_requested() {
     return v;
 }
 
-// AMP_VAMP_GEMM=x3 keeps the bf16x3 form where AUTO would pick fp16x2 (A/B runs)
-static bool gemm_x3_requested() {
+// AMP_VAMP_GEMM=h2 makes AUTO pick the fp16x2 form (A/B runs only: 22-bit operands)
+static bool gemm_h2_requested() {
     static const bool v = [] {
         const char* e = getenv("AMP_VAMP_GEMM");
-        return e && e[0] == 'x';
+        return e && e[0] == 'h';
     }();
     return v;
 }
 
 // The persistent engine's GEMM arithmetic for a shape whose planes fit (amp_vamp_args.gemm):
-// 0 f32 MFMA, 1 bf16x3, 2 fp16x2.  AUTO: fp16x2 (the fastest, f32-level accuracy), unless the
-// environment asks for f32 or bf16x3.
+// 0 f32 MFMA, 1 bf16x3, 2 fp16x2.  AUTO: bf16x3 — the fastest form whose operands keep all 24
+// bits of an f32 (three 8-bit pieces) and whose dropped product terms are < 2^-24 relative, i.e.
+// the reference's c64 operand precision (vamp.py:67, 72).  fp16x2 (two 11-bit pieces, 22 bits,
+// the 2^-22 lo.lo term dropped) is narrower than the reference and runs only when asked for
+// (AMP_GEMM_H2 or AMP_VAMP_GEMM=h2).
 static int vamp_gemm_mode(int gemm, bool fits) {
     if (gemm == AMP_GEMM_H2) return 2;
     if (gemm == AMP_GEMM_X3) return 1;
     if (gemm == AMP_GEMM_F32 || !fits || gemm_f32_requested()) return 0;
-    return gemm_x3_requested() ? 1 : 2;
+    return gemm_h2_requested() ? 2 : 1;
 }
 
 static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64) {

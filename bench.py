@@ -94,22 +94,28 @@ def cpu_baseline(cfgname, EbN0, seed, sample_trials, repeats=3):
                 port_over_reference_time=PORT_OVER_REFERENCE)
 
 
-def traffic_from_profile(persistent):
+# The PMC summary (tools/profile.sh -> tools/prof_summary.py) of THIS build's default command, per
+# GEMM arithmetic; `roofline.traffic` names it (`traffic_source`).  The counters cannot be read by
+# the timed run itself (rocprofv3 --pmc replays the launch), so the file is the measurement.
+TRAFFIC_PROFILE = {'bf16x3': 'profiles/r04_cfg4_vamp_x3.txt', 'fp16x2': 'profiles/r03_cfg4_vamp_swz.txt'}
+
+
+def traffic_from_profile(persistent, gname):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary of the same
-    command (tools/profile.sh -> tools/prof_summary.py -> profiles/): FETCH_SIZE x 2 (gfx950
-    tallies 128-B requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE.  None when absent."""
-    import glob
+    command: FETCH_SIZE x 2 (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md) +
+    WRITE_SIZE.  Returns (bytes or None, the profile file it came from or None)."""
     import re
     name = 'amp::vamp_persist' if persistent else 'amp::vamp_k2'
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_cfg4_vamp*.txt')))
-    for f in reversed(files):
-        for line in open(f):
-            if line.startswith(name) and 'FETCH_SIZE' in line and 'WRITE_SIZE' in line:
-                fe = re.search(r'FETCH_SIZE=(\d+)KB', line)
-                wr = re.search(r'WRITE_SIZE=(\d+)KB', line)
-                if fe and wr:
-                    return (2 * int(fe.group(1)) + int(wr.group(1))) * 1024
-    return None
+    rel = TRAFFIC_PROFILE.get(gname) if persistent else None
+    if not rel or not os.path.exists(os.path.join(REPO, rel)):
+        return None, None
+    for line in open(os.path.join(REPO, rel)):
+        if line.startswith(name) and 'FETCH_SIZE' in line and 'WRITE_SIZE' in line:
+            fe = re.search(r'FETCH_SIZE=(\d+)KB', line)
+            wr = re.search(r'WRITE_SIZE=(\d+)KB', line)
+            if fe and wr:
+                return (2 * int(fe.group(1)) + int(wr.group(1))) * 1024, rel
+    return None, None
 
 
 def timed_epochs(step, counts_of, steps, warmup, merge, sync=lambda: None, barrier=lambda: None,
@@ -189,6 +195,10 @@ def main():
     ap.add_argument('--cpu-sample', type=int, default=4096)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--engine', default='auto', choices=['auto', 'launches', 'persistent'])
+    # the persistent engine's GEMM arithmetic: auto = bf16x3 (three bf16 pieces per f32 operand,
+    # 24 bits, dropped product terms < 2^-24: the reference's c64 operand precision); h2 = the
+    # opt-in fp16x2 form (22-bit operands, narrower than the reference: a second, labelled line)
+    ap.add_argument('--gemm', default='auto', choices=['auto', 'x3', 'f32', 'h2'])
     # independent epochs per rank (weak scaling, the default) or ONE batch of B trials split over
     # the ranks (strong scaling: ShardedVAMP, the batch scalars all-reduced every iteration)
     ap.add_argument('--shard', default='epochs', choices=['epochs', 'trials'])
@@ -226,7 +236,8 @@ def main():
     # and noise: seed + rank); trials: every rank draws the SAME epoch and detects its slice
     inp = make_inputs(cfg, args.seed + (0 if trials else rank), args.ebn0, device)
     engine = {'auto': nat.ENGINE_AUTO, 'launches': nat.ENGINE_LAUNCHES, 'persistent': nat.ENGINE_PERSISTENT}[args.engine]
-    det = ShardedVAMP(cfg) if trials else VAMP(cfg, engine=engine)
+    gemm = {'auto': nat.GEMM_AUTO, 'x3': nat.GEMM_X3, 'f32': nat.GEMM_F32, 'h2': nat.GEMM_H2}[args.gemm]
+    det = ShardedVAMP(cfg) if trials else VAMP(cfg, engine=engine, gemm=gemm)
     seq = [0]
 
     def step():
@@ -280,6 +291,12 @@ def main():
     flops_mv = 8.0 * Bp * N * k                    # complex [N x k] . [k] per trial = 8 real flop / CMAC
     gmode = nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) if persistent else nat.GEMM_F32
     gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2'}.get(gmode, 'f32')
+    arith = {'bf16x3': 'GEMMs: every f32 operand split into three bf16 pieces (24 significant bits), six '
+                       'products per f32 product (dropped terms < 2^-24 relative), f32 accumulation on '
+                       'v_mfma_f32_16x16x32_bf16; denoiser f32, scalars f32/f64 as the reference',
+             'fp16x2': 'OPT-IN, narrower than the reference: GEMM operands split into two fp16 pieces (22 '
+                       'significant bits), the 2^-22 lo.lo term dropped, f32 accumulation',
+             'f32': 'GEMMs on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32)'}[gname]
     # the fp16x2 engine forms y~ = (s Uh) y in its prologue when n == 2N (amp_vamp.hip): those
     # 8 B n k flops per trial belong to the launch then
     ytil_in = persistent and gname == 'fp16x2' and Nr == 2 * Nt and os.environ.get('AMP_YTIL_IN_KERNEL') != '0'
@@ -291,6 +308,7 @@ def main():
         kern, flops_launch = 'vamp_k2 (GEMM2 + Onsager update + section denoiser)', flops_mv
         kms = {'gemm1': ms[0], 'gemm2_denoise': ms[1], 'reduce': ms[2], 'forward': ms[3]}
     achieved = flops_launch / (ms[1] * 1e-3) / 1e12
+    traffic, traffic_src = traffic_from_profile(persistent, gname)
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -308,7 +326,7 @@ def main():
         'metric': 'detected symbol-vectors/sec, VAMP Nt=256 Nr=512 16-QAM; SER match vs ref',
         'value': value, 'unit': 'symbol-vectors/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': ms_step, 'higher_is_better': True, 'scaling': 'strong' if trials else 'weak',
-        'vs_baseline': None, 'dtype': 'f32',
+        'vs_baseline': None, 'dtype': gname,
         'data': 'synthetic (reference generators replayed: sparc channel, segmented 16-QAM messages, AWGN)',
         'config': {'workload': f'{args.config}: VAMP Nt={Nt} Nr={Nr} Na={Na} {alph} batch={B} iterations<={iters} '
                                f'EbN0={args.ebn0} dB, one channel per batch',
@@ -316,10 +334,12 @@ def main():
         'detail': {'T': T, 'ver': ver, 'ser': ser, 'epochs': n_epochs,
                    'trial_iterations_per_s': gb * T / (el / args.steps),
                    'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms,
+                   'arithmetic': arith,
                    'prewarm': {'ms': args.prewarm_ms, 'steps': npre,
                                'why': 'untimed steps before --warmup: the clocks ramp over the first ~25 ms'}},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic_from_profile(persistent),
+                     'frac': achieved / FP32_MFMA_PEAK_TFLOPS, 'traffic': traffic,
+                     'traffic_source': traffic_src,
                      'kernel': kern, 'flop_per_launch': flops_launch,
                      'gemm': gname},
     }

@@ -13,11 +13,12 @@ from test_gpu_vamp import _check_T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('gemm', ['auto', 'f32'])
+@pytest.mark.parametrize('gemm', ['auto', 'h2'])
 @pytest.mark.parametrize('name,key', g6_points())
 def test_cfg5_correlated_curve_point(device, name, key, gemm):
-    """Both GEMM arithmetics of BAMP's launch engine: 'auto' is the fp16x2 tile GEMM at this
-    shape (amp_gemm_h2.h), 'f32' the exact-f32 MFMA one."""
+    """Both GEMM arithmetics of BAMP's launch engine: 'auto' is the exact-f32 MFMA GEMM (the
+    reference's operand precision), 'h2' the opt-in fp16x2 tile GEMM (amp_gemm_h2.h, 22-bit
+    operands)."""
     import amp_native as nat
     from bamp import BAMP
     ent = g6_curves()[name]
@@ -28,7 +29,7 @@ def test_cfg5_correlated_curve_point(device, name, key, gemm):
     if 'SNR' in ref:
         assert inp['SNR'] == pytest.approx(ref['SNR'], rel=1e-12)
     mv = lambda t: t.to(device)  # noqa: E731
-    L = BAMP(cfg, gemm=nat.GEMM_AUTO if gemm == 'auto' else nat.GEMM_F32)(mv(inp['A']), mv(inp['y']), inp['SNR'],
+    L = BAMP(cfg, gemm=nat.GEMM_AUTO if gemm == 'auto' else nat.GEMM_H2)(mv(inp['A']), mv(inp['y']), inp['SNR'],
                                                                         mv(inp['x']), inp['sym'], inp['idx'])
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])

@@ -214,9 +214,9 @@ VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk'
 
 
 ENGINES = {'launches': 1, 'persistent': 2}   # amp_native.ENGINE_*
-# (engine, persistent GEMM arithmetic): 'persistent' = the product default (fp16x2 where it fits),
-# 'persistent-x3' the bf16x3 form, 'persistent-f32' the f32-MFMA form
-VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 'persistent-x3': (2, 2)}
+# (engine, persistent GEMM arithmetic): 'persistent' = the product default (bf16x3 where it fits:
+# 24-bit operands), 'persistent-f32' the f32-MFMA form, 'persistent-h2' the opt-in fp16x2 form
+VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 'persistent-h2': (2, 3)}
 
 
 @pytest.mark.parametrize('variant', sorted(VARIANTS))
@@ -224,7 +224,7 @@ VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 
 def test_vamp_curve_point(device, name, key, variant):
     """VER / SER within 1e-3 of the reference at the same seed and EbN0 (north-star bar),
     for both engines of amp_vamp_run (cfg2 and cfg4 are both persistent-eligible) and the three
-    GEMM arithmetics of the persistent engine (split fp16x2, the default; split bf16x3; f32 MFMA)."""
+    GEMM arithmetics of the persistent engine (split bf16x3, the default; f32 MFMA; opt-in fp16x2)."""
     from vamp import VAMP
     ent = CURVES[name]
     ref = ent['points'][key]
@@ -282,7 +282,7 @@ def test_vamp_x3_gemm_matches_f32(device, name, iters):
     inp = _regen_inputs(cfg, 0, 8.0)
     assert nat.lib().amp_vamp_select_engine(cfg.dims(), ent['Nt'], nat.ENGINE_AUTO) == nat.ENGINE_PERSISTENT
     r = {}
-    assert nat.lib().amp_vamp_select_gemm(cfg.dims(), ent['Nt'], nat.GEMM_AUTO) == nat.GEMM_H2
+    assert nat.lib().amp_vamp_select_gemm(cfg.dims(), ent['Nt'], nat.GEMM_AUTO) == nat.GEMM_X3
     for gemm in (nat.GEMM_F32, nat.GEMM_X3, nat.GEMM_H2):
         T = VAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm).detect(inp['U'], inp['s'], inp['Vh'], inp['y'],
                                                                      inp['SNR'])

@@ -1,0 +1,39 @@
+#!/usr/bin/env bash
+# Round-4 GPU session driver (run from the repo root on the box).  STEPS names the steps to run,
+# in order, e.g. STEPS="bench bench_h2 trace tests_vamp".  Each GPU step has its own time limit;
+# any non-zero exit ends the session (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r04}
+mkdir -p "$OUT"
+run() {
+    local name=$1 lim=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"; tail -4 "$OUT/$name.log"
+    if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+PYT="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+for s in ${STEPS:-bench}; do
+    case $s in
+    bench) run bench 300 python3 bench.py ;;
+    bench_nocpu) run bench_nocpu 300 python3 bench.py --no-cpu-baseline ;;
+    bench_h2) run bench_h2 300 python3 bench.py --no-cpu-baseline --gemm h2 ;;
+    bench_f32) run bench_f32 300 python3 bench.py --no-cpu-baseline --gemm f32 ;;
+    trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;
+    trace_h2) run trace_h2 300 env AMP_VAMP_GEMM=h2 python3 tools/trace_persist.py --config cfg4 ;;
+    configs) run configs 600 python3 tools/configs_bench.py ;;
+    tests_vamp) run tests_vamp 900 $PYT tests/test_gpu_vamp.py -m gpu ;;
+    tests_epochs) run tests_epochs 600 $PYT tests/test_gpu_epochs.py -m gpu ;;
+    tests_cfg5) run tests_cfg5 900 $PYT tests/test_gpu_cfg5.py -m gpu ;;
+    tests_bs) run tests_bs 900 $PYT tests/test_gpu_bamp_scamp.py -m gpu ;;
+    tests) run tests 1100 $PYT tests -m gpu ;;
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    profile) run profile 900 bash tools/profile.sh ;;
+    ubench) run ubench 300 bash tools/ubench/run.sh ;;
+    *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "=== done"
