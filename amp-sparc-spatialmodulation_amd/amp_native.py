@@ -106,6 +106,7 @@ SIGNATURES = {
     'amp_vamp_debug_offsets': (C.c_int, [_D, _I, _I, _I, C.POINTER(C.c_uint64)]),
     'amp_vamp_debug_dump': (C.c_int, [_P]),
     'amp_vamp_max_epochs': (C.c_int, [_D, _I]),
+    'amp_vamp_max_epochs_gemm': (C.c_int, [_D, _I, _I]),
     'amp_set_allreduce_hook': (C.c_int, [_P, _P]),
     'amp_vamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
     'amp_bamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _I, _P]),

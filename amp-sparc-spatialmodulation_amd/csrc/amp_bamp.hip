@@ -70,8 +70,10 @@ struct BampK {
     int* rexp;             // [rows_pad] row exponents
 };
 
-// BAMP's fp16x2 operator scale exponent: |H|^2 and |H| below 64 (the channel's entries are
-// ~CN(0, 1/Nr)); larger entries overflow their fp16 piece, so the result is non-finite
+// BAMP's fp16x2 operator scale exponent (the opt-in AMP_GEMM_H2 form): every operator piece is
+// scaled by 2^10, so |H|^2 must stay below 64 (|H| < 8; the channel's entries are ~CN(0, 1/Nr));
+// larger entries overflow their fp16 piece, the result is then non-finite (NaN detections,
+// counted as errors), never silently wrong
 constexpr int BH2_EX = 10;
 
 // the fp16x2 GEMMs need whole 64-wide reduction groups and output tiles (a block-banded H reduces

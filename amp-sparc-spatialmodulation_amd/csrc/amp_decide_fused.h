@@ -13,20 +13,27 @@ namespace amp {
 // this workgroup's rows while the decision input (VAMP: r, vamp.py:187; SCAMP: xmap,
 // scamp.py:107) and xmmse are still in LDS (sR / sX, row stride ldr);
 // per-workgroup records, folded by the last workgroup to finish (threadfence reduction).
-// mism: >= nrows * L bytes of free LDS; scr: >= 16 * sizeof(DecWG) bytes.
+// lab_lds: lab_cap bytes of free LDS (at least nrows * L for the mismatch flags; the labels are
+// staged there too when 17 nrows L bytes fit, else read from global memory in the decision loop);
+// scr: >= 16 * sizeof(DecWG) bytes.
 // row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
 // (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
 template <int PWG, int KK, class PK>
 __device__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
-                                int lrow0, int nrows, float* sT, void* lab_lds, void* scr) {
+                                int lrow0, int nrows, float* sT, void* lab_lds, int lab_cap, void* scr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int M = P.M, L = P.L, N = P.N;
     const int S = nrows * L;
     // one coalesced bulk load of this workgroup's truth rows and labels into LDS (a per-section
-    // global load inside the decision loop left every round waiting on HBM latency)
+    // global load inside the decision loop left every round waiting on HBM latency); labels that
+    // do not fit the free region (17 bytes per section: small M, many sections per row) stay in
+    // global memory
+    const bool stage = 17 * S <= lab_cap;   // workgroup-uniform
     long long* lsym = reinterpret_cast<long long*>(lab_lds);
     long long* lidx = lsym + S;
-    unsigned char* mism = reinterpret_cast<unsigned char*>(lidx + S);
+    unsigned char* mism = stage ? reinterpret_cast<unsigned char*>(lidx + S) : reinterpret_cast<unsigned char*>(lab_lds);
+    const long long* gsym = P.sym + (size_t)row0 * L;
+    const long long* gidx = P.idx + (size_t)row0 * L;
     {
         // PBM rows of 2N floats = PBM * N / 2 float4: all loads in flight before the LDS stores
         constexpr int CH = 8;
@@ -52,9 +59,11 @@ __device__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR
             }
         }
     }
-    for (int e = tid; e < S; e += PWG) {
-        lsym[e] = P.sym[(size_t)row0 * L + e];
-        lidx[e] = P.idx[(size_t)row0 * L + e];
+    if (stage) {
+        for (int e = tid; e < S; e += PWG) {
+            lsym[e] = gsym[e];
+            lidx[e] = gidx[e];
+        }
     }
     __syncthreads();
     const long long ibmask = dec_ibmask(P.ibits);
@@ -81,7 +90,8 @@ __device__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR
         if (act && g == 0) {
             const long long s = (long long)(lrow0 + row) * L + l;
             mism[lsc] = (unsigned char)mm;
-            count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, lsym[lsc], lidx[lsc], ibmask, q);
+            count_section<KK>(dc, s, M, L, P.Na, P.Lin, bi, se, stage ? lsym[lsc] : gsym[lsc],
+                              stage ? lidx[lsc] : gidx[lsc], ibmask, q);
         }
     }
     __syncthreads();

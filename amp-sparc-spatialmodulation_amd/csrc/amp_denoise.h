@@ -30,6 +30,14 @@ namespace amp {
 
 #define AMP_LOG2E 1.44269504088896340736f
 
+// Which waves of the workgroup share a denoiser call: this wave's index among them and their
+// count (default: every wave of the workgroup).  The wave-specialized engine
+// (amp_vamp_persist_kernel.h, WS) hands half the sections to a subset of its waves.
+struct DenWaves {
+    int wave, nw;
+    __device__ static DenWaves block() { return DenWaves{(int)(threadIdx.x >> 6), (int)(blockDim.x >> 6)}; }
+};
+
 // A uniform kernel-argument value taken through readfirstlane: the loads stay scalar loads of
 // the kernarg segment (left alone, memcpyopt merged consecutive constellation loads into a copy
 // of c.re into a private array, i.e. scratch memory, once Const held 64 points).
@@ -51,11 +59,11 @@ __device__ __forceinline__ float kval(const float& x) {
 // max |logit|, non-finite input) are kept per lane in float32 and folded into the float64
 // PartAcc once at the end.
 template <bool kVar, int KK, int U, int G, class P>
-__device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const Const& c, PartAcc& pa) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
+    const int lane = threadIdx.x & 63, wave = dw.wave;
     constexpr int gpw = 64 / G;
     const int gid = lane / G, g = lane % G;
-    const int nw = blockDim.x >> 6;
+    const int nw = dw.nw;
     float cre[KK], cim[KK];
 #pragma unroll
     for (int k = 0; k < KK; ++k) {
@@ -600,16 +608,16 @@ constexpr int grid_r() { return KK == 4 ? 2 : KK == 16 ? 4 : KK == 64 ? 8 : 0; }
 // The grid loop over this wave's sections; returns false (nothing done) when c is not a grid of
 // the size KK admits.  c.grid / c.gfull are kernel arguments: the branch is uniform.
 template <bool kVar, int KK, int U, int G, bool PKG = true, class P>
-__device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+__device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     constexpr int R = grid_r<KK>();
     if constexpr (R == 0) {
         return false;
     } else {
         const int grid = __builtin_amdgcn_readfirstlane(c.grid), gfull = __builtin_amdgcn_readfirstlane(c.gfull);
         if (grid != R) return false;
-        const int wave = threadIdx.x >> 6;
+        const int wave = dw.wave;
         constexpr int gpw = 64 / G;
-        const int nw = blockDim.x >> 6;
+        const int nw = dw.nw;
         DenStat S;
         GridRegs<R> Q;
         Q.load(c);
@@ -634,11 +642,11 @@ __device__ __forceinline__ bool denoise_sections_grid(const P& pol, int nsec, co
 }
 
 template <bool kVar, int KK, int U, int G, class P>
-__device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa) {
-    if (denoise_sections_grid<kVar, KK, U, G>(pol, nsec, c, pa)) return;
-    const int wave = threadIdx.x >> 6;
+__device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
+    if (denoise_sections_grid<kVar, KK, U, G>(pol, nsec, c, pa, dw)) return;
+    const int wave = dw.wave;
     constexpr int gpw = 64 / G;
-    const int nw = blockDim.x >> 6;
+    const int nw = dw.nw;
     DenRegs<KK> R;
     R.load(c);
     DenStat S;
@@ -654,24 +662,24 @@ __device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, cons
 // in lanes 48-63 now and then (results not reproducible run to run; the scalar
 // form was bit-identical in every run).
 template <bool kVar, int KK, int U, int G, bool PK, class P>
-__device__ __forceinline__ void denoise_sections_sel(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+__device__ __forceinline__ void denoise_sections_sel(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     if constexpr (PK && KK % 2 == 0) {
-        denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa);
+        denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa, dw);
     } else {
-        if (denoise_sections_grid<kVar, KK, U, G, false>(pol, nsec, c, pa)) return;
-        denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa);
+        if (denoise_sections_grid<kVar, KK, U, G, false>(pol, nsec, c, pa, dw)) return;
+        denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa, dw);
     }
 }
 template <bool kVar, int KK, int U, bool PK = true, class P>
-__device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+__device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     switch (M) {
-    case 64: denoise_sections_sel<kVar, KK, U, 64, PK>(pol, nsec, c, pa); break;
-    case 32: denoise_sections_sel<kVar, KK, U, 32, PK>(pol, nsec, c, pa); break;
-    case 16: denoise_sections_sel<kVar, KK, U, 16, PK>(pol, nsec, c, pa); break;
-    case 8: denoise_sections_sel<kVar, KK, U, 8, PK>(pol, nsec, c, pa); break;
-    case 4: denoise_sections_sel<kVar, KK, U, 4, PK>(pol, nsec, c, pa); break;
-    case 2: denoise_sections_sel<kVar, KK, U, 2, PK>(pol, nsec, c, pa); break;
-    default: denoise_sections_sel<kVar, KK, U, 1, PK>(pol, nsec, c, pa); break;
+    case 64: denoise_sections_sel<kVar, KK, U, 64, PK>(pol, nsec, c, pa, dw); break;
+    case 32: denoise_sections_sel<kVar, KK, U, 32, PK>(pol, nsec, c, pa, dw); break;
+    case 16: denoise_sections_sel<kVar, KK, U, 16, PK>(pol, nsec, c, pa, dw); break;
+    case 8: denoise_sections_sel<kVar, KK, U, 8, PK>(pol, nsec, c, pa, dw); break;
+    case 4: denoise_sections_sel<kVar, KK, U, 4, PK>(pol, nsec, c, pa, dw); break;
+    case 2: denoise_sections_sel<kVar, KK, U, 2, PK>(pol, nsec, c, pa, dw); break;
+    default: denoise_sections_sel<kVar, KK, U, 1, PK>(pol, nsec, c, pa, dw); break;
     }
 }
 
@@ -683,13 +691,13 @@ __device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M
 // per position instead of 64, against 5 GEMM launches per iteration at cfg5).
 // One position per lane (G = M <= 64 lanes per section).
 template <bool kVar, int KK, int G, class P>
-__device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, const Const& c, PartAcc& pa) {
+__device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     static_assert(KK % 8 == 0, "chunks of 8 points");
-    if (denoise_sections_grid<kVar, KK, 1, G>(pol, nsec, c, pa)) return;   // square 64-QAM
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (denoise_sections_grid<kVar, KK, 1, G>(pol, nsec, c, pa, dw)) return;   // square 64-QAM
+    const int lane = threadIdx.x & 63, wave = dw.wave;
     constexpr int gpw = 64 / G;
     const int gid = lane / G, g = lane % G;
-    const int nw = blockDim.x >> 6;
+    const int nw = dw.nw;
     // the table in LDS: the rolled loops below index it at runtime, which on the by-value kernel
     // argument made the compiler copy the whole Const into scratch memory at every kernel entry
     __shared__ float s_cre[KK], s_cim[KK];
@@ -760,15 +768,15 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
 }
 
 template <bool kVar, int KK, class P>
-__device__ __forceinline__ void denoise_sections_wide_m(const P& pol, int nsec, int M, const Const& c, PartAcc& pa) {
+__device__ __forceinline__ void denoise_sections_wide_m(const P& pol, int nsec, int M, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     switch (M) {
-    case 64: denoise_sections_wide<kVar, KK, 64>(pol, nsec, c, pa); break;
-    case 32: denoise_sections_wide<kVar, KK, 32>(pol, nsec, c, pa); break;
-    case 16: denoise_sections_wide<kVar, KK, 16>(pol, nsec, c, pa); break;
-    case 8: denoise_sections_wide<kVar, KK, 8>(pol, nsec, c, pa); break;
-    case 4: denoise_sections_wide<kVar, KK, 4>(pol, nsec, c, pa); break;
-    case 2: denoise_sections_wide<kVar, KK, 2>(pol, nsec, c, pa); break;
-    default: denoise_sections_wide<kVar, KK, 1>(pol, nsec, c, pa); break;
+    case 64: denoise_sections_wide<kVar, KK, 64>(pol, nsec, c, pa, dw); break;
+    case 32: denoise_sections_wide<kVar, KK, 32>(pol, nsec, c, pa, dw); break;
+    case 16: denoise_sections_wide<kVar, KK, 16>(pol, nsec, c, pa, dw); break;
+    case 8: denoise_sections_wide<kVar, KK, 8>(pol, nsec, c, pa, dw); break;
+    case 4: denoise_sections_wide<kVar, KK, 4>(pol, nsec, c, pa, dw); break;
+    case 2: denoise_sections_wide<kVar, KK, 2>(pol, nsec, c, pa, dw); break;
+    default: denoise_sections_wide<kVar, KK, 1>(pol, nsec, c, pa, dw); break;
     }
 }
 

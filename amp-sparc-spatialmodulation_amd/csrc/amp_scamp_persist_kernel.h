@@ -548,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         // fused MAP decision + counters on xmap (scamp.py:107 -> loss.py:67-179): the s / plane region
         // holds the truth rows (n >= N: rows of ldx floats fit), the z region the labels
         __syncthreads();
-        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldx, row0, row0, nrows, sS, sZ, scr);
+        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldx, row0, row0, nrows, sS, sZ, 4 * SPB * Y.ldz, scr);
     }
 }
 

@@ -66,6 +66,22 @@ bool vamp_persist_ytil_h2(const VampK& P) {
     return P.n == 2 * P.N && P.k == P.N && 2 * PBM * pl_ldx(P.n) <= playout(P.N, P.k, P.L, true).offV0;
 }
 
+// the bf16x3 y~ prologue: n == 2N and the six y planes (16 rows x n bf16) within the A / R / X
+// region of the split-precision carve
+bool vamp_persist_ytil_x3(const VampK& P) {
+    return P.n == 2 * P.N && P.k == P.N && 3 * PBM * pl_ldx(P.n) <= playout(P.N, P.k, P.L, true).offV0;
+}
+
+// The f32-streamed bf16x3 form (x3 = 3): eight waves, N = 128 or 256 (whole complex tiles per
+// wave); AMP_VAMP_X3F=0 keeps the pre-split bf16x3 operators (A/B runs).
+bool vamp_persist_x3f_ok(int N) {
+    static const bool off = [] {
+        const char* e = getenv("AMP_VAMP_X3F");
+        return e && e[0] == '0';
+    }();
+    return !off && (N == 128 || N == 256);
+}
+
 bool vamp_persist_x3_fits(int N, int k, int L) {
     return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
 }
@@ -84,27 +100,33 @@ bool persist_wg2() {
     }();
     return v;
 }
-static int persist_wg_cap(int N) { return (N == 64 && persist_wg2()) ? 2 : 1; }
+// gemm_mode: the persistent GEMM arithmetic of the call (vamp_gemm_select: 0 f32, 1 bf16x3,
+// 2 fp16x2); only the split-precision engines have a two-per-CU instantiation
+static int persist_wg_cap(int N, int gemm_mode) { return (N == 64 && gemm_mode != 0 && persist_wg2()) ? 2 : 1; }
 
-int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu) {
+int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu, int gemm) {
+    const int gemm_mode = vamp_gemm_select(d, k, gemm);
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return 0;
     if ((size_t)playout(d->N, k, d->L).total * 4 + 2048 > 160 * 1024) return 0;
     const int wpe = cdiv(d->B, PBM);
     if (wpe > ncu) return 0;
     if (d->B % PBM != 0) return 1;
-    return std::max(1, persist_wg_cap(d->N) * ncu / wpe);
+    return std::max(1, persist_wg_cap(d->N, gemm_mode) * ncu / wpe);
 }
 
-bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs) {
+bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs, int gemm) {
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return false;
     if (epochs < 1 || (epochs > 1 && d->B % PBM != 0)) return false;
-    if (cdiv(d->B, PBM) > ncu || (long)epochs * cdiv(d->B, PBM) > (long)persist_wg_cap(d->N) * ncu) return false;
+    if (cdiv(d->B, PBM) > ncu ||
+        (long)epochs * cdiv(d->B, PBM) > (long)persist_wg_cap(d->N, vamp_gemm_select(d, k, gemm)) * ncu)
+        return false;
     return (size_t)playout(d->N, k, d->L).total * 4 + 2048 <= 160 * 1024;
 }
 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_x3.hip
 int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_h2.hip
+int persist_dispatch_x3f(const VampK& P, const DecConst& dc, hipStream_t st);  // amp_vamp_persist_x3f.hip
 
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
@@ -123,21 +145,13 @@ static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) 
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
     if (P.x3 == 2) return persist_dispatch_h2(P, dc, st);
+    if (P.x3 == 3) return persist_dispatch_x3f(P, dc, st);
     if (P.x3) return persist_dispatch_x3(P, dc, st);
-    if (persist_waves() == 4) {
-        switch (P.N) {
-        case 64: return persist_launch_nt<2, 4, false>(P, dc, st);
-        case 128: return persist_launch_nt<4, 4, false>(P, dc, st);
-        case 256: return persist_launch_nt<8, 4, false>(P, dc, st);
-        default: break;
-        }
-    } else {
-        switch (P.N) {
-        case 64: return persist_launch_nt<1, 8, false>(P, dc, st);
-        case 128: return persist_launch_nt<2, 8, false>(P, dc, st);
-        case 256: return persist_launch_nt<4, 8, false>(P, dc, st);
-        default: break;
-        }
+    switch (P.N) {
+    case 64: return persist_launch_nt<2, 4, false>(P, dc, st);
+    case 128: return persist_launch_nt<4, 4, false>(P, dc, st);
+    case 256: return persist_launch_nt<8, 4, false>(P, dc, st);
+    default: break;
     }
     set_error("vamp_persist: N = %d not supported", P.N);
     return AMP_E_ARG;

@@ -188,7 +188,10 @@ class LazyResult:
         bounded; the grid drains and the results are invalid).  `rescue()` then re-runs that
         forward on the launch engine in this process (no exec, no co-residency needed) and
         returns its (status, counts); the event is counted in self.grid_rescues.  Without a
-        rescue (or if it fails too) the resolve raises."""
+        rescue (or if it fails too) the resolve raises.  The rescue re-reads the forward's input
+        tensors when the Loss resolves (at the latest inside the next forward call), so they must
+        not be overwritten in place before then — the reference's own contract for the returned
+        Loss (read it before the next call, vamp_model.py:61-62)."""
         host.copy_(res, non_blocking=True)
         done = torch.cuda.Event()
         done.record(torch.cuda.current_stream(res.device))   # the stream the launches and the copy ran on
@@ -207,12 +210,13 @@ class LazyResult:
         L._pending = finish
 
     grid_rescues = 0
+    # Test-only hook (tests/test_gpu_rescue.py): a callable that may rewrite a resolved persistent
+    # status record (e.g. report the grid as lost) before it is checked; None in production.
+    status_hook = None
 
     def _check_grid(self, status, counts, rescue, what):
-        global _TEST_LOSE_GRID
-        if _TEST_LOSE_GRID > 0 and rescue is not None:     # test seam: report this launch's grid as lost
-            _TEST_LOSE_GRID -= 1
-            status.nan_state = -1
+        if self.status_hook is not None and rescue is not None:
+            status = self.status_hook(status)
         if status.nan_state >= 0:
             return status, counts
         if rescue is not None:
@@ -223,16 +227,13 @@ class LazyResult:
         raise RuntimeError(f'{what}: persistent engine grid barrier timed out (results invalid)')
 
 
-# Test seam (tests only): the next N persistent results resolved are reported as lost grids
-# (nan_state = -1, what a timed-out grid exchange writes), to exercise the launch-engine rescue.
-_TEST_LOSE_GRID = 0
-
 
 class VAMP(LazyResult, nn.Module):
     """``engine``: nat.ENGINE_AUTO (persistent single-launch engine when the shape allows it,
     else three launches per iteration), ENGINE_LAUNCHES or ENGINE_PERSISTENT (amp_sparc.h).
     ``gemm``: the persistent engine's GEMM arithmetic, nat.GEMM_AUTO (split-precision bf16x3
-    where it fits, else f32 MFMA), GEMM_F32 or GEMM_X3 (amp_sparc.h)."""
+    where it fits: 24-bit operands, the reference's; else f32 MFMA), GEMM_F32, GEMM_X3, or the
+    opt-in GEMM_H2 (fp16x2, 22-bit operands: narrower than the reference) (amp_sparc.h)."""
 
     def __init__(self, config: Config, engine: int = nat.ENGINE_AUTO, gemm: int = nat.GEMM_AUTO) -> None:
         super().__init__()
@@ -318,7 +319,7 @@ class VAMP(LazyResult, nn.Module):
         d = self.config.dims()
         if nat.lib().amp_vamp_select_engine(C.byref(d), k, self.engine) != nat.ENGINE_PERSISTENT:
             return 0
-        return int(nat.lib().amp_vamp_max_epochs(C.byref(d), k))
+        return int(nat.lib().amp_vamp_max_epochs_gemm(C.byref(d), k, self.gemm))
 
     def epochs_eligible(self, n: int, k: int, epochs: int) -> bool:
         """Whether `epochs` forwards of this config fit ONE persistent launch

@@ -109,17 +109,19 @@ typedef struct amp_vamp_args {
  *  AUTO       PERSISTENT when eligible, else LAUNCHES. */
 /* Persistent-engine GEMM arithmetic (amp_vamp_args.gemm):
  *  F32   v_mfma_f32_16x16x4_f32 on the real expansion of each operator;
- *  X3    split precision: every f32 operand as three bf16 pieces, six bf16 MFMA products per
- *        product (terms below 2^-24 relative dropped), f32 accumulation — the f32 GEMM's
- *        accuracy at 2.7x the MFMA rate (needs k == N, N % 64 == 0 and 160 KB of LDS);
- *  H2    split precision in fp16: every A row scaled by its own power of two, every value as two
- *        fp16 pieces (22 significant bits), three fp16 MFMA products per product, f32
- *        accumulation, the scales taken off exactly — f32-level accuracy (max error below a
- *        sequential f32 sum's) with 2/3 of X3's operator bytes and half its MFMAs; the operators
- *        must have entries of magnitude < 4 (SVD factors: <= 1; larger entries give non-finite
- *        results, never silently wrong ones); same shape constraints as X3;
- *  AUTO  H2 where the planes fit, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32,
- *        AMP_VAMP_GEMM=x3 picks X3). */
+ *  X3    split precision: every f32 operand as three bf16 pieces (all 24 bits: the reference's
+ *        c64 operand precision), six bf16 MFMA products per product (terms below 2^-24 relative
+ *        dropped), f32 accumulation — the f32 GEMM's accuracy at 2.7x the MFMA rate (needs
+ *        k == N, N % 64 == 0 and 160 KB of LDS).  At N = 128 / 256 the operators are streamed
+ *        as plain f32 and split in registers (8 bytes per complex entry instead of 12;
+ *        AMP_VAMP_X3F=0 keeps the pre-split planes);
+ *  H2    OPT-IN, narrower than the reference: every A row scaled by its own power of two, every
+ *        value as two fp16 pieces (22 significant bits), three fp16 MFMA products per product
+ *        (the 2^-22 lo.lo term dropped), f32 accumulation, the scales taken off exactly; the
+ *        operators must have entries of magnitude < 4 (SVD factors: <= 1; larger entries give
+ *        non-finite results, never silently wrong ones); same shape constraints as X3;
+ *  AUTO  X3 where the planes fit, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32,
+ *        AMP_VAMP_GEMM=h2 picks H2). */
 #define AMP_GEMM_AUTO 0
 #define AMP_GEMM_F32 1
 #define AMP_GEMM_X3 2
@@ -132,7 +134,7 @@ typedef struct amp_vamp_args {
 /* The engine amp_vamp_run will use for this shape on the current device (LAUNCHES or
  * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
-/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_H2, AMP_GEMM_X3 or
+/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_X3, AMP_GEMM_H2 or
  * AMP_GEMM_F32 (AMP_E_ARG when `gemm` is AMP_GEMM_X3 / _H2 and the shape does not fit it). */
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
@@ -208,6 +210,9 @@ int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32
 int amp_vamp_debug_dump(void* buf);
 /* The most epochs of d->B trials one launch holds on this device (0: not persistent-eligible). */
 int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
+/* The same for a given persistent GEMM arithmetic (amp_vamp_args.gemm): two workgroups per CU
+ * only where that arithmetic has the two-per-CU build (the split-precision forms at N = 64). */
+int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                  const amp_vamp_decide_args* dec, int32_t epochs, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
@@ -234,10 +239,13 @@ typedef struct amp_bamp_args {
     void* ws;
     size_t ws_bytes;
     float P0, Ps;       /* Config.P0 / Config.Ps as float32 (bamp.py:36), denoiser 1 only */
-    int32_t gemm;       /* GEMM arithmetic: AMP_GEMM_AUTO (fp16x2 where N % 64 == 0, n % 64 == 0 and
-                           Lin = Lout = 1, else f32; environment AMP_BAMP_GEMM=f32 keeps f32),
-                           AMP_GEMM_F32 or AMP_GEMM_H2 (amp_gemm_h2.h: every GEMM's A rows split once
-                           into per-row scaled fp16 pieces; |H| must stay below 64) */
+    int32_t gemm;       /* GEMM arithmetic: AMP_GEMM_AUTO (f32 MFMA, the reference's operand
+                           precision; environment AMP_BAMP_GEMM=h2 picks fp16x2 where N % 64 == 0 and
+                           n % 64 == 0, block-banded channels included), AMP_GEMM_F32, or AMP_GEMM_H2
+                           (OPT-IN, 22-bit operands, amp_gemm_h2.h: every GEMM's A rows split once into
+                           per-row scaled fp16 pieces; the operator pieces are scaled by 2^10, so |H|^2
+                           must stay below 64, i.e. |H| < 8: beyond it a piece is inf and the detection
+                           turns NaN, counted as errors, never silently wrong) */
     int32_t pad;
 } amp_bamp_args;
 

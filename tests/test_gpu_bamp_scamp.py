@@ -217,17 +217,25 @@ def torch_ncu():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
-@pytest.mark.parametrize('alph,ebn0,B', [('16QAM', 8.0, 4096), ('QPSK', 2.0, 4096), ('16QAM', 20.0, 4096),
-                                         ('16QAM', 12.0, 1000), ('QPSK', 6.0, 17)])
-def test_scamp_fused_decision_equals_standalone(device, alph, ebn0, B):
+@pytest.mark.parametrize('alph,ebn0,B,shape', [('16QAM', 8.0, 4096, (128, 8, 256)), ('QPSK', 2.0, 4096, (128, 8, 256)),
+                                               ('16QAM', 20.0, 4096, (128, 8, 256)), ('16QAM', 12.0, 1000, (128, 8, 256)),
+                                               ('QPSK', 6.0, 17, (128, 8, 256)),
+                                               # M = 1 and M = 2: 128 / 64 sections per row, whose labels
+                                               # (17 B per section) exceed the free LDS region at
+                                               # (2N, 2n) = (256, 256) and are then read from global memory
+                                               ('16QAM', 8.0, 4096, (128, 128, 128)), ('QPSK', 4.0, 1000, (128, 64, 128)),
+                                               ('16QAM', 10.0, 4096, (128, 128, 256))])
+def test_scamp_fused_decision_equals_standalone(device, alph, ebn0, B, shape):
     """amp_scamp_detect_count (decision + counters inside the persistent SCAMP launch, from LDS;
     scamp.py:107 -> loss.py:67-179) gives the same amp_counts as amp_scamp_run followed by
     amp_map_decide_count on the same forward: integer counters exactly, the float64 squared-error
-    sums to summation-order rounding; ragged batches (B = 1000, 17) included."""
+    sums to summation-order rounding; ragged batches (B = 1000, 17) and one-position sections
+    (M = 1, 2: the label staging bound of amp_decide_fused.h) included."""
     import amp_native as nat
     from scamp import SCAMP
     from vamp import read_result
-    cfg = _config(128, 8, 256, B, alph, iterations=20)
+    Nt, Na, Nr = shape
+    cfg = _config(Nt, Na, Nr, B, alph, iterations=20)
     inp = _regen_inputs(cfg, 0, ebn0, svd=False)
     det = SCAMP(cfg, engine=nat.ENGINE_PERSISTENT)
     L = det(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])

@@ -2,8 +2,9 @@
 the grid drains, the results are invalid) is re-run on the launch engine in the same process
 (LazyResult._check_grid), and the event is counted in `grid_rescues`.
 
-The loss is injected through the test seam vamp._TEST_LOSE_GRID (the status record is reported as
-a timed-out grid exactly as the kernel writes it); the rescued Loss must equal a plain
+The loss is injected through the detectors' test-only status hook (LazyResult.status_hook: the
+status record is reported as a timed-out grid exactly as the kernel writes it); the rescued Loss
+must equal a plain
 launch-engine forward of the same epoch exactly (same engine, same inputs, same arithmetic).
 """
 import numpy as np
@@ -33,6 +34,19 @@ def _inputs(cfg, seed, ebn0, E=1):
     return W, A, SNR, eps
 
 
+def _lose_grids(n):
+    """A status hook that reports the next `n` persistent results as lost grids (nan_state = -1,
+    what a timed-out grid exchange writes)."""
+    left = [n]
+
+    def hook(status):
+        if left[0] > 0:
+            left[0] -= 1
+            status.nan_state = -1
+        return status
+    return hook
+
+
 def _same(a, b):
     for k in KEYS:
         va, vb = np.asarray(a[k], dtype=np.float64), np.asarray(b[k], dtype=np.float64)
@@ -53,21 +67,21 @@ def test_vamp_lost_grid_rescued_on_launch_engine(device, alphabet, ebn0):
     ref = dict(vm.VAMP(cfg, engine=nat.ENGINE_LAUNCHES)(U, s, Vh, mv(y), SNR, mv(x), sym, idx).loss)
     det = vm.VAMP(cfg)
     assert det.max_epochs(64) >= 2        # the shape runs on the persistent engine
-    vm._TEST_LOSE_GRID = 1
+    det.status_hook = _lose_grids(1)
     try:
         got = dict(det(U, s, Vh, mv(y), SNR, mv(x), sym, idx).loss)
     finally:
-        vm._TEST_LOSE_GRID = 0
+        det.status_hook = None
     assert det.grid_rescues == 1
     _same(got, ref)
     # side-by-side epochs: epoch 0's grid lost, epoch 1 kept
-    vm._TEST_LOSE_GRID = 1
+    det.status_hook = _lose_grids(1)
     try:
         Ls = det.forward_epochs(U, s, Vh, [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
                                 [e[1] for e in eps], [e[2] for e in eps])
         got0, got1 = dict(Ls[0].loss), dict(Ls[1].loss)
     finally:
-        vm._TEST_LOSE_GRID = 0
+        det.status_hook = None
     assert det.grid_rescues == 2
     _same(got0, ref)
     x1, sym1, idx1, y1 = eps[1]
@@ -86,10 +100,10 @@ def test_scamp_lost_grid_rescued_on_launch_engine(device):
     mv = lambda t: t.to(device).contiguous()  # noqa: E731
     ref = dict(SCAMP(cfg, engine=nat.ENGINE_LAUNCHES)(mv(W), mv(A), mv(y), SNR, mv(x), sym, idx).loss)
     det = SCAMP(cfg)
-    vm._TEST_LOSE_GRID = 1
+    det.status_hook = _lose_grids(1)
     try:
         got = dict(det(mv(W), mv(A), mv(y), SNR, mv(x), sym, idx).loss)
     finally:
-        vm._TEST_LOSE_GRID = 0
+        det.status_hook = None
     assert det.grid_rescues == 1
     _same(got, ref)

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Build-time check (run by the csrc Makefile after linking): no persistent-engine instantiation
+that the host can dispatch may spill VGPRs to scratch, except the documented ones below.
+
+Reads the gfx950 code object of each object file (the .hip_fatbin offload bundle), its
+amdhsa.kernels metadata (.vgpr_spill_count, .private_segment_fixed_size), and fails when a
+vamp_persist / scamp_persist kernel spills and is not listed in ALLOWED.  Why spills matter here:
+scratch is per-lane memory traffic inside the persistent loop, and the round-3 review tied the
+two-workgroups-per-CU corruption to the spilling instantiations (DESIGN.md §3.8 has the outcome
+of that investigation).
+
+  python tools/check_spills.py amp-sparc-spatialmodulation_amd/build/*.o [--list]
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = '/opt/rocm/lib/llvm/bin'
+
+# Documented exceptions: (kernel-name regex, reason).  Each is an instantiation the host can
+# dispatch whose spills are loop-invariant values reloaded a few times per iteration.
+ALLOWED = [
+    # vamp_persist<NT=2, KK=16, NWV=4, DU=2, X3, OCC=2, H2?>: the cfg2 two-per-CU build (256 VGPRs),
+    # 12 / 25 spilled values = the per-lane s^2 / y~ registers kept across the loop
+    (r'_ZN3amp12vamp_persistILi2ELi16ELi4ELi2ELb1ELi2ELb[01]E', 'cfg2 16-QAM two-per-CU build'),
+    # the other two-per-CU alphabets (QPSK / 8-PSK / 64-QAM at N = 64, side-by-side epochs)
+    (r'_ZN3amp12vamp_persistILi2ELi(4|8|64)ELi4ELi[124]ELb1ELi2ELb[01]E', 'N = 64 two-per-CU builds'),
+]
+
+
+def kernels(obj):
+    """[(name, vgpr_spill, private_segment)] of the gfx950 code object inside `obj`."""
+    with tempfile.TemporaryDirectory() as td:
+        fb = os.path.join(td, 'fb.bin')
+        dev = os.path.join(td, 'dev.o')
+        subprocess.run([f'{LLVM}/llvm-objcopy', '--dump-section=.hip_fatbin=' + fb, obj, os.path.join(td, 'h.o')],
+                       check=True, capture_output=True)
+        subprocess.run([f'{LLVM}/clang-offload-bundler', '--type=o', '--unbundle', '--input=' + fb,
+                        '--targets=hipv4-amdgcn-amd-amdhsa--gfx950', '--output=' + dev], check=True,
+                       capture_output=True)
+        notes = subprocess.run([f'{LLVM}/llvm-readelf', '--notes', dev], check=True, capture_output=True,
+                               text=True).stdout
+    out = []
+    for blk in re.split(r'\n\s*- \.agpr_count:', notes)[1:]:
+        name = re.search(r'\.name:\s+(\S+)', blk)
+        spill = re.search(r'\.vgpr_spill_count:\s+(\d+)', blk)
+        priv = re.search(r'\.private_segment_fixed_size:\s+(\d+)', blk)
+        if name:
+            out.append((name.group(1), int(spill.group(1)) if spill else 0, int(priv.group(1)) if priv else 0))
+    return out
+
+
+def main(argv):
+    objs = [a for a in argv if not a.startswith('--')]
+    listing = '--list' in argv
+    bad = []
+    for obj in objs:
+        for name, spill, priv in kernels(obj):
+            if not re.search(r'(vamp|scamp)_persist', name):
+                continue
+            allowed = [why for rx, why in ALLOWED if re.search(rx, name)]
+            if listing or (spill and not allowed):
+                print(f'{os.path.basename(obj):32s} spill {spill:4d} private {priv:5d}  {name}'
+                      + (f'  [allowed: {allowed[0]}]' if spill and allowed else ''))
+            if spill and not allowed:
+                bad.append(name)
+    if bad:
+        print(f'check_spills: {len(bad)} persistent instantiation(s) spill VGPRs (tools/check_spills.py ALLOWED)',
+              file=sys.stderr)
+        return 1
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main(sys.argv[1:]))

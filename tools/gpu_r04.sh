@@ -23,6 +23,12 @@ for s in ${STEPS:-bench}; do
     bench_h2) run bench_h2 300 python3 bench.py --no-cpu-baseline --gemm h2 ;;
     bench_f32) run bench_f32 300 python3 bench.py --no-cpu-baseline --gemm f32 ;;
     trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;
+    bench_nows) run bench_nows 300 env AMP_VAMP_WS=0 python3 bench.py --no-cpu-baseline ;;
+    trace_nows) run trace_nows 300 env AMP_VAMP_WS=0 python3 tools/trace_persist.py --config cfg4 ;;
+    bench_x3pre) run bench_x3pre 300 env AMP_VAMP_X3F=0 python3 bench.py --no-cpu-baseline ;;
+    bench_x3f8) run bench_x3f8 300 env AMP_VAMP_X3F_WAVES=8 python3 bench.py --no-cpu-baseline ;;
+    trace_x3pre) run trace_x3pre 300 env AMP_VAMP_X3F=0 python3 tools/trace_persist.py --config cfg4 ;;
+    trace_x3f8) run trace_x3f8 300 env AMP_VAMP_X3F_WAVES=8 python3 tools/trace_persist.py --config cfg4 ;;
     trace_h2) run trace_h2 300 env AMP_VAMP_GEMM=h2 python3 tools/trace_persist.py --config cfg4 ;;
     configs) run configs 600 python3 tools/configs_bench.py ;;
     tests_vamp) run tests_vamp 900 $PYT tests/test_gpu_vamp.py -m gpu ;;
@@ -30,6 +36,10 @@ for s in ${STEPS:-bench}; do
     tests_cfg5) run tests_cfg5 900 $PYT tests/test_gpu_cfg5.py -m gpu ;;
     tests_bs) run tests_bs 900 $PYT tests/test_gpu_bamp_scamp.py -m gpu ;;
     tests) run tests 1100 $PYT tests -m gpu ;;
+    occ2) run occ2_prod 300 python3 tools/occ2_repro.py 10 &&
+          run occ2_pk4 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du4.so python3 tools/occ2_repro.py 10 &&
+          run occ2_pk2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du2.so python3 tools/occ2_repro.py 10 ;;
+    tests_vdef) run tests_vdef 900 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2" ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     profile) run profile 900 bash tools/profile.sh ;;
     ubench) run ubench 300 bash tools/ubench/run.sh ;;

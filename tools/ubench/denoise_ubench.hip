@@ -100,7 +100,11 @@ extern "C" int ubench_main() {
     printf("grid %d full %d\n", c.grid, c.gfull);
     run<16, 1, 4, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
     run<16, 2, 4, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 2, 4, false>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 1, 8, false>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
     run<16, 2, 8, true>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 2, 8, false>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
+    run<16, 1, 16, false>("cfg4 16QAM grid", dr, c, N, M, inv, dout, dsink);
     fflush(stdout);
     return 0;
 }
