@@ -79,17 +79,6 @@ __host__ __device__ __forceinline__ size_t x3_index(int o, int j, int f, int J) 
     return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 6 + f) * 64 + lane) * 8 + (kk & 7);
 }
 
-// The f32-streamed split form (gemm_x3f, amp_persist.h): X[o][j] as plain f32, two planes per
-// (tile, group) (f = 0: Re, 1: Im), each in two 1 KB halves h: lane (o & 15) + 16 ((j & 31) >> 3)
-// holds elements 4h .. 4h + 3 of its 8 consecutive j (j & 7) in half h: one 16-byte buffer load
-// per lane, plane and half.  Returns a float index; 4 KB per (tile, group).
-__host__ __device__ __forceinline__ size_t x3f_index(int o, int j, int f, int J) {
-    const int kk = j & 31;
-    const int lane = (o & 15) + 16 * (kk >> 3);
-    const int e = kk & 7;
-    return (((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 2 + f) * 2 + (e >> 2)) * 64 + lane) * 4 + (e & 3);
-}
-
 // The same for the fp16x2 form (gemm_h2): four planes per (tile, group), f = 0-1: Re h0 h1,
 // 2-3: Im h0 h1.
 __host__ __device__ __forceinline__ size_t h2_index(int o, int j, int f, int J) {

@@ -275,107 +275,6 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
     }
 }
 
-// ---- split-precision complex GEMM, f32-streamed operator (bf16x3 split in registers) ----
-// The per-iteration GEMMs are bound by each CU's operator stream from L2 (the bf16x3 and fp16x2
-// GEMMs took 18.8k / 12.6k cycles at cfg4 for 12 / 8 bytes per complex entry: ~41 B/clk per CU
-// either way, profiles/r04_cfg4_phases.txt).  gemm_x3f streams the operator as plain f32 (8 bytes
-// per complex entry, x3f_index) and splits it in registers by truncation: hi = x with the low 16
-// bits cleared, r1 = x - hi (exact), mid = r1 truncated, lo = r1 - mid (exact, at most 8
-// significant bits), so x = hi + mid + lo EXACTLY: the operator keeps all 24 bits of the
-// reference's f32 (vamp.py:67, 72) and the six kept products drop only terms < 2^-24 |ab|, as
-// gemm_x3.  The split costs ~5.5 VALU operations per operator value; with two waves per SIMD they
-// issue in the MFMAs' shadow.
-
-// Eight f32 operator values (x0: elements 0-3, x1: 4-7) -> their three bf16 pieces, element e in
-// dword e / 2 (even elements in the low half), as a bf16x8 MFMA operand each.
-__device__ __forceinline__ void split3t8(const u32x4& x0, const u32x4& x1, u32x4& p0, u32x4& p1, u32x4& p2) {
-    unsigned xs[8], r1[8], r2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const unsigned x = e < 4 ? x0[e] : x1[e - 4];
-        const float r = __uint_as_float(x) - __uint_as_float(x & 0xffff0000u);   // exact
-        const unsigned ru = __float_as_uint(r);
-        const float l = r - __uint_as_float(ru & 0xffff0000u);                   // exact
-        xs[e] = x; r1[e] = ru; r2[e] = __float_as_uint(l);
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {   // high halves of elements 2d (low) and 2d + 1 (high)
-        p0[d] = __builtin_amdgcn_perm(xs[2 * d + 1], xs[2 * d], 0x07060302u);
-        p1[d] = __builtin_amdgcn_perm(r1[2 * d + 1], r1[2 * d], 0x07060302u);
-        p2[d] = __builtin_amdgcn_perm(r2[2 * d + 1], r2[2 * d], 0x07060302u);
-    }
-}
-
-// gemm_x3's contract with the operator packed by x3f_index (f32).  RR operator groups in flight
-// per wave (one: with two waves per SIMD the partner's MFMAs cover a wave's load latency).
-#ifndef AMP_X3F_RING
-#define AMP_X3F_RING 1
-#endif
-template <int NT, int G, int R = AMP_X3F_RING>
-__device__ __forceinline__ void gemm_x3f(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
-                                         f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
-    constexpr int RR = G < R ? G : R;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) { cr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; ci[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 4096, (short)0, 0x7ffffff0, 0x00020000);
-    const int vo = lane * 16;
-    u32x4 ring[RR][NT][4];   // q = 0, 1: Re halves; 2, 3: Im halves
-#pragma unroll
-    for (int d = 0; d < RR; ++d)
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                ring[d][t][q] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + d) * 4 + q) * 1024, 0);
-    const int ln = pl_opaque(lane);
-    const int sw = (ln & 15) & pl_mask(ldx);
-    const unsigned short* ap = sP + (ln & 15) * ldx + 8 * ((ln >> 4) ^ (sw & 3));
-    const int s32 = 32 * (sw >> 2);
-    const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const int d = g % RR;
-        // this group's A fragments (no prefetch: the SIMD's partner wave covers the LDS latency)
-        u32x4 a[6], na[3];
-#pragma unroll
-        for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + ((32 * g) ^ s32) + f * 16 * ldx);
-#pragma unroll
-        for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            u32x4 w[6];   // w[0..2]: Re x0 x1 x2, w[3..5]: Im (gemm_x3's plane order)
-            split3t8(ring[d][t][0], ring[d][t][1], w[0], w[1], w[2]);
-            split3t8(ring[d][t][2], ring[d][t][3], w[3], w[4], w[5]);
-#define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
-            // smallest terms first (gemm_x3's order)
-            AMP_MF(cr[t], a[0], w[2]);  AMP_MF(ci[t], a[0], w[5]);
-            AMP_MF(cr[t], a[1], w[1]);  AMP_MF(ci[t], a[1], w[4]);
-            AMP_MF(cr[t], a[2], w[0]);  AMP_MF(ci[t], a[2], w[3]);
-            AMP_MF(cr[t], na[0], w[5]); AMP_MF(ci[t], a[3], w[2]);
-            AMP_MF(cr[t], na[1], w[4]); AMP_MF(ci[t], a[4], w[1]);
-            AMP_MF(cr[t], na[2], w[3]); AMP_MF(ci[t], a[5], w[0]);
-            AMP_MF(cr[t], a[0], w[1]);  AMP_MF(ci[t], a[0], w[4]);
-            AMP_MF(cr[t], a[1], w[0]);  AMP_MF(ci[t], a[1], w[3]);
-            AMP_MF(cr[t], na[0], w[4]); AMP_MF(ci[t], a[3], w[1]);
-            AMP_MF(cr[t], na[1], w[3]); AMP_MF(ci[t], a[4], w[0]);
-            AMP_MF(cr[t], a[0], w[0]);  AMP_MF(ci[t], a[0], w[3]);
-            AMP_MF(cr[t], na[0], w[3]); AMP_MF(ci[t], a[3], w[0]);
-#undef AMP_MF
-        }
-        if (g + RR < G) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    ring[d][t][q] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + RR) * 4 + q) * 1024, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // ---- split-precision complex GEMM (fp16x2) ----
 // v 2^e = h0 + h1 with fp16 pieces (round-to-nearest-even; 22 significant bits), so a product
 // keeps the three terms h0g0 h0g1 h1g0 (the dropped h1g1 is <= 2^-22 of it) on

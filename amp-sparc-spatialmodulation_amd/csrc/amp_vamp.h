@@ -276,9 +276,6 @@ int vamp_gemm_select(const amp_dims* d, int k, int gemm);   // 0 f32, 1 bf16x3, 
 bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);
 bool vamp_persist_ytil_h2(const VampK& P);
-bool vamp_persist_ytil_x3(const VampK& P);
-bool vamp_persist_x3f_ok(int N);
-bool vamp_persist_ws_ok(const VampK& P);   // the wave-specialized bf16x3 form (amp_vamp_persist_x3.hip)
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu);
 int device_cu_count();
 float* debug_dump_ptr();   // amp_vamp_debug_dump's buffer (null: off)

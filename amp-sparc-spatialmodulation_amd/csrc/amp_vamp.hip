@@ -473,9 +473,7 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2) || x3_fits,
                 "amp_vamp: the split-precision engines need k == N, N %% 64 == 0 and "
                 "their LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
-    // x3 = 1 (bf16x3) runs on the f32-streamed operators (x3 = 3) where that engine takes the shape
     P.x3 = vamp_gemm_mode(a->gemm, x3_fits);
-    if (P.x3 == 1 && vamp_persist_x3f_ok(d->N)) P.x3 = 3;
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.dump = debug_dump_ptr();
     return AMP_OK;
@@ -568,17 +566,12 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     const int env = ytil_in_kernel_env();
     if (P.x3 == 2)
         P.ytil_in_kernel = (env != 0 && vamp_persist_ytil_h2(P)) ? 1 : 0;
-    else if (P.x3 == 1 || P.x3 == 3)
-        // bf16x3: the in-kernel y~ measured no faster than its launch (its 16 x n planes take the
-        // prologue as long as gemm_store's MFMAs); AMP_YTIL_IN_KERNEL=1 turns it on (not for the
-        // wave-specialized form, which reads y~ back from the workspace every iteration)
-        P.ytil_in_kernel = (env == 1 && vamp_persist_ytil_x3(P) && !(P.x3 == 1 && vamp_persist_ws_ok(P))) ? 1 : 0;
     else
         P.ytil_in_kernel = (!P.x3 && env == 1 && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
     const bool yk = P.ytil_in_kernel != 0;
     CWeightJob j[3];
     if (P.x3) {
-        const int pk = P.x3 == 2 ? WPACKH2 : P.x3 == 3 ? WPACKX3F : WPACKX3;
+        const int pk = P.x3 == 2 ? WPACKH2 : WPACKX3;
         //   q = Vh r~    (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N   (bf16x3 / fp16x2 planes)
         j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wx1, P.N, P.k, pk};
         //   V (x~ - q)   (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
@@ -592,9 +585,6 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     j[2] = (yk && P.x3 == 2)
                ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, P.n, P.k, WPACKH2, YH2_EX}
-           : (yk && (P.x3 == 1 || P.x3 == 3))
-               ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, P.n, P.k,
-                            P.x3 == 3 ? WPACKX3F : WPACKX3}
            : yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
                 : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
     int rc = build_cweights(j, 3, P.pbar, PBAR_WORDS, st);

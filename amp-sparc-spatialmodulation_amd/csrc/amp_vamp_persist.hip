@@ -66,22 +66,6 @@ bool vamp_persist_ytil_h2(const VampK& P) {
     return P.n == 2 * P.N && P.k == P.N && 2 * PBM * pl_ldx(P.n) <= playout(P.N, P.k, P.L, true).offV0;
 }
 
-// the bf16x3 y~ prologue: n == 2N and the six y planes (16 rows x n bf16) within the A / R / X
-// region of the split-precision carve
-bool vamp_persist_ytil_x3(const VampK& P) {
-    return P.n == 2 * P.N && P.k == P.N && 3 * PBM * pl_ldx(P.n) <= playout(P.N, P.k, P.L, true).offV0;
-}
-
-// The f32-streamed bf16x3 form (x3 = 3): eight waves, N = 128 or 256 (whole complex tiles per
-// wave); AMP_VAMP_X3F=0 keeps the pre-split bf16x3 operators (A/B runs).
-bool vamp_persist_x3f_ok(int N) {
-    static const bool off = [] {
-        const char* e = getenv("AMP_VAMP_X3F");
-        return e && e[0] == '0';
-    }();
-    return !off && (N == 128 || N == 256);
-}
-
 bool vamp_persist_x3_fits(int N, int k, int L) {
     return k == N && N % 64 == 0 && (size_t)playout(N, k, L, true).total * 4 + 2048 <= 160 * 1024;
 }
@@ -126,7 +110,6 @@ bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs, int ge
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_x3.hip
 int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_h2.hip
-int persist_dispatch_x3f(const VampK& P, const DecConst& dc, hipStream_t st);  // amp_vamp_persist_x3f.hip
 
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
@@ -145,7 +128,6 @@ static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) 
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
     if (P.x3 == 2) return persist_dispatch_h2(P, dc, st);
-    if (P.x3 == 3) return persist_dispatch_x3f(P, dc, st);
     if (P.x3) return persist_dispatch_x3(P, dc, st);
     switch (P.N) {
     case 64: return persist_launch_nt<2, 4, false>(P, dc, st);

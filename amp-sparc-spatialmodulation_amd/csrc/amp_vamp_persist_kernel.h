@@ -19,9 +19,6 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #ifndef AMP_KK4_DU
 #define AMP_KK4_DU 4                    // QPSK sections in flight per lane group (diagnostic builds vary it)
 #endif
-#ifndef AMP_X3_YTIL
-#define AMP_X3_YTIL 1                   // the bf16x3 engines' y~ prologue (0: diagnostic builds without it)
-#endif
 #ifndef AMP_X3_DU
 #define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
 #endif
@@ -58,22 +55,6 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
     return y;
 }
 
-// One of the two column passes' sections (WS): local section s -> the block of 2^lhs sections
-// of pass `half` it falls in ((s >> lhs) << (lhs + 1) + half 2^lhs + (s & (2^lhs - 1))).
-template <class P>
-struct HalfSecPolicy {
-    P p;
-    int lhs, half;
-    __device__ __forceinline__ int map(int s) const {
-        return ((s >> lhs) << (lhs + 1)) + (half << lhs) + (s & ((1 << lhs) - 1));
-    }
-    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const { p.load(map(sec), m, rr, ri, it); }
-    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
-        p.store(map(sec), m, xr, xi, var, pa);
-    }
-    __device__ __forceinline__ void section(int sec, float smax, float sabs) const { p.section(map(sec), smax, sabs); }
-};
-
 // dc: the decision table; its Const64 base is also the exact rare path's float64 constellation.
 // X3: both per-iteration GEMMs on the split-precision bf16x3 engine (gemm_x3): the A operand
 // (r~, then w) lives in LDS as six bf16 planes, each wave owns NT/2 complex column tiles (the
@@ -83,27 +64,13 @@ struct HalfSecPolicy {
 // H2 (with X3): the split-precision GEMMs in the fp16x2 form (gemm_h2: four A planes, the operators
 // h2-packed); every A row (r~, then w) is scaled by its own power of two (h2_row_exp) before the
 // split and the accumulators are scaled back by 2^-(e_row + H2_EX).
-// XF (with X3): the operators streamed as plain f32 and split in registers (gemm_x3f): 8 bytes
-// per complex entry instead of 12, the same exact-f32 operands.  NWV = 8 (two waves per SIMD, each
-// owning half a wave's columns) takes the split's VALU work and the denoiser's in the partner's
-// MFMA / wait shadow; the denoiser then runs its scalar float32 form (two waves per SIMD,
-// amp_denoise.h denoise_sections_sel).
-// WS (with X3, NWV = 8): wave-specialized — waves 0-3 run the GEMMs (each owning NT / 2 complex
-// tiles, as the four-wave form; every GEMM in two passes over half of them), waves 4-7 start the
-// section denoiser on the columns of GEMM2's first pass while its second pass runs, then all
-// eight waves denoise the second half.  The matrix cores of a SIMD work on one wave's GEMM while
-// its partner wave's denoiser VALU runs (vamp.py:72-84 unchanged: the same operations per element,
-// only scheduled side by side).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool XF = false, bool WS = false>
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
-    static_assert(!X3 || ((NWV == 4 || NWV == 8) && NT % 2 == 0), "X3: four or eight waves, whole complex tiles");
-    static_assert(!XF || (X3 && !H2), "XF: the bf16x3 engine's operator format");
-    static_assert(!WS || (X3 && !H2 && !XF && NWV == 8 && KK <= 16 && NT % 4 == 0), "WS: bf16x3, eight waves");
+    static_assert(!X3 || (NWV == 4 && NT % 2 == 0), "X3: four waves, whole complex tiles");
     constexpr bool PKDEN = (OCC * NWV / 4 == 1) || AMP_OCC2_PK;   // packed denoiser only at one wave per SIMD
     constexpr int PWG = 64 * NWV;
-    constexpr int GW = WS ? 4 : NWV;           // waves that run the GEMMs
-    constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per GEMM wave (X3)
-    constexpr int G3 = NT * GW / 4;            // 32-wide complex reduction groups: N / 32
+    constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
+    constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
     constexpr int X3R = 1;                     // weight groups in flight (gemm_x3)
     const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -129,7 +96,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
     const int ldr = Y.ldr, lda = Y.lda;
     const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
-    const int cc0 = (WS ? (wave & 3) : wave) * NC;   // X3: this (GEMM) wave's complex 16-column tiles
+    const int cc0 = wave * NC;                 // X3: this wave's complex 16-column tiles
     unsigned short* sP = reinterpret_cast<unsigned short*>(sA);
     const int ldx = x3_ldx(N);
 
@@ -198,39 +165,6 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         }
         __syncthreads();   // the planes region becomes the Tracker's state
       }
-    } else if (X3 && !H2 && AMP_X3_YTIL && P.ytil_in_kernel) {
-      if constexpr (X3 && !H2 && AMP_X3_YTIL) {
-        // y~ = (s Uh) y (vamp.py:22) for this workgroup's rows on the bf16x3 GEMM (n == 2N): the y
-        // rows split into six bf16 planes over the A / R / X region (free until the Tracker's state
-        // is formed below), the operator s Uh x3-packed (K = n); no scaling (bf16 keeps f32's range)
-        constexpr int IPY = NT * GW / (2 * NWV);      // items per thread: PBM n / 8 / PWG, n = 16 NT GW
-        const int n = P.n, ldy = pl_ldx(n);
-        const int row = tid % PBM;
-#pragma unroll
-        for (int i = 0; i < IPY; ++i) {
-            const int e = tid + i * PWG;
-            const int j0 = 8 * (e / PBM);
-            float re[8], im[8];
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 2 * n + 2 * j0 + 4 * h);
-                re[2 * h] = v.x; im[2 * h] = v.y; re[2 * h + 1] = v.z; im[2 * h + 1] = v.w;
-            }
-            x3_store8(sP, ldy, row, j0, re, im);
-        }
-        __syncthreads();
-        f32x4 yr[NC], yi[NC];
-        if constexpr (XF)
-            gemm_x3f<NC, 2 * G3>(sP, ldy, P.Wq0, cc0, yr, yi);   // K = n = 2N: 2 G3 groups of 32
-        else if (!WS || wave < 4)
-            gemm_x3<NC, 2 * G3, X3R>(sP, ldy, P.Wq0, cc0, yr, yi);
-#pragma unroll
-        for (int t = 0; t < NC; ++t)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { yt[2 * t][r] = yr[t][r]; yt[2 * t + 1][r] = yi[t][r]; }
-        __syncthreads();   // the planes region becomes the Tracker's state
-      }
     } else if (X3) {
 #pragma unroll
         for (int t = 0; t < NC; ++t) {
@@ -287,7 +221,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 
     unsigned long long* trc = P.trace;
     auto stamp = [&](int t, int ph) {
-        if (trc && tid == 0) trc[((size_t)wg * P.max_iter + t) * AMP_TRACE_STRIDE + ph] = __builtin_amdgcn_s_memtime();
+        if (trc && tid == 0 && t < P.max_iter) trc[((size_t)wg * P.max_iter + t) * AMP_TRACE_STRIDE + ph] = __builtin_amdgcn_s_memtime();
     };
     if (trc && tid == 0) {
         trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg] = __builtin_amdgcn_s_memtime();
@@ -297,6 +231,96 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
     int fixed = 0, last_t = 0, aborted = 0;
     VampIter nx = cur;
+    // 5. batch scalars of iteration te (its partials published): every workgroup gathers and reduces
+    // every partial, settles the rare exact-float64 sections, and forms the scalars of te + 1 (nx).
+    // vnew / vprev: te's var buffers.  False: a grid exchange timed out (the grid is released).
+    auto exchange = [&](int te, float* vnew, const float* vprev) -> bool {
+            PartAcc g;
+            const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)te + 1u;
+            if (!part_gather(grs, ((unsigned)te * nwg + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) return false;
+            stamp(te, 6);
+            fixed = 0;
+            if (part_allnan(g)) {
+                // the reference's G is NaN / inf: every section of this iteration is NaN
+                if (!cur.fixed_all) {
+                    const float qn = __int_as_float(0x7fc00000);
+                    for (int e = tid; e < nrows * twoN; e += PWG) sX[(e / twoN) * ldr + e % twoN] = qn;
+                    for (int e = tid; e < nrows * N; e += PWG) vnew[e] = qn;
+                }
+                g.sumvar = __longlong_as_double(0x7ff8000000000000LL);
+                g.notclose = 1;
+                fixed = -1;
+            } else if (part_danger(g)) {
+                // (a) exact float64 G over the candidate sections of every workgroup
+                const double G32 = g.maxabs, slack = logit_slack(G32);
+                const float inv = cur.inv_sigma2;
+                auto ldf = [=](int s) {
+                    const int row = s / spr, sj = s - row * spr;
+                    const float* rp = sR + row * ldr + 2 * sj * M;
+                    return [=](int m, float& rr, float& ri, float& it) {
+                        rr = rp[2 * m]; ri = rp[2 * m + 1]; it = inv;
+                    };
+                };
+                double gm = 0.0;
+                for (int s = tid; s < nrows * spr; s += PWG)
+                    if ((double)sS[s] >= G32 - slack) gm = fmax(gm, section_absmax_f64(ldf(s), M, c64));
+                gm = group_max(gm, 64);
+                if (lane == 0) s_d[wave][0] = gm;
+                __syncthreads();
+                if (tid == 0) {
+                    double m4 = 0.0;
+                    for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
+                    P.pxch[((size_t)te * nwg + wg) * 4 + 0] = m4;
+                }
+                if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) return false;
+                double G = 0.0;
+                for (int w = wg0; w < wg0 + P.wpe; ++w) G = fmax(G, P.pxch[((size_t)te * nwg + w) * 4 + 0]);
+                // (b) exact recompute of this workgroup's sections below the danger line
+                double dsum = 0.0;
+                int dnc = 0, cnt = 0;
+                for (int s = tid; s < nrows * spr; s += PWG) {
+                    if (!((double)sM[s] - G < AMP_DANGER + slack)) continue;
+                    ++cnt;
+                    const int row = s / spr, sj = s - row * spr;
+                    float* xp = sX + row * ldr + 2 * sj * M;
+                    const int v0 = row * N + sj * M;
+                    auto st = [&](int m, float xr, float xi, float var) {
+                        const float old = vnew[v0 + m];
+                        dsum += (double)var - (double)old;
+                        dnc += (torch_close(var, vprev[v0 + m]) ? 0 : 1) - (torch_close(old, vprev[v0 + m]) ? 0 : 1);
+                        xp[2 * m] = xr; xp[2 * m + 1] = xi;
+                        vnew[v0 + m] = var;
+                    };
+                    exact_section_f64<true>(ldf(s), st, M, c64, G);
+                }
+                dsum = group_sum(dsum, 64);
+                dnc = group_sum(dnc, 64);
+                cnt = group_sum(cnt, 64);
+                __syncthreads();
+                if (lane == 0) { s_d[wave][1] = dsum; s_d[wave][2] = (double)dnc; s_d[wave][3] = (double)cnt; }
+                __syncthreads();
+                if (tid == 0) {
+                    double a = 0.0, b = 0.0, c = 0.0;
+                    for (int w = 0; w < PWG / 64; ++w) { a += s_d[w][1]; b += s_d[w][2]; c += s_d[w][3]; }
+                    P.pxch[((size_t)te * nwg + wg) * 4 + 1] = a;
+                    P.pxch[((size_t)te * nwg + wg) * 4 + 2] = b;
+                    P.pxch[((size_t)te * nwg + wg) * 4 + 3] = c;
+                }
+                if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) return false;
+                double a = 0.0, b = 0.0, c = 0.0;
+                for (int w = wg0; w < wg0 + P.wpe; ++w) {
+                    const double* q = P.pxch + ((size_t)te * nwg + w) * 4;
+                    a += q[1]; b += q[2]; c += q[3];
+                }
+                g.sumvar += a;   // (sum - old) + new, in float64
+                g.notclose = (uint32_t)((long long)g.notclose + (long long)b);
+                g.maxabs = G;
+                fixed = (int)c;
+            }
+        nx = vamp_advance(P, cur, g, fixed, te, scr, &s2l);
+        stamp(te, 7);
+        return true;
+    };
 
     for (int t = 0; t < P.max_iter; ++t) {
         last_t = t;
@@ -383,21 +407,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
         f32x4 acc[NT];
         f32x4 cr[NC], ci[NC];
-        if constexpr (WS) {
-            // GEMM waves only, in two passes of NC / 2 tiles (half the operator ring in registers);
-            // both passes' accumulators are kept until the barrier below ends every read of r~
-            constexpr int NH = NC / 2;
-            if (wave < 4) {
-                f32x4 ra[NH], ia[NH], rb[NH], ib[NH];
-                gemm_x3<NH, G3, 2, true>(sP, ldx, P.Wx1, cc0, ra, ia);
-                gemm_x3<NH, G3, 2, true>(sP, ldx, P.Wx1, cc0 + NH, rb, ib);
-#pragma unroll
-                for (int t2 = 0; t2 < NH; ++t2) { cr[t2] = ra[t2]; ci[t2] = ia[t2]; cr[NH + t2] = rb[t2]; ci[NH + t2] = ib[t2]; }
-            }
-        } else if constexpr (H2)
+        if constexpr (H2)
             gemm_h2<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
-        else if constexpr (XF)
-            gemm_x3f<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
         else if constexpr (X3)
             gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx1, cc0, cr, ci);
         else
@@ -451,7 +462,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                     wi[r] = __builtin_amdgcn_ldexpf(ci[t2][r], hew[r]);
                 }
                 h2_store_acc(sP, ldx, o, wr, wi);
-                if (!WS && P.dump) {
+                if (P.dump) {
                     float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 0) * PBM * twoN;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -463,42 +474,19 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
             for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(hew[r] + H2_EX));
         } else if constexpr (X3) {
-          if (!WS || wave < 4) {
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lane & 15);
-                float ytr[4], yti[4], s2v;
-                if constexpr (WS) {
-                    // y~ and s^2 read back each iteration (32 KB per workgroup from L2) rather
-                    // than held in registers: the GEMM waves have 256 of them.  The lane index is
-                    // pinned (pl_opaque) so that the addresses are formed here, not hoisted out of
-                    // the iteration loop and kept live across it
-                    const int ln = pl_opaque(lane);
-                    const int oo = 16 * (cc0 + t2) + (ln & 15);
-                    const float sv = P.s[oo];
-                    s2v = sv * sv;                                       // vamp.py:17
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = 4 * (ln >> 4) + r;
-                        const float2 v = row < nrows ? *reinterpret_cast<const float2*>(P.ytil + (size_t)(row0 + row) * twok + 2 * oo)
-                                                     : make_float2(0.f, 0.f);
-                        ytr[r] = v.x; yti[r] = v.y;
-                    }
-                } else {
-                    s2v = s2c[t2];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { ytr[r] = yt[2 * t2][r]; yti[r] = yt[2 * t2 + 1][r]; }
-                }
-                const float sc = 1.0f / (s2v + cur.vr);
+                const float sc = 1.0f / (s2c[t2] + cur.vr);
                 float wr[4], wi[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float qr = cr[t2][r], qi = ci[t2][r];
-                    wr[r] = sc * (ytr[r] + cur.vr * qr) - qr;
-                    wi[r] = sc * (yti[r] + cur.vr * qi) - qi;
+                    wr[r] = sc * (yt[2 * t2][r] + cur.vr * qr) - qr;
+                    wi[r] = sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi;
                 }
                 x3_store_acc(sP, ldx, o, wr, wi);
-                if (!WS && P.dump) {
+                if (P.dump) {
                     float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 0) * PBM * twoN;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -507,7 +495,6 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                     }
                 }
             }
-          }
         } else
 #pragma unroll
         for (int t2 = 0; t2 < NT; ++t2) {
@@ -522,65 +509,13 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         __syncthreads();
         stamp(t, 3);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
-        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
-        if (!WS && P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
-        PartAcc pa;
-        if constexpr (WS) {
-            // r = (V w + r~ - alpha r~) / (1 - alpha) for complex tile t of this GEMM wave
-            auto r_epi = [&](int tt, const f32x4& xr4, const f32x4& xi4) {
-                const int ln = pl_opaque(lane);   // addresses formed here, not hoisted (see above)
-                const int o = 16 * (cc0 + tt) + (ln & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int b = (4 * (ln >> 4) + r) * ldr + 2 * o;
-                    const float rtr = (sX[b] - cur.dxdr_prev * sR[b]) * cur.ns_prev;
-                    const float rti = (sX[b + 1] - cur.dxdr_prev * sR[b + 1]) * cur.ns_prev;
-                    const float xtr = xr4[r] + rtr, xti = xi4[r] + rti;
-                    sR[b] = (xtr - cur.alpha * rtr) * cur.inv1ma;
-                    sR[b + 1] = (xti - cur.alpha * rti) * cur.inv1ma;
-                    if (!WS && P.dump) {
-                        float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 1) * PBM * twoN;
-                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o] = sR[b];
-                        dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = sR[b + 1];
-                    }
-                }
-            };
-            constexpr int NH = NC / 2;
-            constexpr int MS = 16 * NH;   // the section size: one section per GEMM wave and pass (vamp_persist_ws_ok)
-            const int nhalf = nrows * spr / 2;
-            if (wave < 4) {
-                f32x4 ra[NH], ia[NH];
-                gemm_x3<NH, G3, 2, true>(sP, ldx, P.Wx2, cc0, ra, ia);
-#pragma unroll
-                for (int t2 = 0; t2 < NH; ++t2) r_epi(t2, ra[t2], ia[t2]);
-            }
-            // phase 0: GEMM waves run the second pass while waves 4-7 denoise the first pass's
-            // sections; phase 1: all eight waves denoise the second pass's sections.  One loop, so
-            // that the denoiser is inlined once (its loop-invariant set-up stays out of the prologue)
-#pragma unroll 1
-            for (int ph = 0; ph < 2; ++ph) {
-                __syncthreads();   // this phase's input rows r in LDS
-                if (ph == 1) stamp(t, 4);
-                if (ph == 0 && wave < 4) {
-                    f32x4 ra[NH], ia[NH];
-                    gemm_x3<NH, G3, 2, true>(sP, ldx, P.Wx2, cc0 + NH, ra, ia);
-#pragma unroll
-                    for (int t2 = 0; t2 < NH; ++t2) r_epi(NH + t2, ra[t2], ia[t2]);
-                } else {
-                    const DenWaves dw = ph == 0 ? DenWaves{wave - 4, 4} : DenWaves{wave, 8};
-                    denoise_sections_sel<true, KK, DU, MS, false>(HalfSecPolicy<PDenoisePolicy>{pol, 0, ph}, nhalf, P.c,
-                                                                  pa, dw);
-                }
-            }
-        } else if constexpr (X3) {
+        if constexpr (X3) {
             if constexpr (H2) {
                 gemm_h2<NC, G3>(sP, ldx, P.Wx2, cc0, cr, ci);
 #pragma unroll
                 for (int t2 = 0; t2 < NC; ++t2)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
-            } else if constexpr (XF) {
-                gemm_x3f<NC, G3>(sP, ldx, P.Wx2, cc0, cr, ci);
             } else {
                 gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx2, cc0, cr, ci);
             }
@@ -595,7 +530,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                     const float xtr = cr[t2][r] + rtr, xti = ci[t2][r] + rti;
                     sR[b] = (xtr - cur.alpha * rtr) * cur.inv1ma;
                     sR[b + 1] = (xti - cur.alpha * rti) * cur.inv1ma;
-                    if (!WS && P.dump) {
+                    if (P.dump) {
                         float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 1) * PBM * twoN;
                         dp[(4 * (lane >> 4) + r) * twoN + 2 * o] = sR[b];
                         dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = sR[b + 1];
@@ -616,19 +551,20 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             }
         }
         }
-        if constexpr (!WS) {
         __syncthreads();
         stamp(t, 4);
         // 4. denoiser (vamp.py:84)
+        PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
+        if (P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
+        PartAcc pa;
         if constexpr (KK > 16)
             denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
         else
             denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
-        }
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
-        if (!WS && P.dump) {   // xmmse and var after the denoiser (part_publish's barrier ordered the LDS writes)
+        if (P.dump) {   // xmmse and var after the denoiser (part_publish's barrier ordered the LDS writes)
             float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 2) * PBM * twoN;
             for (int e = tid; e < PBM * twoN; e += PWG) dp[e] = sX[(e / twoN) * ldr + e % twoN];
             for (int e = tid; e < PBM * N; e += PWG) dp[PBM * twoN + (e / N) * twoN + e % N] = vnew[e];
@@ -642,93 +578,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             }
         }
         stamp(t, 5);
-        // 5. batch scalars: every workgroup gathers and reduces every partial
-        PartAcc g;
-        if (!part_gather(grs, ((unsigned)t * nwg + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) {
-            aborted = 1;
-            break;
-        }
-        stamp(t, 6);
-        fixed = 0;
-        if (part_allnan(g)) {
-            // the reference's G is NaN / inf: every section of this iteration is NaN
-            if (!cur.fixed_all) {
-                const float qn = __int_as_float(0x7fc00000);
-                for (int e = tid; e < nrows * twoN; e += PWG) sX[(e / twoN) * ldr + e % twoN] = qn;
-                for (int e = tid; e < nrows * N; e += PWG) vnew[e] = qn;
-            }
-            g.sumvar = __longlong_as_double(0x7ff8000000000000LL);
-            g.notclose = 1;
-            fixed = -1;
-        } else if (part_danger(g)) {
-            // (a) exact float64 G over the candidate sections of every workgroup
-            const double G32 = g.maxabs, slack = logit_slack(G32);
-            const float inv = cur.inv_sigma2;
-            auto ldf = [=](int s) {
-                const int row = s / spr, sj = s - row * spr;
-                const float* rp = sR + row * ldr + 2 * sj * M;
-                return [=](int m, float& rr, float& ri, float& it) {
-                    rr = rp[2 * m]; ri = rp[2 * m + 1]; it = inv;
-                };
-            };
-            double gm = 0.0;
-            for (int s = tid; s < nrows * spr; s += PWG)
-                if ((double)sS[s] >= G32 - slack) gm = fmax(gm, section_absmax_f64(ldf(s), M, c64));
-            gm = group_max(gm, 64);
-            if (lane == 0) s_d[wave][0] = gm;
-            __syncthreads();
-            if (tid == 0) {
-                double m4 = 0.0;
-                for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
-                P.pxch[((size_t)t * nwg + wg) * 4 + 0] = m4;
-            }
-            if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) { aborted = 1; break; }
-            double G = 0.0;
-            for (int w = wg0; w < wg0 + P.wpe; ++w) G = fmax(G, P.pxch[((size_t)t * nwg + w) * 4 + 0]);
-            // (b) exact recompute of this workgroup's sections below the danger line
-            double dsum = 0.0;
-            int dnc = 0, cnt = 0;
-            for (int s = tid; s < nrows * spr; s += PWG) {
-                if (!((double)sM[s] - G < AMP_DANGER + slack)) continue;
-                ++cnt;
-                const int row = s / spr, sj = s - row * spr;
-                float* xp = sX + row * ldr + 2 * sj * M;
-                const int v0 = row * N + sj * M;
-                auto st = [&](int m, float xr, float xi, float var) {
-                    const float old = vnew[v0 + m];
-                    dsum += (double)var - (double)old;
-                    dnc += (torch_close(var, vprev[v0 + m]) ? 0 : 1) - (torch_close(old, vprev[v0 + m]) ? 0 : 1);
-                    xp[2 * m] = xr; xp[2 * m + 1] = xi;
-                    vnew[v0 + m] = var;
-                };
-                exact_section_f64<true>(ldf(s), st, M, c64, G);
-            }
-            dsum = group_sum(dsum, 64);
-            dnc = group_sum(dnc, 64);
-            cnt = group_sum(cnt, 64);
-            __syncthreads();
-            if (lane == 0) { s_d[wave][1] = dsum; s_d[wave][2] = (double)dnc; s_d[wave][3] = (double)cnt; }
-            __syncthreads();
-            if (tid == 0) {
-                double a = 0.0, b = 0.0, c = 0.0;
-                for (int w = 0; w < PWG / 64; ++w) { a += s_d[w][1]; b += s_d[w][2]; c += s_d[w][3]; }
-                P.pxch[((size_t)t * nwg + wg) * 4 + 1] = a;
-                P.pxch[((size_t)t * nwg + wg) * 4 + 2] = b;
-                P.pxch[((size_t)t * nwg + wg) * 4 + 3] = c;
-            }
-            if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) { aborted = 1; break; }
-            double a = 0.0, b = 0.0, c = 0.0;
-            for (int w = wg0; w < wg0 + P.wpe; ++w) {
-                const double* q = P.pxch + ((size_t)t * nwg + w) * 4;
-                a += q[1]; b += q[2]; c += q[3];
-            }
-            g.sumvar += a;   // (sum - old) + new, in float64
-            g.notclose = (uint32_t)((long long)g.notclose + (long long)b);
-            g.maxabs = G;
-            fixed = (int)c;
-        }
-        nx = vamp_advance(P, cur, g, fixed, t, scr, &s2l);
-        stamp(t, 7);
+        if (!exchange(t, vnew, vprev)) { aborted = 1; break; }
         if (nx.stopped || t + 1 == P.max_iter) break;
         cur = nx;
     }
@@ -757,9 +607,9 @@ int device_cu_count();
 
 // Launch path: persist_grid_launch (amp_host.h): a plain launch after an explicit co-residency
 // check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool XF = false, bool WS = false>
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC, H2, XF, WS>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC, H2>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
     // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
@@ -783,22 +633,17 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
     return persist_grid_launch("vamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
-// WS: the wave-specialized eight-wave form (K <= 16; 64-point alphabets run the four-wave form)
-template <int NT, int NWV, bool X3, int OCC = 1, bool H2 = false, bool XF = false, bool WS = false>
+template <int NT, int NWV, bool X3, int OCC = 1, bool H2 = false>
 static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC, H2, XF, WS>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC, H2, XF, WS>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV, AMP_KK4_DU, X3, OCC, H2, XF, WS>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC, H2, XF, WS>(P, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC, H2>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC, H2>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV, AMP_KK4_DU, X3, OCC, H2>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC, H2>(P, dc, st);
     case 16:
-        // experiment: sections in flight per lane group in the denoiser (AMP_DEN_U = 2 | 4 | 8;
-        // f32 engine only: 4 and 8 spill beside the bf16x3 GEMM's registers)
         // two sections in flight per lane group (4 and 8 measured no faster, and spill)
-        return persist_launch_t<NT, 16, NWV, X3 ? AMP_X3_DU : 2, X3, OCC, H2, XF, WS>(P, dc, st);
-    default:
-        if constexpr (WS) return persist_launch_t<NT, 64, 4, 1, X3, OCC, H2, XF>(P, dc, st);
-        else return persist_launch_t<NT, 64, NWV, 1, X3, OCC, H2, XF>(P, dc, st);
+        return persist_launch_t<NT, 16, NWV, X3 ? AMP_X3_DU : 2, X3, OCC, H2>(P, dc, st);
+    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC, H2>(P, dc, st);
     }
 }
 

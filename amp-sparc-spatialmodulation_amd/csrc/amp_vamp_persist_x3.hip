@@ -5,22 +5,7 @@
 
 namespace amp {
 
-// The wave-specialized eight-wave form (vamp_persist WS) where it applies: N = 256 or 128, K <= 16,
-// one section per GEMM wave and pass (M = 16 NC / 2: 32 at N = 256, 16 at N = 128, i.e. Na = 8);
-// AMP_VAMP_WS=0 keeps the four-wave form.
-bool vamp_persist_ws_ok(const VampK& P) {
-    static const bool off = [] {
-        const char* e = getenv("AMP_VAMP_WS");
-        return e && e[0] == '0';
-    }();
-    return !off && P.c.K <= 16 && ((P.N == 256 && P.M == 32) || (P.N == 128 && P.M == 16));
-}
-
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st) {
-    if (vamp_persist_ws_ok(P)) {
-        if (P.N == 256) return persist_launch_nt<8, 8, true, 1, false, false, true>(P, dc, st);
-        return persist_launch_nt<4, 8, true, 1, false, false, true>(P, dc, st);
-    }
     switch (P.N) {
     case 64:   // the two-per-CU build for every N = 64 launch, so that one epoch and side-by-side
                // epochs run the same arithmetic (bit-identical results, tests/test_gpu_epochs.py)

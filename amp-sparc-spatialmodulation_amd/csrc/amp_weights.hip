@@ -143,27 +143,6 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         }
         return;
     }
-    if (J.packed == WPACKX3F) {
-        // plain f32 planes of X (gemm_x3f splits them in registers): kap = J, ncp = O (complex counts)
-        const long tot = (long)J.ncp * J.kap;
-        for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
-            const int o = (int)(e / J.kap), j = (int)(e % J.kap);
-            float xr = 0.f, xi = 0.f;
-            if (o < J.O && j < J.J) {
-                const float2 v = J.src[o * J.so + j * J.sj];
-                xr = v.x;
-                xi = J.conj ? -v.y : v.y;
-                if (J.rowscale) {
-                    const float s = J.rowscale[o];
-                    xr = s * xr;
-                    xi = s * xi;
-                }
-            }
-            J.wt[x3f_index(o, j, 0, J.kap)] = xr;
-            J.wt[x3f_index(o, j, 1, J.kap)] = xi;
-        }
-        return;
-    }
     if (J.packed == WPACKH2) {
         // fp16x2 planes of X 2^ex (amp_persist.h gemm_h2): kap = J, ncp = O (complex counts).
         // |x| 2^ex >= 65520 leaves fp16's range: the piece is then inf, so the GEMM's result is
@@ -239,7 +218,7 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     long most = 0;
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
-        const bool planar = J.packed == WPACKX3 || J.packed == WPACKX3F || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2;
+        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2;
         AMP_REQUIRE((planar ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
                          (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||

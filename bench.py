@@ -299,7 +299,7 @@ def main():
              'f32': 'GEMMs on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32)'}[gname]
     # the fp16x2 engine forms y~ = (s Uh) y in its prologue when n == 2N (amp_vamp.hip): those
     # 8 B n k flops per trial belong to the launch then
-    ytil_in = persistent and gname in ('fp16x2', 'bf16x3') and Nr == 2 * Nt and os.environ.get('AMP_YTIL_IN_KERNEL') != '0'
+    ytil_in = persistent and gname == 'fp16x2' and Nr == 2 * Nt and os.environ.get('AMP_YTIL_IN_KERNEL') != '0'
     if persistent:
         kern, flops_launch = 'vamp_persist (whole iteration loop: 2 GEMMs + LMMSE + Onsager + denoiser per iteration' + \
             (', y~ GEMM in the prologue)' if ytil_in else ')'), 2.0 * flops_mv * T + (8.0 * Bp * Nr * k if ytil_in else 0.0)

@@ -112,9 +112,7 @@ typedef struct amp_vamp_args {
  *  X3    split precision: every f32 operand as three bf16 pieces (all 24 bits: the reference's
  *        c64 operand precision), six bf16 MFMA products per product (terms below 2^-24 relative
  *        dropped), f32 accumulation — the f32 GEMM's accuracy at 2.7x the MFMA rate (needs
- *        k == N, N % 64 == 0 and 160 KB of LDS).  At N = 128 / 256 the operators are streamed
- *        as plain f32 and split in registers (8 bytes per complex entry instead of 12;
- *        AMP_VAMP_X3F=0 keeps the pre-split planes);
+ *        k == N, N % 64 == 0 and 160 KB of LDS);
  *  H2    OPT-IN, narrower than the reference: every A row scaled by its own power of two, every
  *        value as two fp16 pieces (22 significant bits), three fp16 MFMA products per product
  *        (the 2^-22 lo.lo term dropped), f32 accumulation, the scales taken off exactly; the

@@ -34,7 +34,7 @@ Groups:
   g11 ISI / spatial coupling (Lin > 1, Lh > 1, tail) Loss dicts for VAMP, BAMP and SCAMP
   g12 vamp2.py damped VAMP: per-iteration traces and Loss dicts (sparc mode)
 
-Usage: python tests/golden/make_goldens.py [g1 g2 g3 g4 ...]
+Usage: python tests/golden/make_goldens.py [g1 g2 g3 g4 g4p g4pp ...]
 """
 import hashlib
 import json
@@ -815,6 +815,82 @@ def g4p(names=None):
                 json.dump(db, f, indent=1, sort_keys=True)
 
 
+PERTURBATIONS = (1.0 - 2.0 ** -23, 1.0 + 2.0 ** -22, 1.0 - 2.0 ** -22)
+
+
+def g4pp(names=None):
+    """Where the reference's own early exit moved under the one-ulp rerun (T != T_pert), three more
+    reruns with y scaled by PERTURBATIONS: `T_span` = [min, max] of T over all five runs, the bar
+    the GPU tests hold T to there (tests/test_gpu_vamp.py _check_T; round-3 review item 7)."""
+    path = os.path.join(HERE, 'g4_curves.json')
+    db = json.load(open(path))
+    for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
+        if names and name not in names:
+            continue
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = db[name]
+        for key in sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1]))):
+            rec = ent['points'][key]
+            if 'T_pert' not in rec or rec['T'] == rec['T_pert'] or 'T_span' in rec:
+                continue
+            seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
+            inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
+            assert sha(inp['x']) == rec['sha_x']
+            Ts = [rec['T'], rec['T_pert']]
+            for f in PERTURBATIONS:
+                y = inp['y'] * np.float32(f)
+                if algo == 'vamp':
+                    L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], y, inp['SNR'], inp['x'], inp['sym'],
+                                           inp['idx'])
+                elif algo == 'bamp':
+                    L = ref_bamp.BAMP(cfg)(inp['A'], y, inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                else:
+                    L = ref_scamp.SCAMP(cfg)(inp['W'], inp['A'], y, inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                Ts.append(float(np.asarray(L.loss['T'])))
+            rec['T_runs'] = Ts
+            rec['T_span'] = [min(Ts), max(Ts)]
+            print(name, key, 'T runs', Ts, flush=True)
+            with open(path, 'w') as f:
+                json.dump(db, f, indent=1, sort_keys=True)
+
+
+PERT_SEEDS = tuple(range(8))
+
+
+def g4pp_elem(names=None):
+    """More evidence where the reference's exit moved: eight reruns with every element of y moved
+    independently by -1, 0 or +1 float32 ulp (seeded), the closest model of a summation-order
+    change in the GEMMs.  Appended to `T_runs`; `T_span` widened to their [min, max]."""
+    path = os.path.join(HERE, 'g4_curves.json')
+    db = json.load(open(path))
+    for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
+        if names and name not in names:
+            continue
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = db[name]
+        for key in sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1]))):
+            rec = ent['points'][key]
+            if 'T_runs' not in rec or len(rec['T_runs']) > 5:
+                continue
+            seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
+            inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
+            assert sha(inp['x']) == rec['sha_x']
+            Ts = list(rec['T_runs'])
+            for ps in PERT_SEEDS:
+                g = torch.Generator().manual_seed(1000 + ps)
+                y0 = torch.as_tensor(inp['y'])
+                u = torch.randint(-1, 2, y0.shape, generator=g).to(torch.float32) * 2.0 ** -23
+                y = y0 * (1.0 + u).to(y0.dtype)
+                assert algo == 'vamp'
+                L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], y, inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+                Ts.append(float(np.asarray(L.loss['T'])))
+            rec['T_runs'] = Ts
+            rec['T_span'] = [min(Ts), max(Ts)]
+            print(name, key, 'T runs', Ts, flush=True)
+            with open(path, 'w') as f:
+                json.dump(db, f, indent=1, sort_keys=True)
+
+
 def g4(names=None):
     path = os.path.join(HERE, 'g4_curves.json')
     db = json.load(open(path)) if os.path.exists(path) else {}
@@ -878,6 +954,10 @@ if __name__ == '__main__':
             g10()
         elif w == 'g4p':
             g4p(names or None)
+        elif w == 'g4pp':
+            g4pp(names or None)
+        elif w == 'g4pe':
+            g4pp_elem(names or None)
         elif w == 'g11':
             g11()
         elif w == 'g12':

@@ -27,6 +27,9 @@ ALLOWED = [
     (r'_ZN3amp12vamp_persistILi2ELi16ELi4ELi2ELb1ELi2ELb[01]E', 'cfg2 16-QAM two-per-CU build'),
     # the other two-per-CU alphabets (QPSK / 8-PSK / 64-QAM at N = 64, side-by-side epochs)
     (r'_ZN3amp12vamp_persistILi2ELi(4|8|64)ELi4ELi[124]ELb1ELi2ELb[01]E', 'N = 64 two-per-CU builds'),
+    # 64-point alphabets at N = 256 (no BASELINE VAMP config): the wide denoiser's chunked table
+    # beside the N = 256 GEMM registers, 12 values reloaded once per iteration
+    (r'_ZN3amp12vamp_persistILi8ELi64ELi4ELi1ELb[01]ELi1ELb[01]E', '64-point alphabet at N = 256'),
 ]
 
 

@@ -23,12 +23,6 @@ for s in ${STEPS:-bench}; do
     bench_h2) run bench_h2 300 python3 bench.py --no-cpu-baseline --gemm h2 ;;
     bench_f32) run bench_f32 300 python3 bench.py --no-cpu-baseline --gemm f32 ;;
     trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;
-    bench_nows) run bench_nows 300 env AMP_VAMP_WS=0 python3 bench.py --no-cpu-baseline ;;
-    trace_nows) run trace_nows 300 env AMP_VAMP_WS=0 python3 tools/trace_persist.py --config cfg4 ;;
-    bench_x3pre) run bench_x3pre 300 env AMP_VAMP_X3F=0 python3 bench.py --no-cpu-baseline ;;
-    bench_x3f8) run bench_x3f8 300 env AMP_VAMP_X3F_WAVES=8 python3 bench.py --no-cpu-baseline ;;
-    trace_x3pre) run trace_x3pre 300 env AMP_VAMP_X3F=0 python3 tools/trace_persist.py --config cfg4 ;;
-    trace_x3f8) run trace_x3f8 300 env AMP_VAMP_X3F_WAVES=8 python3 tools/trace_persist.py --config cfg4 ;;
     trace_h2) run trace_h2 300 env AMP_VAMP_GEMM=h2 python3 tools/trace_persist.py --config cfg4 ;;
     configs) run configs 600 python3 tools/configs_bench.py ;;
     tests_vamp) run tests_vamp 900 $PYT tests/test_gpu_vamp.py -m gpu ;;
@@ -39,6 +33,8 @@ for s in ${STEPS:-bench}; do
     occ2) run occ2_prod 300 python3 tools/occ2_repro.py 10 &&
           run occ2_pk4 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du4.so python3 tools/occ2_repro.py 10 &&
           run occ2_pk2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du2.so python3 tools/occ2_repro.py 10 ;;
+    ttrace) run ttrace 600 python3 tools/t_trace.py --save 11,12 ;;
+    tprobe) run tprobe 300 python3 tools/t_probe.py ;;
     tests_vdef) run tests_vdef 900 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2" ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     profile) run profile 900 bash tools/profile.sh ;;
