@@ -891,6 +891,85 @@ def g4pp_elem(names=None):
                 json.dump(db, f, indent=1, sort_keys=True)
 
 
+def g4pp_den(names=None):
+    """Where the reference's exit moved: eight reruns on the UNPERTURBED inputs with every value of
+    the denoiser's exponential (vamp.py:110, torch.exp, float64 in the reference) moved by a random
+    relative amount within +-2^-22 (seeded) — the size of a float32 evaluation of that denoiser,
+    which is what every GPU engine runs (amp_denoise.h).  Appended to `T_runs`, `T_span` widened."""
+    path = os.path.join(HERE, 'g4_curves.json')
+    db = json.load(open(path))
+    exp0 = torch.exp
+    for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
+        if names and name not in names:
+            continue
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ent = db[name]
+        for key in sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1]))):
+            rec = ent['points'][key]
+            if 'T_runs' not in rec or 'T_runs_den' in rec:
+                continue
+            seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
+            inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
+            assert sha(inp['x']) == rec['sha_x'] and algo == 'vamp'
+            Td = []
+            for ps in PERT_SEEDS:
+                g = torch.Generator().manual_seed(2000 + ps)
+
+                def exp_f32(x, g=g):
+                    e = exp0(x)
+                    u = (torch.rand(e.shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -22
+                    return e * (1 + u).to(e.dtype)
+                torch.exp = exp_f32
+                try:
+                    L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'],
+                                           inp['idx'])
+                finally:
+                    torch.exp = exp0
+                Td.append(float(np.asarray(L.loss['T'])))
+            rec['T_runs_den'] = Td
+            Ts = rec['T_runs'] + Td
+            rec['T_span'] = [min(Ts), max(Ts)]
+            print(name, key, 'T runs (denoiser exp +-2^-22)', Td, flush=True)
+            with open(path, 'w') as f:
+                json.dump(db, f, indent=1, sort_keys=True)
+
+
+def g4pp_f32den(names=None):
+    """Where the reference's exit moved: the oracle's restatement of the reference (pinned to it
+    by g1-g4) run once more with its denoiser in the GPU engines' float32 arithmetic
+    (oracle.block_denoise_f32; the reference's denoiser is float64).  At noise-limited points the
+    float32 rounding keeps the batch mean var in a period-2 cycle in its last bits, which the exp
+    of the logits (|xi| ~ 10) amplifies past allclose's rtol in a few dozen elements, so the exit
+    never fires.  `T_f32den` joins `T_span`."""
+    sys.path.insert(0, os.path.join(HERE, '..', '..'))
+    from oracle import OracleConfig
+    from oracle import amp_oracle as O
+    path = os.path.join(HERE, 'g4_curves.json')
+    db = json.load(open(path))
+    for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
+        if names and name not in names:
+            continue
+        cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
+        ocfg = OracleConfig(Nt, Na, Nr, B=B, alphabet=alph, iterations=iters)
+        ent = db[name]
+        for key in sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1]))):
+            rec = ent['points'][key]
+            if 'T_runs' not in rec or 'T_f32den' in rec:
+                continue
+            seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
+            inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
+            assert sha(inp['x']) == rec['sha_x'] and algo == 'vamp'
+            c = lambda t: np.asarray(t)[..., 0] if np.asarray(t).ndim == 3 else np.asarray(t)  # noqa: E731
+            out = O.vamp_detect(c(inp['U']), c(inp['s']), c(inp['Vh']), c(inp['y']), float(inp['SNR']), ocfg,
+                                den32=True)
+            rec['T_f32den'] = float(out['T'])
+            Ts = rec['T_runs'] + rec.get('T_runs_den', []) + [rec['T_f32den']]
+            rec['T_span'] = [min(Ts), max(Ts)]
+            print(name, key, 'T with a float32 denoiser', out['T'], 'span', rec['T_span'], flush=True)
+            with open(path, 'w') as f:
+                json.dump(db, f, indent=1, sort_keys=True)
+
+
 def g4(names=None):
     path = os.path.join(HERE, 'g4_curves.json')
     db = json.load(open(path)) if os.path.exists(path) else {}
@@ -958,6 +1037,10 @@ if __name__ == '__main__':
             g4pp(names or None)
         elif w == 'g4pe':
             g4pp_elem(names or None)
+        elif w == 'g4pd':
+            g4pp_den(names or None)
+        elif w == 'g4pf':
+            g4pp_f32den(names or None)
         elif w == 'g11':
             g11()
         elif w == 'g12':

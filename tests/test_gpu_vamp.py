@@ -307,9 +307,13 @@ def _check_T(got, ref, max_iter, ver_ref=0.0, ref_pert=None, ref_span=None):
     * both runs agree: exact where the exit is well conditioned (the loop ran to the end or
       stopped within 3 iterations), else within one iteration;
     * the reference itself moved (its exit is decided by rounding): within one iteration of the
-      span of its own runs — `ref_span`, the [min, max] of T over five reference runs (y scaled by
-      1, 1 + 2^-23, 1 - 2^-23, 1 + 2^-22, 1 - 2^-22: make_goldens.g4pp) where the goldens hold it,
-      else the two runs'.
+      span of the evidence the goldens hold for that point (`ref_span`, make_goldens.py g4pp*):
+      T of the reference on y scaled by 1, 1 +- 2^-23, 1 +- 2^-22 and on eight seeded element-wise
+      one-ulp moves of y; T of the reference with its denoiser's exp moved by a seeded relative
+      +-2^-22 (eight runs); and T of the oracle's restatement with the denoiser in the GPU
+      engines' float32 arithmetic (oracle.block_denoise_f32), which at the 0 dB cfg4-QPSK points
+      keeps the batch mean var in a period-2 cycle in its last bits and never exits.
+      Else (goldens without the span) the two runs'.
     Without it (goldens that predate the rerun): exact at the end / by 3 iterations, the
     noise-limited range where the detector fails (VER > 0.5), else +-5."""
     if ref_pert is not None:

@@ -34,6 +34,11 @@ for s in ${STEPS:-bench}; do
           run occ2_pk4 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du4.so python3 tools/occ2_repro.py 10 &&
           run occ2_pk2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du2.so python3 tools/occ2_repro.py 10 ;;
     ttrace) run ttrace 600 python3 tools/t_trace.py --save 11,12 ;;
+    pkocc2) run pkocc2 300 tools/ubench/bin/pk_occ2 20 ;;
+    gemms) run gemm_x3 120 tools/ubench/bin/gemm_x3 && run gemm_h2 120 tools/ubench/bin/gemm_h2 &&
+           run gemm_i8 120 tools/ubench/bin/gemm_i8 ;;
+    pkdpp) run pkdpp 300 tools/ubench/bin/pk_dpp 3 ;;
+    gi8) run gemm_i8 120 tools/ubench/bin/gemm_i8 ;;
     tprobe) run tprobe 300 python3 tools/t_probe.py ;;
     tests_vdef) run tests_vdef 900 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2" ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
