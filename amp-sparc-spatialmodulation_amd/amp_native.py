@@ -41,7 +41,7 @@ class AmpCounts(C.Structure):
 
 
 ENGINE_AUTO, ENGINE_LAUNCHES, ENGINE_PERSISTENT = 0, 1, 2   # amp_vamp_args.engine
-GEMM_AUTO, GEMM_F32, GEMM_X3, GEMM_H2 = 0, 1, 2, 3              # amp_vamp_args.gemm
+GEMM_AUTO, GEMM_F32, GEMM_X3, GEMM_H2, GEMM_I8 = 0, 1, 2, 3, 4   # amp_vamp_args.gemm
 
 
 class AmpVampArgs(C.Structure):

@@ -87,6 +87,17 @@ __host__ __device__ __forceinline__ size_t h2_index(int o, int j, int f, int J) 
     return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 4 + f) * 64 + lane) * 8 + (kk & 7);
 }
 
+// The same for the int8x4 form (gemm_i8, amp_persist.h): X[o][j] 2^(30 - e_o) rounded to a 31-bit
+// integer, written as four balanced base-256 digits; 16-column tile ct = o >> 4, group g = j >> 6
+// (J % 64 == 0), plane f (0-3: Re digits top first, 4-7: Im), lane (o & 15) + 16 ((j & 63) >> 4),
+// byte j & 15: one 16-byte buffer load per lane and plane (the i8 16x16x64 fragment).  The column
+// exponents e_o follow the planes as ints (amp_persist.h i8_exp_offset bytes in).
+__host__ __device__ __forceinline__ size_t i8_index(int o, int j, int f, int J) {
+    const int kk = j & 63;
+    const int lane = (o & 15) + 16 * (kk >> 4);
+    return ((((size_t)(o >> 4) * (J >> 6) + (j >> 6)) * 8 + f) * 64 + lane) * 16 + (kk & 15);
+}
+
 // XCD-aware tile order.  Workgroups are dispatched in linear order (x fastest) round-robin over
 // the 8 XCDs, each with its own 4 MB L2.  The row-block-fastest grid would make every XCD sweep
 // ALL column blocks, i.e. the whole packed weight (8 MB for BAMP's H at cfg5) through each L2.

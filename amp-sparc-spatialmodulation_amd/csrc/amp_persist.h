@@ -10,6 +10,8 @@
 // Every spin is bounded (2 s) and raises an abort word that releases every other workgroup.
 #pragma once
 
+#include <cfloat>
+
 #include "amp_common.h"
 
 namespace amp {
@@ -428,6 +430,218 @@ __device__ __forceinline__ void gemm_h2(const unsigned short* sP, int ldx, const
                     ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + RR) * 4 + f) * 1024, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ---- split-precision complex GEMM (int8x4: block fixed point on the integer matrix cores) ----
+// Every A row (r~, then w) carries its own power-of-two scale, every operator column its own:
+// with e the smallest exponent such that the row's (column's) max |value| < 2^e, a value v becomes
+// the 31-bit integer V = rint(v 2^(30 - e)) (|V| < 2^30), written as four balanced base-256 digits
+// d0 .. d3 (V = d0 2^24 + d1 2^16 + d2 2^8 + d3; |d0| <= 64, the others in [-128, 127]): byte k of
+// digit plane s is the low byte of (V + c_s) >> 8 (3 - s), c = 0x808080, 0x8080, 0x80, 0.  A
+// product keeps the digit pairs i + j <= 3 (ten of the sixteen), summed per level s = i + j on
+// v_mfma_i32_16x16x64_i8 — exact in int32 (a level sum is below 2^25 for K <= 512) — and the levels
+// are combined in f32 at the end (smallest first), then scaled by 2^(e_row + e_col - 12).
+// Operands: 31 significant bits relative to the row / column maximum, i.e. at least 24 bits for
+// every element down to 2^-7 of its row's (column's) largest; the dropped pairs (i + j >= 4) are
+// below 2^-30 of (row max . column max).  Measured on the cfg4 GEMM shape against a float64 sum
+// (tools/ubench/gemm_i8_ubench.hip): max |error| 6.0e-8, a sequential f32 sum's 1.4e-6, bf16x3's
+// 1.3e-6.  8 bytes per complex operator entry (bf16x3: 12) and 40 i8 MFMAs per complex tile and
+// 64-deep group (bf16x3: 48 bf16 MFMAs of the same cycles for the same depth).
+// A non-finite value anywhere in an A row makes the whole row's result NaN (the row's factor is
+// NaN; its digits are zero).  The reference's matmul gives NaN there for a NaN input (every output
+// of the row sums over it) and +-inf or NaN for an infinite one.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+#ifndef AMP_I8_APF
+#define AMP_I8_APF 1   // gemm_i8: A fragments read one step ahead
+#endif
+// byte offset of the column exponents behind an i8-packed [O][J] operator's planes
+__host__ __device__ __forceinline__ size_t i8_exp_offset(int O, int J) { return (size_t)O * J * 8; }
+
+// bytes per LDS row of one digit plane: N + 16 (rows 16 bytes apart in bank order: the
+// 16-row fragment reads and the 8-byte row stores are conflict-free for N % 64 == 0)
+__host__ __device__ __forceinline__ int i8_ldb(int N) { return N + 16; }
+__host__ __device__ __forceinline__ int i8_plane_floats(int N) { return 8 * 16 * i8_ldb(N) / 4; }
+
+// The exponent e with m < 2^e for a finite m > 0 (0 for m == 0); INT_MAX for a non-finite m.
+__device__ __forceinline__ int i8_row_exp(float m) {
+    if (!(m <= FLT_MAX)) return 0x7fffffff;
+    if (!(m > 0.f)) return 0;
+    return __builtin_amdgcn_frexp_expf(m);
+}
+// |v| as the row maximum's contribution: a NaN counts as +inf (fmaxf would drop it)
+__device__ __forceinline__ float i8_absmax(float m, float v) {
+    const float a = fabsf(v);
+    return fmaxf(m, a <= FLT_MAX ? a : INFINITY);
+}
+// 2^(e - 12) as the row factor of gemm_i8's epilogue (NaN for a non-finite row)
+__device__ __forceinline__ float i8_row_factor(int e) {
+    return e == 0x7fffffff ? __int_as_float(0x7fc00000) : __builtin_amdgcn_ldexpf(1.0f, e - 12);
+}
+// v -> V = rint(v 2^(30 - e)) (0 for a non-finite row)
+__device__ __forceinline__ int i8_fix(float v, int e) {
+    return e == 0x7fffffff ? 0 : (int)__builtin_rintf(__builtin_amdgcn_ldexpf(v, 30 - e));
+}
+// four integers -> one dword of digit plane s (byte i = digit s of V_i)
+template <int S>
+__device__ __forceinline__ unsigned i8_digits4(int v0, int v1, int v2, int v3) {
+    constexpr int sh = 8 * (3 - S);
+    constexpr int c = S == 0 ? 0x808080 : S == 1 ? 0x8080 : S == 2 ? 0x80 : 0;
+    const unsigned y0 = (unsigned)((v0 + c) >> sh), y1 = (unsigned)((v1 + c) >> sh);
+    const unsigned y2 = (unsigned)((v2 + c) >> sh), y3 = (unsigned)((v3 + c) >> sh);
+    const unsigned lo = __builtin_amdgcn_perm(y1, y0, 0x0c0c0400u);   // [y0.b0, y1.b0, 0, 0]
+    const unsigned hi = __builtin_amdgcn_perm(y3, y2, 0x0c0c0400u);
+    return lo | (hi << 16);
+}
+// two integers -> one 16-bit word of digit plane s
+template <int S>
+__device__ __forceinline__ unsigned short i8_digits2(int v0, int v1) {
+    constexpr int sh = 8 * (3 - S);
+    constexpr int c = S == 0 ? 0x808080 : S == 1 ? 0x8080 : S == 2 ? 0x80 : 0;
+    return (unsigned short)__builtin_amdgcn_perm((unsigned)((v1 + c) >> sh), (unsigned)((v0 + c) >> sh), 0x0c0c0400u);
+}
+
+// Eight consecutive complex values of one row -> the eight digit planes (Re d0..d3, Im d0..d3) of
+// an i8 A operand: plane f, row `row`, bytes j0 .. j0+7 (one 8-byte store each).  e: the row's
+// exponent (i8_row_exp).
+__device__ __forceinline__ void i8_store8(signed char* sB, int ldb, int row, int j0, const float (&re)[8],
+                                          const float (&im)[8], int e) {
+    int vr[8], vi[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) { vr[h] = i8_fix(re[h], e); vi[h] = i8_fix(im[h], e); }
+    signed char* p = sB + pl_opaque(row) * ldb + j0;
+    const int pl = 16 * ldb;
+#define AMP_I8ST(S)                                                                                          \
+    *reinterpret_cast<uint2*>(p + (S) * pl) =                                                                \
+        make_uint2(i8_digits4<S>(vr[0], vr[1], vr[2], vr[3]), i8_digits4<S>(vr[4], vr[5], vr[6], vr[7]));     \
+    *reinterpret_cast<uint2*>(p + (4 + (S)) * pl) =                                                          \
+        make_uint2(i8_digits4<S>(vi[0], vi[1], vi[2], vi[3]), i8_digits4<S>(vi[4], vi[5], vi[6], vi[7]));
+    AMP_I8ST(0) AMP_I8ST(1) AMP_I8ST(2) AMP_I8ST(3)
+#undef AMP_I8ST
+}
+
+// One accumulator tile's values (this lane: rows 4*(lane>>4) + r, complex column o; already
+// fixed-point integers) -> the eight digit planes as 16-bit words of column pairs: the even lane
+// of each pair writes rows +0 / +1, the odd lane rows +2 / +3 (one DPP swap per sent value).
+__device__ __forceinline__ void i8_store_acc(signed char* sB, int ldb, int o, const int (&vr)[4], const int (&vi)[4]) {
+    const int lane = pl_opaque((int)threadIdx.x) & 63;
+    const bool odd = (lane & 1) != 0;
+    int gr[2], gi[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        gr[h] = __builtin_amdgcn_update_dpp(0, odd ? vr[h] : vr[2 + h], 0xB1, 0xF, 0xF, false);
+        gi[h] = __builtin_amdgcn_update_dpp(0, odd ? vi[h] : vi[2 + h], 0xB1, 0xF, 0xF, false);
+    }
+    const int row0 = 4 * (lane >> 4) + (odd ? 2 : 0);
+    const int pl = 16 * ldb;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        signed char* p = sB + (row0 + h) * ldb + (o & ~1);
+        const int mr = odd ? vr[2 + h] : vr[h], mi = odd ? vi[2 + h] : vi[h];
+        const int r0 = odd ? gr[h] : mr, r1 = odd ? mr : gr[h];
+        const int i0 = odd ? gi[h] : mi, i1 = odd ? mi : gi[h];
+        *reinterpret_cast<unsigned short*>(p + 0 * pl) = i8_digits2<0>(r0, r1);
+        *reinterpret_cast<unsigned short*>(p + 1 * pl) = i8_digits2<1>(r0, r1);
+        *reinterpret_cast<unsigned short*>(p + 2 * pl) = i8_digits2<2>(r0, r1);
+        *reinterpret_cast<unsigned short*>(p + 3 * pl) = i8_digits2<3>(r0, r1);
+        *reinterpret_cast<unsigned short*>(p + 4 * pl) = i8_digits2<0>(i0, i1);
+        *reinterpret_cast<unsigned short*>(p + 5 * pl) = i8_digits2<1>(i0, i1);
+        *reinterpret_cast<unsigned short*>(p + 6 * pl) = i8_digits2<2>(i0, i1);
+        *reinterpret_cast<unsigned short*>(p + 7 * pl) = i8_digits2<3>(i0, i1);
+    }
+}
+
+// C[16 x 16 NT] (complex, f32, fully scaled) = A[16 x 64 G] (complex, eight int8 digit planes in
+// LDS, row stride ldb bytes) . X^T, X packed by i8_index with its column exponents behind the
+// planes.  Tile-outer: complex column tile t runs all G groups before tile t + 1, so one tile's
+// level sums are live (P = Ar.Xr, Q = Ai.Xi, C = Ar.Xi + Ai.Xr, four levels each; Re = P - Q in
+// int32, exact) and leave as f32; the A fragments are re-read from LDS per tile (one group ahead),
+// the operator streams through a ring of D (tile, group) slots in (t, g) order.
+// rowf[r]: this lane's rows' factors (i8_row_factor).  Accumulator t, register r: row
+// 4*(lane>>4) + r, complex column 16*(ct0 + t) + (lane & 15).
+template <int NT, int G, int D = 2, bool APF = AMP_I8_APF>
+__device__ __forceinline__ void gemm_i8(const signed char* sB, int ldb, const void* __restrict__ wq, int O, int ct0,
+                                        const float (&rowf)[4], f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
+    constexpr int NS = NT * G;
+    constexpr int DD = NS < D ? NS : D;
+    const int lane = threadIdx.x & 63;
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 8 * 1024, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = pl_opaque(lane * 16);   // opaque: the first ring loads stay inside the caller's loop
+    const int* ecol = reinterpret_cast<const int*>((const char*)wq + i8_exp_offset(O, 64 * G));
+    u32x4 ring[DD][8];
+#pragma unroll
+    for (int d = 0; d < DD; ++d)
+#pragma unroll
+        for (int f = 0; f < 8; ++f) ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, (d * 8 + f) * 1024, 0);
+    const int ln = pl_opaque(lane);
+    const signed char* ap = sB + (ln & 15) * ldb + 16 * (ln >> 4);
+    u32x4 an[8];
+    if constexpr (APF) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldb);
+    }
+    i32x4 P[4], Q[4], C[4];
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+        const int t = st / G, g = st % G, d = st % DD;
+        __builtin_amdgcn_sched_barrier(0);   // no motion across steps: one tile's sums live at a time
+        if (g == 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) { P[s] = i32x4{0, 0, 0, 0}; Q[s] = P[s]; C[s] = P[s]; }
+        }
+        // the same group's fragments are re-read for every tile: the offsets are pinned (opaque)
+        // so that the compiler does not keep all G groups' fragments live across the tiles
+        u32x4 a[8];
+        if constexpr (APF) {
+#pragma unroll
+            for (int f = 0; f < 8; ++f) a[f] = an[f];
+            if (st + 1 < NS) {
+                const int off = pl_opaque(64 * ((st + 1) % G));
+#pragma unroll
+                for (int f = 0; f < 8; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldb + off);
+            }
+        } else {
+            const int off = pl_opaque(64 * g);
+#pragma unroll
+            for (int f = 0; f < 8; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldb + off);
+        }
+        const u32x4* w = ring[d];   // w[0..3]: Re digits, w[4..7]: Im digits
+#define AMP_MI(acc_, x, y) \
+    acc_ = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, x), __builtin_bit_cast(i32x4, y), acc_, 0, 0, 0)
+#pragma unroll
+        for (int s = 3; s >= 0; --s)
+#pragma unroll
+            for (int i = 0; i <= s; ++i) {
+                AMP_MI(P[s], a[i], w[s - i]);          // Ar Xr
+                AMP_MI(Q[s], a[4 + i], w[4 + s - i]);  // Ai Xi
+                AMP_MI(C[s], a[i], w[4 + s - i]);      // Ar Xi
+                AMP_MI(C[s], a[4 + i], w[s - i]);      // Ai Xr
+            }
+#undef AMP_MI
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + DD < NS) {
+#pragma unroll
+            for (int f = 0; f < 8; ++f)
+                ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((st + DD) * 8 + f) * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (g == G - 1) {
+            const float cf = __builtin_amdgcn_ldexpf(1.0f, ecol[16 * (ct0 + t) + (lane & 15)]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float vr = (float)(P[3][r] - Q[3][r]), vi = (float)C[3][r];
+                vr = fmaf(vr, 0x1p-8f, (float)(P[2][r] - Q[2][r]));
+                vi = fmaf(vi, 0x1p-8f, (float)C[2][r]);
+                vr = fmaf(vr, 0x1p-8f, (float)(P[1][r] - Q[1][r]));
+                vi = fmaf(vi, 0x1p-8f, (float)C[1][r]);
+                vr = fmaf(vr, 0x1p-8f, (float)(P[0][r] - Q[0][r]));
+                vi = fmaf(vi, 0x1p-8f, (float)C[0][r]);
+                cr[t][r] = vr * rowf[r] * cf;
+                ci[t][r] = vi * rowf[r] * cf;
+            }
+        }
     }
 }
 

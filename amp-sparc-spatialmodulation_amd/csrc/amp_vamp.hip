@@ -421,16 +421,26 @@ static bool gemm_h2_requested() {
 // the reference's c64 operand precision (vamp.py:67, 72).  fp16x2 (two 11-bit pieces, 22 bits,
 // the 2^-22 lo.lo term dropped) is narrower than the reference and runs only when asked for
 // (AMP_GEMM_H2 or AMP_VAMP_GEMM=h2).
+// AMP_GEMM_I8 (3): int8x4 block fixed point — 31-bit operands per row / column, more accurate than
+// an f32 sum (amp_persist.h gemm_i8).
+static bool gemm_i8_requested() {   // AMP_VAMP_GEMM=i8: AUTO picks int8x4 (A/B runs)
+    static const bool v = [] {
+        const char* e = getenv("AMP_VAMP_GEMM");
+        return e && e[0] == 'i';
+    }();
+    return v;
+}
 static int vamp_gemm_mode(int gemm, bool fits) {
+    if (gemm == AMP_GEMM_I8) return 3;
     if (gemm == AMP_GEMM_H2) return 2;
     if (gemm == AMP_GEMM_X3) return 1;
     if (gemm == AMP_GEMM_F32 || !fits || gemm_f32_requested()) return 0;
-    return gemm_h2_requested() ? 2 : 1;
+    return gemm_h2_requested() ? 2 : gemm_i8_requested() ? 3 : 1;
 }
 
 int vamp_gemm_select(const amp_dims* d, int k, int gemm) {
     const bool fits = vamp_persist_x3_fits(d->N, k, d->L);
-    if ((gemm == AMP_GEMM_X3 || gemm == AMP_GEMM_H2) && !fits) return 0;
+    if ((gemm == AMP_GEMM_X3 || gemm == AMP_GEMM_H2 || gemm == AMP_GEMM_I8) && !fits) return 0;
     return vamp_gemm_mode(gemm, fits);
 }
 
@@ -468,9 +478,9 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.trace = nullptr;
     P.c = to_const(c);
     c64 = to_const64(c);
-    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_H2, "amp_vamp: gemm %d", a->gemm);
+    AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_I8, "amp_vamp: gemm %d", a->gemm);
     const bool x3_fits = vamp_persist_x3_fits(d->N, a->k, d->L);
-    AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2) || x3_fits,
+    AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2 && a->gemm != AMP_GEMM_I8) || x3_fits,
                 "amp_vamp: the split-precision engines need k == N, N %% 64 == 0 and "
                 "their LDS carve within 160 KB (N = %d, L = %d)", d->N, d->L);
     P.x3 = vamp_gemm_mode(a->gemm, x3_fits);
@@ -571,7 +581,7 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     const bool yk = P.ytil_in_kernel != 0;
     CWeightJob j[3];
     if (P.x3) {
-        const int pk = P.x3 == 2 ? WPACKH2 : WPACKX3;
+        const int pk = P.x3 == 3 ? WPACKI8 : P.x3 == 2 ? WPACKH2 : WPACKX3;
         //   q = Vh r~    (vamp.py:67)    X[o][j] = Vh[o][j],           o < k, j < N   (bf16x3 / fp16x2 planes)
         j[0] = CWeightJob{(const float2*)a->Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)P.Wx1, P.N, P.k, pk};
         //   V (x~ - q)   (vamp.py:19,72) X[o][j] = conj(Vh[j][o]),     o < N, j < k
@@ -679,10 +689,10 @@ int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const 
 }
 
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
-    if (!d || k <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_H2) return AMP_E_ARG;
+    if (!d || k <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_I8) return AMP_E_ARG;
     const bool fits = vamp_persist_x3_fits(d->N, k, d->L);
-    if ((gemm == AMP_GEMM_X3 || gemm == AMP_GEMM_H2) && !fits) return AMP_E_ARG;
-    static const int code[3] = {AMP_GEMM_F32, AMP_GEMM_X3, AMP_GEMM_H2};
+    if ((gemm == AMP_GEMM_X3 || gemm == AMP_GEMM_H2 || gemm == AMP_GEMM_I8) && !fits) return AMP_E_ARG;
+    static const int code[4] = {AMP_GEMM_F32, AMP_GEMM_X3, AMP_GEMM_H2, AMP_GEMM_I8};
     return code[vamp_gemm_mode(gemm, fits)];
 }
 
@@ -784,7 +794,7 @@ int amp_vamp_max_epochs(const amp_dims* d, int32_t k) {
 }
 
 int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
-    if (!d || k <= 0 || d->B <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_H2) return 0;
+    if (!d || k <= 0 || d->B <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_I8) return 0;
     return vamp_persist_max_epochs(d, k, device_cu_count(), gemm);
 }
 

@@ -86,7 +86,9 @@ bool persist_wg2() {
 }
 // gemm_mode: the persistent GEMM arithmetic of the call (vamp_gemm_select: 0 f32, 1 bf16x3,
 // 2 fp16x2); only the split-precision engines have a two-per-CU instantiation
-static int persist_wg_cap(int N, int gemm_mode) { return (N == 64 && gemm_mode != 0 && persist_wg2()) ? 2 : 1; }
+static int persist_wg_cap(int N, int gemm_mode) {
+    return (N == 64 && (gemm_mode == 1 || gemm_mode == 2) && persist_wg2()) ? 2 : 1;
+}
 
 int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu, int gemm) {
     const int gemm_mode = vamp_gemm_select(d, k, gemm);
@@ -110,6 +112,7 @@ bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs, int ge
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st);
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_x3.hip
 int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_h2.hip
+int persist_dispatch_i8(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_i8.hip
 
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
@@ -127,6 +130,7 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
 static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) {
     // the barrier words were zeroed by the prepare launch; the granules carry generation tags
     // NT = 2N / (16 * waves) column tiles of 16 per wave (both GEMMs are 2N x 2N: k == N)
+    if (P.x3 == 3) return persist_dispatch_i8(P, dc, st);
     if (P.x3 == 2) return persist_dispatch_h2(P, dc, st);
     if (P.x3) return persist_dispatch_x3(P, dc, st);
     switch (P.N) {

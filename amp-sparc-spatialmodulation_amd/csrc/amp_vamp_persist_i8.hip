@@ -1,0 +1,20 @@
+// amp_vamp_persist_i8.hip — the persistent VAMP engine with both per-iteration GEMMs in the
+// split-precision int8x4 form (amp_persist.h gemm_i8: block fixed point on the integer matrix
+// cores, per-row / per-column exponents); its own translation unit so that it compiles in parallel
+// with the other instantiations.  One workgroup per CU at every N.
+#include "amp_vamp_persist_kernel.h"
+
+namespace amp {
+
+int persist_dispatch_i8(const VampK& P, const DecConst& dc, hipStream_t st) {
+    switch (P.N) {
+    case 64: return persist_launch_nt<2, 4, true, 1, false, true>(P, dc, st);
+    case 128: return persist_launch_nt<4, 4, true, 1, false, true>(P, dc, st);
+    case 256: return persist_launch_nt<8, 4, true, 1, false, true>(P, dc, st);
+    default: break;
+    }
+    set_error("vamp_persist (int8x4): N = %d not supported", P.N);
+    return AMP_E_ARG;
+}
+
+}  // namespace amp

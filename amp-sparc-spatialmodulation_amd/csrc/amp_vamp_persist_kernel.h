@@ -64,9 +64,13 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // H2 (with X3): the split-precision GEMMs in the fp16x2 form (gemm_h2: four A planes, the operators
 // h2-packed); every A row (r~, then w) is scaled by its own power of two (h2_row_exp) before the
 // split and the accumulators are scaled back by 2^-(e_row + H2_EX).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
+// I8 (with X3): the split-precision GEMMs in the int8x4 form (gemm_i8: eight int8 digit planes of
+// the A operand, each row with its own exponent; the operators i8-packed with per-column
+// exponents); the results come out of the GEMM fully scaled.
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
     static_assert(!X3 || (NWV == 4 && NT % 2 == 0), "X3: four waves, whole complex tiles");
+    static_assert(!(H2 && I8) && (!I8 || X3), "I8: a split-precision form of its own");
     constexpr bool PKDEN = (OCC * NWV / 4 == 1) || AMP_OCC2_PK;   // packed denoiser only at one wave per SIMD
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
@@ -99,6 +103,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     const int cc0 = wave * NC;                 // X3: this wave's complex 16-column tiles
     unsigned short* sP = reinterpret_cast<unsigned short*>(sA);
     const int ldx = x3_ldx(N);
+    signed char* sB = reinterpret_cast<signed char*>(sA);   // I8: the digit planes
+    const int ldb = i8_ldb(N);
 
     // y~ rows and s^2 of this wave's GEMM1 columns, in the accumulator layout
     // (X3: yt[2t] / yt[2t+1] = Re / Im of complex tile t, s2c[t] its s^2)
@@ -166,6 +172,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         __syncthreads();   // the planes region becomes the Tracker's state
       }
     } else if (X3) {
+      if constexpr (!I8) {   // (I8 reads y~ back every iteration)
 #pragma unroll
         for (int t = 0; t < NC; ++t) {
             const int o = 16 * (cc0 + t) + (lane & 15);
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 yt[2 * t + 1][r] = in ? P.ytil[(size_t)(row0 + row) * twok + 2 * o + 1] : 0.f;
             }
         }
+      }
     } else if (P.ytil_in_kernel) {
         // y~ = (s Uh) y (vamp.py:22) for this workgroup's rows: y staged in LDS over the A/R/X
         // region (row stride 2n + 4 = 4N + 4), GEMM on the packed s Uh operand (K = 2n = 4N)
@@ -328,7 +336,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         const float* vprev = lds + ((t & 1) ? Y.offV0 : Y.offV1);
         float* vnew = lds + ((t & 1) ? Y.offV1 : Y.offV0);
         // 1. A <- r~ (vamp.py:91; t = 0: dxdr 0, normScalar 1)
-        if constexpr (H2) {
+        if constexpr (H2 || I8) {
             // r~ rows in registers (item e: row e % PBM == tid % PBM, 8 complex values), the
             // row's max |value| over the workgroup, then the scaled split
             constexpr int IPT = (NT + 3) / 4;             // items per thread: PBM N / 8 / PWG
@@ -353,7 +361,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                     im[i][2 * h + 1] = (x.w - cur.dxdr_prev * q.w) * cur.ns_prev;
                 }
 #pragma unroll
-                for (int h = 0; h < 8; ++h) m = fmaxf(m, fmaxf(fabsf(re[i][h]), fabsf(im[i][h])));
+                for (int h = 0; h < 8; ++h) {
+                    if constexpr (I8) m = i8_absmax(i8_absmax(m, re[i][h]), im[i][h]);
+                    else m = fmaxf(m, fmaxf(fabsf(re[i][h]), fabsf(im[i][h])));
+                }
             }
             m = fmaxf(m, __shfl_xor(m, 16));
             m = fmaxf(m, __shfl_xor(m, 32));
@@ -362,18 +373,22 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             float mr = s_hmax[0][row];
 #pragma unroll
             for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][row]);
-            const int ex = h2_row_exp(mr);
+            const int ex = I8 ? i8_row_exp(mr) : h2_row_exp(mr);
             if (tid < PBM) s_hexp[tid] = ex;
 #pragma unroll
             for (int i = 0; i < IPT; ++i) {
                 const int e = tid + i * PWG;
                 if (e < PBM * (N >> 3)) {
+                    if constexpr (I8) {
+                        i8_store8(sB, ldb, row, 8 * (e / PBM), re[i], im[i], ex);
+                    } else {
 #pragma unroll
-                    for (int h = 0; h < 8; ++h) {
-                        re[i][h] = __builtin_amdgcn_ldexpf(re[i][h], ex);
-                        im[i][h] = __builtin_amdgcn_ldexpf(im[i][h], ex);
+                        for (int h = 0; h < 8; ++h) {
+                            re[i][h] = __builtin_amdgcn_ldexpf(re[i][h], ex);
+                            im[i][h] = __builtin_amdgcn_ldexpf(im[i][h], ex);
+                        }
+                        h2_store8(sP, ldx, row, 8 * (e / PBM), re[i], im[i]);
                     }
-                    h2_store8(sP, ldx, row, 8 * (e / PBM), re[i], im[i]);
                 }
             }
         } else if constexpr (X3) {
@@ -407,29 +422,53 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         // 2. q = Vh r~ ; w = scale (y~ + vr q) - q  -> A   (vamp.py:67-72)
         f32x4 acc[NT];
         f32x4 cr[NC], ci[NC];
-        if constexpr (H2)
+        if constexpr (I8) {
+            float rowf[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rowf[r] = i8_row_factor(s_hexp[4 * (lane >> 4) + r]);
+            gemm_i8<NC, G3 / 2>(sB, ldb, P.Wx1, N, cc0, rowf, cr, ci);   // 64-deep groups: N / 64
+        } else if constexpr (H2)
             gemm_h2<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
         else if constexpr (X3)
             gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx1, cc0, cr, ci);
         else
             gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
         float hsc[4];                                 // H2: 2^-(e_row + H2_EX) of this lane's rows
-        int hew[4];                                   // H2: the w rows' exponents
-        if constexpr (H2) {
+        int hew[4];                                   // H2 / I8: the w rows' exponents
+        if constexpr (H2 || I8) {
             // w = scale (y~ + vr q) - q for every tile of this wave, its rows' max |w| to LDS; the
             // barrier below also ends every wave's reads of the r~ planes
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + H2_EX));
+            for (int r = 0; r < 4; ++r) hsc[r] = I8 ? 1.0f : __builtin_amdgcn_ldexpf(1.0f, -(s_hexp[4 * (lane >> 4) + r] + H2_EX));
             float mrow[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const float sc = 1.0f / (s2c[t2] + cur.vr);
+                float ytr[4], yti[4];
+                if constexpr (I8) {
+                    // y~ read back each iteration (16 rows x 2N floats per workgroup, L2-resident)
+                    // rather than held in 32 registers across the loop: the int8x4 GEMMs' ring and
+                    // level sums need them.  The lane index is pinned so the addresses are formed here
+                    const int ln = pl_opaque(lane);
+                    const int oo = 16 * (cc0 + t2) + (ln & 15);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 4 * (ln >> 4) + r;
+                        const float2 v = row < nrows ? *reinterpret_cast<const float2*>(P.ytil + (size_t)(row0 + row) * twok + 2 * oo)
+                                                     : make_float2(0.f, 0.f);
+                        ytr[r] = v.x; yti[r] = v.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { ytr[r] = yt[2 * t2][r]; yti[r] = yt[2 * t2 + 1][r]; }
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float qr = cr[t2][r] * hsc[r], qi = ci[t2][r] * hsc[r];
-                    cr[t2][r] = sc * (yt[2 * t2][r] + cur.vr * qr) - qr;
-                    ci[t2][r] = sc * (yt[2 * t2 + 1][r] + cur.vr * qi) - qi;
-                    mrow[r] = fmaxf(mrow[r], fmaxf(fabsf(cr[t2][r]), fabsf(ci[t2][r])));
+                    const float qr = I8 ? cr[t2][r] : cr[t2][r] * hsc[r], qi = I8 ? ci[t2][r] : ci[t2][r] * hsc[r];
+                    cr[t2][r] = sc * (ytr[r] + cur.vr * qr) - qr;
+                    ci[t2][r] = sc * (yti[r] + cur.vr * qi) - qi;
+                    if constexpr (I8) mrow[r] = i8_absmax(i8_absmax(mrow[r], cr[t2][r]), ci[t2][r]);
+                    else mrow[r] = fmaxf(mrow[r], fmaxf(fabsf(cr[t2][r]), fabsf(ci[t2][r])));
                 }
             }
 #pragma unroll
@@ -444,24 +483,31 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         }
         __syncthreads();
         stamp(t, 2);
-        if constexpr (H2) {
+        if constexpr (H2 || I8) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float mr = s_hmax[0][4 * (lane >> 4) + r];
 #pragma unroll
                 for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][4 * (lane >> 4) + r]);
-                hew[r] = h2_row_exp(mr);
+                hew[r] = I8 ? i8_row_exp(mr) : h2_row_exp(mr);
             }
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lane & 15);
-                float wr[4], wi[4];
+                if constexpr (I8) {
+                    int wr[4], wi[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    wr[r] = __builtin_amdgcn_ldexpf(cr[t2][r], hew[r]);
-                    wi[r] = __builtin_amdgcn_ldexpf(ci[t2][r], hew[r]);
+                    for (int r = 0; r < 4; ++r) { wr[r] = i8_fix(cr[t2][r], hew[r]); wi[r] = i8_fix(ci[t2][r], hew[r]); }
+                    i8_store_acc(sB, ldb, o, wr, wi);
+                } else {
+                    float wr[4], wi[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        wr[r] = __builtin_amdgcn_ldexpf(cr[t2][r], hew[r]);
+                        wi[r] = __builtin_amdgcn_ldexpf(ci[t2][r], hew[r]);
+                    }
+                    h2_store_acc(sP, ldx, o, wr, wi);
                 }
-                h2_store_acc(sP, ldx, o, wr, wi);
                 if (P.dump) {
                     float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 0) * PBM * twoN;
 #pragma unroll
@@ -472,7 +518,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 }
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hsc[r] = __builtin_amdgcn_ldexpf(1.0f, -(hew[r] + H2_EX));
+            for (int r = 0; r < 4; ++r) hsc[r] = I8 ? i8_row_factor(hew[r]) : __builtin_amdgcn_ldexpf(1.0f, -(hew[r] + H2_EX));
         } else if constexpr (X3) {
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
@@ -510,7 +556,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         stamp(t, 3);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
         if constexpr (X3) {
-            if constexpr (H2) {
+            if constexpr (I8) {
+                gemm_i8<NC, G3 / 2>(sB, ldb, P.Wx2, N, cc0, hsc, cr, ci);   // hsc: the w rows' factors
+            } else if constexpr (H2) {
                 gemm_h2<NC, G3>(sP, ldx, P.Wx2, cc0, cr, ci);
 #pragma unroll
                 for (int t2 = 0; t2 < NC; ++t2)
@@ -607,9 +655,9 @@ int device_cu_count();
 
 // Launch path: persist_grid_launch (amp_host.h): a plain launch after an explicit co-residency
 // check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).
-template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false>
+template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC, H2>;
+    const void* fn = (const void*)vamp_persist<NT, KK, NWV, DU, X3, OCC, H2, I8>;
     const size_t lds = (size_t)playout(P.N, P.k, P.L, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query cost tens of us per call: once per
     // instantiation and LDS size (single-threaded host use, like the rest of the ABI)
@@ -633,17 +681,17 @@ static int persist_launch_t(const VampK& P, const DecConst& dc, hipStream_t st) 
     return persist_grid_launch("vamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
-template <int NT, int NWV, bool X3, int OCC = 1, bool H2 = false>
+template <int NT, int NWV, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 static int persist_launch_nt(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC, H2>(P, dc, st);
-    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC, H2>(P, dc, st);
-    case 4: return persist_launch_t<NT, 4, NWV, AMP_KK4_DU, X3, OCC, H2>(P, dc, st);
-    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC, H2>(P, dc, st);
+    case 1: return persist_launch_t<NT, 1, NWV, 4, X3, OCC, H2, I8>(P, dc, st);
+    case 2: return persist_launch_t<NT, 2, NWV, 4, X3, OCC, H2, I8>(P, dc, st);
+    case 4: return persist_launch_t<NT, 4, NWV, AMP_KK4_DU, X3, OCC, H2, I8>(P, dc, st);
+    case 8: return persist_launch_t<NT, 8, NWV, 2, X3, OCC, H2, I8>(P, dc, st);
     case 16:
         // two sections in flight per lane group (4 and 8 measured no faster, and spill)
-        return persist_launch_t<NT, 16, NWV, X3 ? AMP_X3_DU : 2, X3, OCC, H2>(P, dc, st);
-    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC, H2>(P, dc, st);
+        return persist_launch_t<NT, 16, NWV, X3 ? AMP_X3_DU : 2, X3, OCC, H2, I8>(P, dc, st);
+    default: return persist_launch_t<NT, 64, NWV, 1, X3, OCC, H2, I8>(P, dc, st);
     }
 }
 

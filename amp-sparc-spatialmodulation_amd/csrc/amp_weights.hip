@@ -143,6 +143,58 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         }
         return;
     }
+    if (J.packed == WPACKI8) {
+        // int8x4 digit planes of X (amp_persist.h gemm_i8): kap = J, ncp = O (complex counts).  One
+        // block per output column o: the column's max |value| (re and im) sets its exponent e_o,
+        // every value becomes rint(x 2^(30 - e_o)) and its four balanced base-256 digits.
+        signed char* w8 = reinterpret_cast<signed char*>(J.wt);
+        int* ecol = reinterpret_cast<int*>(w8 + i8_exp_offset(J.ncp, J.kap));
+        __shared__ float s_m[256 / 64];
+        for (int o = blockIdx.x; o < J.ncp; o += gridDim.x) {
+            auto val = [&](int j, float& xr, float& xi) {
+                xr = 0.f; xi = 0.f;
+                if (o < J.O && j < J.J) {
+                    const float2 v = J.src[o * J.so + j * J.sj];
+                    xr = v.x;
+                    xi = J.conj ? -v.y : v.y;
+                    if (J.rowscale) {
+                        const float sc = J.rowscale[o];
+                        xr = sc * xr;
+                        xi = sc * xi;
+                    }
+                }
+            };
+            float m = 0.f;
+            for (int j = threadIdx.x; j < J.kap; j += blockDim.x) {
+                float xr, xi;
+                val(j, xr, xi);
+                m = i8_absmax(i8_absmax(m, xr), xi);
+            }
+            for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
+            __syncthreads();
+            if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+            __syncthreads();
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, s_m[w]);
+            // a non-finite operator column: its digits are zero and its exponent makes the column
+            // factor inf (the GEMM's results are then non-finite, never silently wrong)
+            const int e = i8_row_exp(m);
+            if (threadIdx.x == 0) ecol[o] = e == 0x7fffffff ? 200 : e;
+            for (int j = threadIdx.x; j < J.kap; j += blockDim.x) {
+                float xr, xi;
+                val(j, xr, xi);
+                const int vr = i8_fix(xr, e), vi = i8_fix(xi, e);
+                w8[i8_index(o, j, 0, J.kap)] = (signed char)((vr + 0x808080) >> 24);
+                w8[i8_index(o, j, 1, J.kap)] = (signed char)((vr + 0x8080) >> 16);
+                w8[i8_index(o, j, 2, J.kap)] = (signed char)((vr + 0x80) >> 8);
+                w8[i8_index(o, j, 3, J.kap)] = (signed char)vr;
+                w8[i8_index(o, j, 4, J.kap)] = (signed char)((vi + 0x808080) >> 24);
+                w8[i8_index(o, j, 5, J.kap)] = (signed char)((vi + 0x8080) >> 16);
+                w8[i8_index(o, j, 6, J.kap)] = (signed char)((vi + 0x80) >> 8);
+                w8[i8_index(o, j, 7, J.kap)] = (signed char)vi;
+            }
+        }
+        return;
+    }
     if (J.packed == WPACKH2) {
         // fp16x2 planes of X 2^ex (amp_persist.h gemm_h2): kap = J, ncp = O (complex counts).
         // |x| 2^ex >= 65520 leaves fp16's range: the piece is then inf, so the GEMM's result is
@@ -218,11 +270,12 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     long most = 0;
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
-        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2;
+        const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2 ||
+                            J.packed == WPACKI8;
         AMP_REQUIRE((planar ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
                          (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||
-                         (planar && J.kap % 32 == 0 && J.ncp % 16 == 0)),
+                         (planar && J.kap % (J.packed == WPACKI8 ? 64 : 32) == 0 && J.ncp % 16 == 0)),
                     "build_cweights: job %d kap %d / ncp %d not tiled for layout %d", i, J.kap, J.ncp, J.packed);
         P.j[i] = J;
         most = std::max(most, planar ? (long)J.ncp * J.kap : (long)(J.ncp / 2) * (J.kap / 2));

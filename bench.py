@@ -198,7 +198,7 @@ def main():
     # the persistent engine's GEMM arithmetic: auto = bf16x3 (three bf16 pieces per f32 operand,
     # 24 bits, dropped product terms < 2^-24: the reference's c64 operand precision); h2 = the
     # opt-in fp16x2 form (22-bit operands, narrower than the reference: a second, labelled line)
-    ap.add_argument('--gemm', default='auto', choices=['auto', 'x3', 'f32', 'h2'])
+    ap.add_argument('--gemm', default='auto', choices=['auto', 'x3', 'f32', 'h2', 'i8'])
     # independent epochs per rank (weak scaling, the default) or ONE batch of B trials split over
     # the ranks (strong scaling: ShardedVAMP, the batch scalars all-reduced every iteration)
     ap.add_argument('--shard', default='epochs', choices=['epochs', 'trials'])
@@ -236,7 +236,7 @@ def main():
     # and noise: seed + rank); trials: every rank draws the SAME epoch and detects its slice
     inp = make_inputs(cfg, args.seed + (0 if trials else rank), args.ebn0, device)
     engine = {'auto': nat.ENGINE_AUTO, 'launches': nat.ENGINE_LAUNCHES, 'persistent': nat.ENGINE_PERSISTENT}[args.engine]
-    gemm = {'auto': nat.GEMM_AUTO, 'x3': nat.GEMM_X3, 'f32': nat.GEMM_F32, 'h2': nat.GEMM_H2}[args.gemm]
+    gemm = {'auto': nat.GEMM_AUTO, 'x3': nat.GEMM_X3, 'f32': nat.GEMM_F32, 'h2': nat.GEMM_H2, 'i8': nat.GEMM_I8}[args.gemm]
     det = ShardedVAMP(cfg) if trials else VAMP(cfg, engine=engine, gemm=gemm)
     seq = [0]
 
@@ -290,12 +290,17 @@ def main():
     N, k = Nt, min(Nt, Nr)
     flops_mv = 8.0 * Bp * N * k                    # complex [N x k] . [k] per trial = 8 real flop / CMAC
     gmode = nat.lib().amp_vamp_select_gemm(C.byref(Tr.dims), Tr.k, Tr.args.gemm) if persistent else nat.GEMM_F32
-    gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2'}.get(gmode, 'f32')
+    gname = {nat.GEMM_X3: 'bf16x3', nat.GEMM_H2: 'fp16x2', nat.GEMM_I8: 'int8x4'}.get(gmode, 'f32')
     arith = {'bf16x3': 'GEMMs: every f32 operand split into three bf16 pieces (24 significant bits), six '
                        'products per f32 product (dropped terms < 2^-24 relative), f32 accumulation on '
                        'v_mfma_f32_16x16x32_bf16; denoiser f32, scalars f32/f64 as the reference',
              'fp16x2': 'OPT-IN, narrower than the reference: GEMM operands split into two fp16 pieces (22 '
                        'significant bits), the 2^-22 lo.lo term dropped, f32 accumulation',
+             'int8x4': 'GEMMs in block fixed point: every A row and operator column scaled by its own power of '
+                       'two, each value a 31-bit integer in four balanced int8 digits, the ten digit products '
+                       'of levels 0-3 exact in int32 on v_mfma_i32_16x16x64_i8, levels combined in f32 '
+                       '(>= 24 significant bits down to 2^-7 of the row/column max; dropped terms < 2^-30 of '
+                       'row max . column max); denoiser f32, scalars f32/f64 as the reference',
              'f32': 'GEMMs on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32)'}[gname]
     # the fp16x2 engine forms y~ = (s Uh) y in its prologue when n == 2N (amp_vamp.hip): those
     # 8 B n k flops per trial belong to the launch then

@@ -118,12 +118,21 @@ typedef struct amp_vamp_args {
  *        (the 2^-22 lo.lo term dropped), f32 accumulation, the scales taken off exactly; the
  *        operators must have entries of magnitude < 4 (SVD factors: <= 1; larger entries give
  *        non-finite results, never silently wrong ones); same shape constraints as X3;
+ *  I8    int8x4 block fixed point on the integer matrix cores: every A row and every operator
+ *        column scaled by its own power of two, every value as a 31-bit integer in four
+ *        balanced 8-bit digits, the ten digit products of levels 0-3 exact in int32
+ *        (v_mfma_i32_16x16x64_i8), the levels combined in f32: 31 bits per element relative to
+ *        its row's / column's maximum (>= 24 bits down to 2^-7 of it), dropped terms < 2^-30 of
+ *        (row max . column max); on the cfg4 GEMM 23x closer to a float64 sum than an f32 sum
+ *        (amp_persist.h gemm_i8); a non-finite A row gives a NaN result row; same shape
+ *        constraints as X3, one workgroup per CU;
  *  AUTO  X3 where the planes fit, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32,
  *        AMP_VAMP_GEMM=h2 picks H2). */
 #define AMP_GEMM_AUTO 0
 #define AMP_GEMM_F32 1
 #define AMP_GEMM_X3 2
 #define AMP_GEMM_H2 3
+#define AMP_GEMM_I8 4
 
 #define AMP_ENGINE_AUTO 0
 #define AMP_ENGINE_LAUNCHES 1
@@ -132,8 +141,8 @@ typedef struct amp_vamp_args {
 /* The engine amp_vamp_run will use for this shape on the current device (LAUNCHES or
  * PERSISTENT), or AMP_E_ARG when `engine` is PERSISTENT and the shape is not eligible. */
 int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
-/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_X3, AMP_GEMM_H2 or
- * AMP_GEMM_F32 (AMP_E_ARG when `gemm` is AMP_GEMM_X3 / _H2 and the shape does not fit it). */
+/* The arithmetic the persistent engine will use for this shape: AMP_GEMM_X3, AMP_GEMM_H2,
+ * AMP_GEMM_I8 or AMP_GEMM_F32 (AMP_E_ARG when `gemm` is X3 / H2 / I8 and the shape does not fit). */
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
  * phase into trace (device, nwg * max_iter * 10 + 2 * nwg uint64; layout in amp_vamp.hip). */

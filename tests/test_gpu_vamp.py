@@ -216,7 +216,8 @@ VAMP_POINTS = (_curve_points('cfg2_vamp_16qam') + _curve_points('cfg2_vamp_qpsk'
 ENGINES = {'launches': 1, 'persistent': 2}   # amp_native.ENGINE_*
 # (engine, persistent GEMM arithmetic): 'persistent' = the product default (bf16x3 where it fits:
 # 24-bit operands), 'persistent-f32' the f32-MFMA form, 'persistent-h2' the opt-in fp16x2 form
-VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 'persistent-h2': (2, 3)}
+VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 'persistent-h2': (2, 3),
+            'persistent-i8': (2, 4)}
 
 
 @pytest.mark.parametrize('variant', sorted(VARIANTS))
@@ -283,7 +284,7 @@ def test_vamp_x3_gemm_matches_f32(device, name, iters):
     assert nat.lib().amp_vamp_select_engine(cfg.dims(), ent['Nt'], nat.ENGINE_AUTO) == nat.ENGINE_PERSISTENT
     r = {}
     assert nat.lib().amp_vamp_select_gemm(cfg.dims(), ent['Nt'], nat.GEMM_AUTO) == nat.GEMM_X3
-    for gemm in (nat.GEMM_F32, nat.GEMM_X3, nat.GEMM_H2):
+    for gemm in (nat.GEMM_F32, nat.GEMM_X3, nat.GEMM_H2, nat.GEMM_I8):
         T = VAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm).detect(inp['U'], inp['s'], inp['Vh'], inp['y'],
                                                                      inp['SNR'])
         r[gemm] = T.r.clone().cpu().numpy()[..., 0]
@@ -294,7 +295,10 @@ def test_vamp_x3_gemm_matches_f32(device, name, iters):
     e32 = float(np.abs(r[nat.GEMM_F32] - o).max())
     ex3 = float(np.abs(r[nat.GEMM_X3] - o).max())
     eh2 = float(np.abs(r[nat.GEMM_H2] - o).max())
+    ei8 = float(np.abs(r[nat.GEMM_I8] - o).max())
+    print(f'max|r - oracle|: f32 {e32:.3e} bf16x3 {ex3:.3e} fp16x2 {eh2:.3e} int8x4 {ei8:.3e}')
     assert ex3 <= max(4 * e32, 2e-6 * scale), (ex3, e32, scale)
+    assert ei8 <= max(4 * e32, 2e-6 * scale), (ei8, e32, scale)
     assert eh2 <= max(4 * e32, 2e-6 * scale), (eh2, e32, scale)
 
 

@@ -30,6 +30,9 @@ ALLOWED = [
     # 64-point alphabets at N = 256 (no BASELINE VAMP config): the wide denoiser's chunked table
     # beside the N = 256 GEMM registers, 12 values reloaded once per iteration
     (r'_ZN3amp12vamp_persistILi8ELi64ELi4ELi1ELb[01]ELi1ELb[01]E', '64-point alphabet at N = 256'),
+    # the int8x4 engine at N = 256: loop-invariant values stored once in the prologue and reloaded
+    # outside the GEMMs (none inside them)
+    (r'_ZN3amp12vamp_persistILi8ELi(1|2|4|8|16|64)ELi4ELi[124]ELb1ELi1ELb0ELb1E', 'int8x4 at N = 256'),
 ]
 
 

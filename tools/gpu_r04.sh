@@ -21,6 +21,9 @@ for s in ${STEPS:-bench}; do
     bench) run bench 300 python3 bench.py ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --no-cpu-baseline ;;
     bench_h2) run bench_h2 300 python3 bench.py --no-cpu-baseline --gemm h2 ;;
+    bench_i8) run bench_i8 300 python3 bench.py --no-cpu-baseline --gemm i8 ;;
+    trace_i8) run trace_i8 300 env AMP_VAMP_GEMM=i8 python3 tools/trace_persist.py --config cfg4 ;;
+    tests_i8) run tests_i8 900 $PYT tests/test_gpu_vamp.py -m gpu -k "i8 or split_engines" ;;
     bench_f32) run bench_f32 300 python3 bench.py --no-cpu-baseline --gemm f32 ;;
     trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;
     trace_h2) run trace_h2 300 env AMP_VAMP_GEMM=h2 python3 tools/trace_persist.py --config cfg4 ;;

@@ -100,6 +100,112 @@ __device__ __forceinline__ void gemm_i8(const signed char* sA, const void* wq, i
     }
 }
 
+// Tile-outer form (the engine's): complex column tile t runs all its K groups before tile t + 1,
+// so only ONE tile's level accumulators are live (P = Ar.Xr, Q = Ai.Xi, C = Ar.Xi + Ai.Xr, four
+// levels each: 48 registers) and the result leaves as f32 (Cr = P - Q exact in int32: every level
+// sum < 2^25).  The A operand is eight planes (Ar, Ai; no -Ai), re-read from LDS per tile.  The
+// operator streams through a ring of D (tile, group) slots in (t, g) order.
+template <int NT, int G, int D>
+__device__ __forceinline__ void gemm_i8t(const signed char* sA, const void* wq, int ct0, const int* aexp,
+                                         const int* xexp, f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
+    const int lane = threadIdx.x & 63;
+    const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 8 * 1024, (short)0, 0x7ffffff0, 0x00020000);
+    const int vo = lane * 16;
+    constexpr int NS = NT * G;                 // (tile, group) steps, t-major
+    u32x4 ring[D][8];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int f = 0; f < 8; ++f) ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, (d * 8 + f) * 1024, 0);
+    const signed char* ap = sA + (lane & 15) * LDA + 16 * (lane >> 4);
+    u32x4 an[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA);
+    i32x4 P[4], Q[4], C[4];
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+        const int t = st / G, g = st % G, d = st % D;
+        if (g == 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) { P[s] = i32x4{0, 0, 0, 0}; Q[s] = P[s]; C[s] = P[s]; }
+        }
+        u32x4 a[8];
+#pragma unroll
+        for (int f = 0; f < 8; ++f) a[f] = an[f];
+        if (st + 1 < NS) {
+            const int g1 = (st + 1) % G;
+#pragma unroll
+            for (int f = 0; f < 8; ++f) an[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * LDA + 64 * g1);
+        }
+        const u32x4* w = ring[d];   // w[0..3] Xr s0..s3, w[4..7] Xi s0..s3
+#define MI(acc_, x, y) acc_ = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, x), __builtin_bit_cast(i32x4, y), acc_, 0, 0, 0)
+#pragma unroll
+        for (int s = 3; s >= 0; --s)
+#pragma unroll
+            for (int i = 0; i <= s; ++i) {
+                const int j = s - i;
+                MI(P[s], a[i], w[j]);          // Ar Xr
+                MI(Q[s], a[4 + i], w[4 + j]);  // Ai Xi
+                MI(C[s], a[i], w[4 + j]);      // Ar Xi
+                MI(C[s], a[4 + i], w[j]);      // Ai Xr
+            }
+#undef MI
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + D < NS) {
+#pragma unroll
+            for (int f = 0; f < 8; ++f)
+                ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((st + D) * 8 + f) * 1024, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (g == G - 1) {
+            const int o = 16 * (ct0 + t) + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = aexp[4 * (lane >> 4) + r] + xexp[o] - 12;
+                float vr = (float)(P[3][r] - Q[3][r]), vi = (float)C[3][r];
+                vr = fmaf(vr, 0x1p-8f, (float)(P[2][r] - Q[2][r])); vi = fmaf(vi, 0x1p-8f, (float)C[2][r]);
+                vr = fmaf(vr, 0x1p-8f, (float)(P[1][r] - Q[1][r])); vi = fmaf(vi, 0x1p-8f, (float)C[1][r]);
+                vr = fmaf(vr, 0x1p-8f, (float)(P[0][r] - Q[0][r])); vi = fmaf(vi, 0x1p-8f, (float)C[0][r]);
+                cr[t][r] = __builtin_amdgcn_ldexpf(vr, e);
+                ci[t][r] = __builtin_amdgcn_ldexpf(vi, e);
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void ki8t(const signed char* apieces, const int* aexp, const void* wq,
+                                               const int* xexp, float* out, unsigned long long* cyc) {
+    __shared__ __attribute__((aligned(16))) signed char sA[8 * 16 * LDA];
+    __shared__ int s_ae[16];
+    for (int e = threadIdx.x; e < 8 * 16 * KC; e += 256) {
+        const int f = e / (16 * KC), rem = e % (16 * KC), row = rem / KC, k = rem % KC;
+        sA[(f * 16 + row) * LDA + k] = apieces[e];
+    }
+    if (threadIdx.x < 16) s_ae[threadIdx.x] = aexp[threadIdx.x];
+    __syncthreads();
+    constexpr int NT = OC / 16 / 4, G = KC / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    f32x4 cr[NT], ci[NT];
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int rep = 0; rep < REPS; ++rep) {
+        gemm_i8t<NT, G, D>(sA, wq, wave * NT, s_ae, xexp, cr, ci);
+        __syncthreads();
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0) {
+        for (int t = 0; t < NT; ++t)
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * (lane >> 4) + r, o = 16 * (wave * NT + t) + (lane & 15);
+                out[(row * OC + o) * 2] = cr[t][r];
+                out[(row * OC + o) * 2 + 1] = ci[t][r];
+            }
+    }
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 __device__ __forceinline__ float i8_combine(const i32x4 (&l)[4], int r) {
     float v = (float)l[3][r];
     v = fmaf(v, 0x1p-8f, (float)l[2][r]);
@@ -153,7 +259,7 @@ static int exp_of(double m) {   // smallest e with m < 2^e
     return e;
 }
 
-template <int R, bool TR>
+template <int R, bool TR, int TOUT = 0>
 static void run(const std::vector<signed char>& ap, const std::vector<int>& ae, const std::vector<signed char>& wp,
                 const std::vector<int>& xe, const std::vector<double>& ref, const std::vector<float>& f32c) {
     signed char* dA;
@@ -171,7 +277,10 @@ static void run(const std::vector<signed char>& ap, const std::vector<int>& ae, 
     hipMemcpy(dae, ae.data(), ae.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(dxe, xe.data(), xe.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(dW, wp.data(), wp.size(), hipMemcpyHostToDevice);
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((ki8<R, TR>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
+    for (int i = 0; i < 3; ++i) {
+        if constexpr (TOUT) hipLaunchKernelGGL((ki8t<TOUT>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
+        else hipLaunchKernelGGL((ki8<R, TR>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
+    }
     hipDeviceSynchronize();
     std::vector<unsigned long long> c(NWG, 0);
     hipMemcpy(c.data(), dc, NWG * 8, hipMemcpyDeviceToHost);
@@ -186,8 +295,8 @@ static void run(const std::vector<signed char>& ap, const std::vector<int>& ae, 
         sf += (f32c[i] - ref[i]) * (f32c[i] - ref[i]);
         nrm = std::max(nrm, fabs(ref[i]));
     }
-    printf("int8x4 R=%d TR=%d: cycles per GEMM median %.0f max %.0f   max|err| i8x4 %.3e f32-seq %.3e   rms i8x4 %.3e f32-seq %.3e (max|C| %.3f)\n",
-           R, (int)TR, (double)c[NWG / 2] / REPS, (double)c[NWG - 1] / REPS, ei, ef, sqrt(si / o.size()), sqrt(sf / o.size()), nrm);
+    printf("int8x4 R=%d TR=%d tile-outer D=%d: cycles per GEMM median %.0f max %.0f   max|err| i8x4 %.3e f32-seq %.3e   rms i8x4 %.3e f32-seq %.3e (max|C| %.3f)\n",
+           R, (int)TR, TOUT, (double)c[NWG / 2] / REPS, (double)c[NWG - 1] / REPS, ei, ef, sqrt(si / o.size()), sqrt(sf / o.size()), nrm);
     hipFree(dA); hipFree(dae); hipFree(dxe); hipFree(dW); hipFree(dO); hipFree(dc);
 }
 
@@ -258,5 +367,10 @@ int main() {
     run<1, true>(ap, ae, wp, xe, ref, f32c);
     run<2, false>(ap, ae, wp, xe, ref, f32c);
     run<2, true>(ap, ae, wp, xe, ref, f32c);
+    // tile-outer: the A planes without -Ai (ap's first eight planes)
+    run<1, false, 2>(ap, ae, wp, xe, ref, f32c);
+    run<1, false, 3>(ap, ae, wp, xe, ref, f32c);
+    run<1, false, 4>(ap, ae, wp, xe, ref, f32c);
+    run<1, false, 6>(ap, ae, wp, xe, ref, f32c);
     return 0;
 }
