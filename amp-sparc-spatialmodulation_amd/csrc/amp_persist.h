@@ -576,6 +576,10 @@ __device__ __forceinline__ void gemm_i8(const signed char* sB, int ldb, const vo
 #pragma unroll
         for (int f = 0; f < 8; ++f) ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, (d * 8 + f) * 1024, 0);
     const int ln = pl_opaque(lane);
+    // this lane's column factors, loaded up front (they arrive during the first tile's MFMAs)
+    float cf[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) cf[t] = __builtin_amdgcn_ldexpf(1.0f, ecol[16 * (ct0 + t) + (ln & 15)]);
     const signed char* ap = sB + (ln & 15) * ldb + 16 * (ln >> 4);
     u32x4 an[8];
     if constexpr (APF) {
@@ -628,7 +632,6 @@ __device__ __forceinline__ void gemm_i8(const signed char* sB, int ldb, const vo
         }
         __builtin_amdgcn_sched_barrier(0);
         if (g == G - 1) {
-            const float cf = __builtin_amdgcn_ldexpf(1.0f, ecol[16 * (ct0 + t) + (lane & 15)]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float vr = (float)(P[3][r] - Q[3][r]), vi = (float)C[3][r];
@@ -638,8 +641,8 @@ __device__ __forceinline__ void gemm_i8(const signed char* sB, int ldb, const vo
                 vi = fmaf(vi, 0x1p-8f, (float)C[1][r]);
                 vr = fmaf(vr, 0x1p-8f, (float)(P[0][r] - Q[0][r]));
                 vi = fmaf(vi, 0x1p-8f, (float)C[0][r]);
-                cr[t][r] = vr * rowf[r] * cf;
-                ci[t][r] = vi * rowf[r] * cf;
+                cr[t][r] = vr * rowf[r] * cf[t];
+                ci[t][r] = vi * rowf[r] * cf[t];
             }
         }
     }

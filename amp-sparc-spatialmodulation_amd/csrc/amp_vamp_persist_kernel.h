@@ -340,12 +340,13 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             // r~ rows in registers (item e: row e % PBM == tid % PBM, 8 complex values), the
             // row's max |value| over the workgroup, then the scaled split
             constexpr int IPT = (NT + 3) / 4;             // items per thread: PBM N / 8 / PWG
-            const int row = tid % PBM;
+            const int tdp = I8 ? pl_opaque(tid) : tid;     // I8: addresses formed here, not hoisted
+            const int row = tdp % PBM;
             float re[IPT][8], im[IPT][8];
             float m = 0.f;
 #pragma unroll
             for (int i = 0; i < IPT; ++i) {
-                const int e = tid + i * PWG;
+                const int e = tdp + i * PWG;
                 const int j0 = 8 * (e / PBM);
                 const bool ok = e < PBM * (N >> 3);
 #pragma unroll
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             if (tid < PBM) s_hexp[tid] = ex;
 #pragma unroll
             for (int i = 0; i < IPT; ++i) {
-                const int e = tid + i * PWG;
+                const int e = tdp + i * PWG;
                 if (e < PBM * (N >> 3)) {
                     if constexpr (I8) {
                         i8_store8(sB, ldb, row, 8 * (e / PBM), re[i], im[i], ex);
@@ -491,9 +492,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 for (int w = 1; w < PWG / 64; ++w) mr = fmaxf(mr, s_hmax[w][4 * (lane >> 4) + r]);
                 hew[r] = I8 ? i8_row_exp(mr) : h2_row_exp(mr);
             }
+            const int lnw = I8 ? pl_opaque(lane) : lane;   // I8: addresses formed here, not hoisted
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
-                const int o = 16 * (cc0 + t2) + (lane & 15);
+                const int o = 16 * (cc0 + t2) + (lnw & 15);
                 if constexpr (I8) {
                     int wr[4], wi[4];
 #pragma unroll
@@ -567,12 +569,15 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             } else {
                 gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx2, cc0, cr, ci);
             }
+            // the lane index pinned here: the 4 NC LDS addresses below are then formed in this
+            // epilogue instead of being hoisted out of the iteration loop (and kept live across it)
+            const int lnr = I8 ? pl_opaque(lane) : lane;
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
-                const int o = 16 * (cc0 + t2) + (lane & 15);
+                const int o = 16 * (cc0 + t2) + (lnr & 15);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int b = (4 * (lane >> 4) + r) * ldr + 2 * o;
+                    const int b = (4 * (lnr >> 4) + r) * ldr + 2 * o;
                     const float rtr = (sX[b] - cur.dxdr_prev * sR[b]) * cur.ns_prev;
                     const float rti = (sX[b + 1] - cur.dxdr_prev * sR[b + 1]) * cur.ns_prev;
                     const float xtr = cr[t2][r] + rtr, xti = ci[t2][r] + rti;

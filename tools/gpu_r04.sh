@@ -42,6 +42,9 @@ for s in ${STEPS:-bench}; do
            run gemm_i8 120 tools/ubench/bin/gemm_i8 ;;
     pkdpp) run pkdpp 300 tools/ubench/bin/pk_dpp 3 ;;
     gi8) run gemm_i8 120 tools/ubench/bin/gemm_i8 ;;
+    svd) run svd 300 python3 tools/svd_bench.py ;;
+    simb) run simb 300 python3 tools/simulate_bench.py --epochs 8 ;;
+    tests_model) run tests_model 600 $PYT tests/test_gpu_vamp.py -m gpu -k "device or random or model" ;;
     tprobe) run tprobe 300 python3 tools/t_probe.py ;;
     tests_vdef) run tests_vdef 900 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2" ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
