@@ -23,6 +23,8 @@
 #include <algorithm>
 #include <vector>
 
+#include "../../amp-sparc-spatialmodulation_amd/csrc/amp_persist.h"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -243,6 +245,39 @@ __global__ __launch_bounds__(256, 1) void ki8(const signed char* apieces, const 
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// The engine's own gemm_i8 (amp_persist.h), operator exponents appended behind the planes.
+__global__ __launch_bounds__(256, 1) void ki8e(const signed char* apieces, const int* aexp, const void* wqe,
+                                               float* out, unsigned long long* cyc) {
+    __shared__ __attribute__((aligned(16))) signed char sA[8 * 16 * LDA];
+    __shared__ int s_ae[16];
+    for (int e = threadIdx.x; e < 8 * 16 * KC; e += 256) {
+        const int f = e / (16 * KC), rem = e % (16 * KC), row = rem / KC, k = rem % KC;
+        sA[(f * 16 + row) * LDA + k] = apieces[e];
+    }
+    if (threadIdx.x < 16) s_ae[threadIdx.x] = aexp[threadIdx.x];
+    __syncthreads();
+    constexpr int NT = OC / 16 / 4, G = KC / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    f32x4 cr[NT], ci[NT];
+    float rowf[4];
+    for (int r = 0; r < 4; ++r) rowf[r] = ldexpf(1.0f, s_ae[4 * (lane >> 4) + r] - 12);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int rep = 0; rep < REPS; ++rep) {
+        amp::gemm_i8<NT, G>(sA, LDA, wqe, OC, wave * NT, rowf, cr, ci);
+        __syncthreads();
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0) {
+        for (int t = 0; t < NT; ++t)
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * (lane >> 4) + r, o = 16 * (wave * NT + t) + (lane & 15);
+                out[(row * OC + o) * 2] = cr[t][r];
+                out[(row * OC + o) * 2 + 1] = ci[t][r];
+            }
+    }
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 // v (|v| < 2^e) -> four balanced base-256 digits of round(v 2^(30 - e)), top first
 static void slice4(double v, int e, signed char d[4]) {
     long long X = llrint(ldexp(v, 30 - e));
@@ -270,15 +305,17 @@ static void run(const std::vector<signed char>& ap, const std::vector<int>& ae, 
     hipMalloc(&dA, ap.size());
     hipMalloc(&dae, ae.size() * 4);
     hipMalloc(&dxe, xe.size() * 4);
-    hipMalloc(&dW, wp.size());
+    hipMalloc(&dW, wp.size() + OC * 4);
     hipMalloc(&dO, 16 * OC * 2 * 4);
     hipMalloc(&dc, NWG * 8);
     hipMemcpy(dA, ap.data(), ap.size(), hipMemcpyHostToDevice);
     hipMemcpy(dae, ae.data(), ae.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(dxe, xe.data(), xe.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(dW, wp.data(), wp.size(), hipMemcpyHostToDevice);
+    hipMemcpy((char*)dW + wp.size(), xe.data(), OC * 4, hipMemcpyHostToDevice);   // the engine's exponent table
     for (int i = 0; i < 3; ++i) {
-        if constexpr (TOUT) hipLaunchKernelGGL((ki8t<TOUT>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
+        if constexpr (TOUT < 0) hipLaunchKernelGGL(ki8e, dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dO, dc);
+        else if constexpr (TOUT) hipLaunchKernelGGL((ki8t<TOUT>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
         else hipLaunchKernelGGL((ki8<R, TR>), dim3(NWG), dim3(256), 0, 0, dA, dae, dW, dxe, dO, dc);
     }
     hipDeviceSynchronize();
@@ -372,5 +409,6 @@ int main() {
     run<1, false, 3>(ap, ae, wp, xe, ref, f32c);
     run<1, false, 4>(ap, ae, wp, xe, ref, f32c);
     run<1, false, 6>(ap, ae, wp, xe, ref, f32c);
+    run<1, false, -1>(ap, ae, wp, xe, ref, f32c);   // the engine's gemm_i8
     return 0;
 }
