@@ -570,6 +570,18 @@ static int ytil_in_kernel_env() {
     return v;
 }
 
+// y~ of the split-precision engines (bf16x3, int8x4) as its own bf16x3 launch (ytil_x3_launch,
+// amp_vamp_persist_x3.hip); AMP_YTIL_X3=0 keeps the f32 gemm_store launch (A/B runs)
+static bool ytil_x3_env() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_YTIL_X3");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+bool ytil_x3_fits(int n, int k);
+int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st);
+
 static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st) {
     static std::atomic<unsigned> gen{0};
     P.gen = ++gen;
@@ -579,6 +591,7 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     else
         P.ytil_in_kernel = (!P.x3 && env == 1 && vamp_persist_ytil_in_kernel(P)) ? 1 : 0;
     const bool yk = P.ytil_in_kernel != 0;
+    const bool yx3 = !yk && (P.x3 == 1 || P.x3 == 3) && ytil_x3_env() && ytil_x3_fits(P.n, P.k);
     CWeightJob j[3];
     if (P.x3) {
         const int pk = P.x3 == 3 ? WPACKI8 : P.x3 == 2 ? WPACKH2 : WPACKX3;
@@ -595,10 +608,12 @@ static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st
     //   y~ = (s U^H) y   (vamp.py:22)    X[o][j] = s_o conj(U[j][o]),  o < k, j < n
     j[2] = (yk && P.x3 == 2)
                ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, P.n, P.k, WPACKH2, YH2_EX}
+           : yx3 ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, P.n, P.k, WPACKX3}
            : yk ? CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wq0, 2 * P.n, 2 * P.k, WPACK16}
                 : CWeightJob{(const float2*)a->U, 1, P.k, 1, P.s, P.k, P.n, (float*)P.Wt0, P.kap0, P.ncp0, WPACK32};
     int rc = build_cweights(j, 3, P.pbar, PBAR_WORDS, st);
     if (rc || yk) return rc;
+    if (yx3) return ytil_x3_launch((const float*)a->y, P.n, P.B * P.E, P.Wq0, P.ytil, P.k, st);
     rc = vamp_attrs();
     if (rc) return rc;
     return gemm_store((const float*)a->y, 2 * P.n, P.B * P.E, 2 * P.n, P.Wt0, P.kap0, P.ncp0, P.ytil, 2 * P.k,
