@@ -19,6 +19,9 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #ifndef AMP_KK4_DU
 #define AMP_KK4_DU 4                    // QPSK sections in flight per lane group (diagnostic builds vary it)
 #endif
+#ifndef AMP_X3_W8_PKGRID
+#define AMP_X3_W8_PKGRID 1              // the eight-wave bf16x3 form keeps 16-QAM's packed grid denoiser
+#endif
 #ifndef AMP_X3_DU
 #define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
 #endif
@@ -69,9 +72,13 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // exponents); the results come out of the GEMM fully scaled.
 template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
-    static_assert(!X3 || (NWV == 4 && NT % 2 == 0), "X3: four waves, whole complex tiles");
+    static_assert(!X3 || ((NWV == 4 || (NWV == 8 && !H2 && !I8 && OCC == 1)) && NT % 2 == 0),
+                  "X3: four waves (eight for the bf16x3 two-waves-per-SIMD form), whole complex tiles");
     static_assert(!(H2 && I8) && (!I8 || X3), "I8: a split-precision form of its own");
-    constexpr bool PKDEN = (OCC * NWV / 4 == 1) || AMP_OCC2_PK;   // packed denoiser only at one wave per SIMD
+    // packed denoiser at one wave per SIMD; with two (OCC = 2, or the eight-wave bf16x3 form) only
+    // the packed product-grid form for 16-point alphabets (AMP_X3_W8_PKGRID; the per-point packed
+    // form lost results there)
+    constexpr bool PKDEN = (OCC * NWV / 4 == 1) || AMP_OCC2_PK || (NWV == 8 && KK == 16 && AMP_X3_W8_PKGRID);
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
     constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
@@ -393,7 +400,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 }
             }
         } else if constexpr (X3) {
-            for (int e = tid; e < PBM * (N >> 3); e += PWG) {   // 8 complex values per item
+            const int tdx = NWV == 8 ? pl_opaque(tid) : tid;   // eight waves: addresses formed here
+            for (int e = tdx; e < PBM * (N >> 3); e += PWG) {   // 8 complex values per item
                 // consecutive items walk the 16 rows (row stride 2N + 4 floats): each group of 16
                 // lanes reads 16 different bank quads (item-major rows put 4 lanes on each)
                 const int row = e % PBM, j0 = 8 * (e / PBM);
@@ -522,9 +530,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
             for (int r = 0; r < 4; ++r) hsc[r] = I8 ? i8_row_factor(hew[r]) : __builtin_amdgcn_ldexpf(1.0f, -(hew[r] + H2_EX));
         } else if constexpr (X3) {
+            const int lnx = NWV == 8 ? pl_opaque(lane) : lane;   // eight waves: addresses formed here
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
-                const int o = 16 * (cc0 + t2) + (lane & 15);
+                const int o = 16 * (cc0 + t2) + (lnx & 15);
                 const float sc = 1.0f / (s2c[t2] + cur.vr);
                 float wr[4], wi[4];
 #pragma unroll
@@ -571,7 +580,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             }
             // the lane index pinned here: the 4 NC LDS addresses below are then formed in this
             // epilogue instead of being hoisted out of the iteration loop (and kept live across it)
-            const int lnr = I8 ? pl_opaque(lane) : lane;
+            const int lnr = (I8 || NWV == 8) ? pl_opaque(lane) : lane;
 #pragma unroll
             for (int t2 = 0; t2 < NC; ++t2) {
                 const int o = 16 * (cc0 + t2) + (lnr & 15);

@@ -5,13 +5,26 @@
 
 namespace amp {
 
+// N = 256: eight waves per workgroup (two per SIMD, 256 registers each, half the column tiles per
+// wave) by default — the VALU phases (denoiser, plane builds) issue at twice the rate of one wave
+// per SIMD, and the GEMMs' operator stream hides better (80.6k -> 70.2k cycles per
+// cfg4 iteration).  AMP_VAMP_X3_WAVES=4 keeps the four-wave form (A/B runs).
+static bool x3_waves8() {
+    static const bool v = [] {
+        const char* e = getenv("AMP_VAMP_X3_WAVES");
+        return !(e && atoi(e) == 4);
+    }();
+    return v;
+}
+
 int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.N) {
     case 64:   // the two-per-CU build for every N = 64 launch, so that one epoch and side-by-side
                // epochs run the same arithmetic (bit-identical results, tests/test_gpu_epochs.py)
         return persist_wg2() ? persist_launch_nt<2, 4, true, 2>(P, dc, st) : persist_launch_nt<2, 4, true>(P, dc, st);
     case 128: return persist_launch_nt<4, 4, true>(P, dc, st);
-    case 256: return persist_launch_nt<8, 4, true>(P, dc, st);
+    case 256:
+        return x3_waves8() ? persist_launch_nt<4, 8, true>(P, dc, st) : persist_launch_nt<8, 4, true>(P, dc, st);
     default: break;
     }
     set_error("vamp_persist (bf16x3): N = %d not supported", P.N);

@@ -458,3 +458,26 @@ def test_vamp_accepts_lazy_conj_views(device):
     if lazy.is_conj():
         with pytest.raises(ValueError):
             nat.dptr(lazy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['cfg4_vamp_16qam', 'cfg4_vamp_qpsk'])
+def test_persistent_n256_reproducible(device, name):
+    """The N = 256 bf16x3 engine runs eight waves per workgroup (two per SIMD; the 16-point
+    alphabets keep the packed product-grid denoiser there): five forwards
+    of the same cfg4 batch give the same r / xmmse / var bits and T every time."""
+    from vamp import VAMP
+    ent = CURVES[name]
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    inp = _regen_inputs(cfg, 1, 8.0)
+    det = VAMP(cfg, engine=2)
+    first = None
+    for rep in range(5):
+        T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+        torch.cuda.synchronize()
+        got = [T.buf.r.clone(), T.buf.xmmse.clone(), T.buf.var.clone()]
+        if first is None:
+            first = got
+            continue
+        for a, b in zip(got, first):
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), rep

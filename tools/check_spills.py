@@ -33,6 +33,9 @@ ALLOWED = [
     # the int8x4 engine at N = 256: loop-invariant values stored once in the prologue and reloaded
     # outside the GEMMs (none inside them)
     (r'_ZN3amp12vamp_persistILi8ELi(1|2|4|8|16|64)ELi4ELi[124]ELb1ELi1ELb0ELb1E', 'int8x4 at N = 256'),
+    # the eight-wave bf16x3 form (the N = 256 default): 256 registers per wave; loop-invariant
+    # addresses and constants reloaded outside the GEMMs
+    (r'_ZN3amp12vamp_persistILi4ELi(1|2|4|8|16|64)ELi8ELi[124]ELb1ELi1ELb0ELb0E', 'eight-wave bf16x3 at N = 256'),
 ]
 
 

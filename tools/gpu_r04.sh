@@ -21,6 +21,9 @@ for s in ${STEPS:-bench}; do
     bench) run bench 300 python3 bench.py ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --no-cpu-baseline ;;
     bench_h2) run bench_h2 300 python3 bench.py --no-cpu-baseline --gemm h2 ;;
+    bench_w8) run bench_w8 300 env AMP_VAMP_X3_WAVES=8 python3 bench.py --no-cpu-baseline ;;
+    trace_w8) run trace_w8 300 env AMP_VAMP_X3_WAVES=8 python3 tools/trace_persist.py --config cfg4 ;;
+    tests_w8) run tests_w8 900 env AMP_VAMP_X3_WAVES=8 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2 and not i8" ;;
     bench_i8) run bench_i8 300 python3 bench.py --no-cpu-baseline --gemm i8 ;;
     trace_i8) run trace_i8 300 env AMP_VAMP_GEMM=i8 python3 tools/trace_persist.py --config cfg4 ;;
     tests_i8) run tests_i8 900 $PYT tests/test_gpu_vamp.py -m gpu -k "i8 or split_engines" ;;
