@@ -40,16 +40,16 @@ namespace amp {
 // split into six bf16 planes in LDS (n complex per row), the operator s Uh x3-packed (K = n,
 // O = k), the result in the accumulator layout straight to ytil.  Replaces the f32-MFMA
 // gemm_store launch (47.7 us per cfg4 step at 0.56 of the f32 peak, profiles/r04_cfg4_vamp_x3.txt).
-template <int NC, int G>
-__global__ __launch_bounds__(256, 1) void ytil_x3_kernel(const float* __restrict__ y, int rows, const void* wq,
-                                                          float* __restrict__ ytil, int k) {
+template <int NC, int G, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __restrict__ y, int rows, const void* wq,
+                                                               float* __restrict__ ytil, int k) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     unsigned short* sP = reinterpret_cast<unsigned short*>(lds);
     constexpr int n = 32 * G;
     const int ldx = pl_ldx(n);
     const int row0 = blockIdx.x * PBM;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int e = tid; e < PBM * (n >> 3); e += 256) {   // 8 complex values per item, rows fastest
+    for (int e = tid; e < PBM * (n >> 3); e += 64 * NWV) {   // 8 complex values per item, rows fastest
         const int row = e % PBM, j0 = 8 * (e / PBM);
         float re[8], im[8];
 #pragma unroll
@@ -74,9 +74,9 @@ __global__ __launch_bounds__(256, 1) void ytil_x3_kernel(const float* __restrict
     }
 }
 
-template <int NC, int G>
+template <int NC, int G, int NWV = 4>
 static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* ytil, int k, hipStream_t st) {
-    const void* fn = (const void*)ytil_x3_kernel<NC, G>;
+    const void* fn = (const void*)ytil_x3_kernel<NC, G, NWV>;
     const size_t lds = (size_t)6 * PBM * pl_ldx(32 * G) * 2;
     static int attr = -1;   // once per instantiation (single-threaded host use, like the rest of the ABI)
     if (attr < 0) {
@@ -87,7 +87,7 @@ static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* yti
         }
         attr = 1;
     }
-    hipLaunchKernelGGL((ytil_x3_kernel<NC, G>), dim3(cdiv(rows, PBM)), dim3(256), lds, st, y, rows, wq, ytil, k);
+    hipLaunchKernelGGL((ytil_x3_kernel<NC, G, NWV>), dim3(cdiv(rows, PBM)), dim3(64 * NWV), lds, st, y, rows, wq, ytil, k);
     AMP_LAUNCH_CHECK("ytil_x3");
     return AMP_OK;
 }
@@ -99,7 +99,8 @@ int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil,
     switch (k) {
     case 64: return ytil_x3_launch_t<1, 4>(y, rows, wq, ytil, k, st);
     case 128: return ytil_x3_launch_t<2, 8>(y, rows, wq, ytil, k, st);
-    case 256: return ytil_x3_launch_t<4, 16>(y, rows, wq, ytil, k, st);
+    case 256:   // eight waves (two per SIMD) hide the operator stream better, as in the engine
+        return ytil_x3_launch_t<2, 16, 8>(y, rows, wq, ytil, k, st);
     default: break;
     }
     set_error("ytil_x3: n = %d / k = %d not supported", n, k);
