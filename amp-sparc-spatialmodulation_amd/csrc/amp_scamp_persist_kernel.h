@@ -93,9 +93,13 @@ __device__ __forceinline__ float block_psi(const float* xrow, int lc, int Nt, in
 // column tiles are NT1/2 (GEMM1) and NT2/2 (GEMM2), the same real columns as the f32 form.
 // H2 (with X3): the fp16x2 form (gemm_h2): every A row (x, then s = z / phi) scaled by its own
 // power of two before the split, the accumulators scaled back by 2^-(e_row + SH2_EX).
-template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false>
-__global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
-    constexpr int PWG = 256, NW = 4;
+// NWV: waves per workgroup — 4 (one per SIMD) or, for bf16x3, 8 (two per SIMD, 256 registers
+// each, half the column tiles per wave; the per-point packed denoiser is then replaced by the
+// scalar one, the 16-point alphabets keep the packed product grid: DESIGN.md §3.1, §3.8).
+template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, DecConst dc) {
+    constexpr int PWG = 64 * NWV, NW = NWV;
+    static_assert(NWV == 4 || (NWV == 8 && X3 && !H2), "eight waves: the bf16x3 form only");
     const Const64& c64 = dc;   // the rare path's float64 table; dc also the fused decision's (dec_on)
     constexpr int NC1 = X3 ? NT1 / 2 : 1, NC2 = X3 ? NT2 / 2 : 1;
     static_assert(!X3 || (NT1 % 2 == 0 && NT2 % 2 == 0), "X3: whole complex tiles");
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         if constexpr (H2) {
             // x rows in registers (item e: row e % SPB == tid % SPB), each row's max |x| over the
             // workgroup, then the scaled split into the four fp16 planes
-            constexpr int IPT = (G1 + 15) / 16;              // items per thread: SPB N / 8 / PWG, N = G1 * 8
+            constexpr int IPT = (SPB * G1 + PWG - 1) / PWG;  // items per thread: SPB N / 8 / PWG, N = G1 * 8
             const int row = tid % SPB;
             float re[IPT][8], im[IPT][8];
             float m = 0.f;
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
         if constexpr (KK > 16)
             denoise_sections_wide_m<false, KK>(pol, nrows * spr, M, P.c, pa);
         else
-            denoise_sections_u<false, KK, (KK >= 8 ? 2 : 4)>(pol, nrows * spr, M, P.c, pa);
+            denoise_sections_u<false, KK, (KK >= 8 ? 2 : 4), (NWV == 4 || KK == 16)>(pol, nrows * spr, M, P.c, pa);
         __syncthreads();
         stamp(t, 5);
         unsigned nc = 0;
@@ -554,9 +558,9 @@ __global__ __launch_bounds__(256, 1) void scamp_persist(ScampK P, DecConst dc) {
 
 int device_cu_count();
 
-template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false>
+template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false, int NWV = 4>
 static int spersist_launch_t(const ScampK& P, const DecConst& dc, hipStream_t st) {
-    const void* fn = (const void*)scamp_persist<NT1, G1, NT2, G2, KK, X3, H2>;
+    const void* fn = (const void*)scamp_persist<NT1, G1, NT2, G2, KK, X3, H2, NWV>;
     const size_t lds = (size_t)slayout(P.N, P.n, P.L, P.Lin, P.Lout, X3).total * 4;
     // the dynamic-LDS attribute and the occupancy query: once per instantiation and LDS size
     static size_t attr_lds = 0;
@@ -567,7 +571,7 @@ static int spersist_launch_t(const ScampK& P, const DecConst& dc, hipStream_t st
             set_error("scamp_persist: hipFuncSetAttribute: %s", hipGetErrorString(e));
             return AMP_E_LAUNCH;
         }
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess) per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * NWV, lds) != hipSuccess) per_cu = 0;
         attr_lds = lds;
     }
     // persist_grid_launch (amp_host.h): plain launch after the co-residency check, or the
@@ -575,18 +579,18 @@ static int spersist_launch_t(const ScampK& P, const DecConst& dc, hipStream_t st
     ScampK Pc = P;
     DecConst cc = dc;
     void* args[] = {(void*)&Pc, (void*)&cc};
-    return persist_grid_launch("scamp_persist", fn, P.nwg, 256, lds, per_cu, args, st);
+    return persist_grid_launch("scamp_persist", fn, P.nwg, 64 * NWV, lds, per_cu, args, st);
 }
 
-template <int NT1, int G1, int NT2, int G2, bool X3, bool H2 = false>
+template <int NT1, int G1, int NT2, int G2, bool X3, bool H2 = false, int NWV = 4>
 static int spersist_launch_s(const ScampK& P, const DecConst& c64, hipStream_t st) {
     switch (P.c.K) {
-    case 1: return spersist_launch_t<NT1, G1, NT2, G2, 1, X3, H2>(P, c64, st);
-    case 2: return spersist_launch_t<NT1, G1, NT2, G2, 2, X3, H2>(P, c64, st);
-    case 4: return spersist_launch_t<NT1, G1, NT2, G2, 4, X3, H2>(P, c64, st);
-    case 8: return spersist_launch_t<NT1, G1, NT2, G2, 8, X3, H2>(P, c64, st);
-    case 16: return spersist_launch_t<NT1, G1, NT2, G2, 16, X3, H2>(P, c64, st);
-    default: return spersist_launch_t<NT1, G1, NT2, G2, 64, X3, H2>(P, c64, st);
+    case 1: return spersist_launch_t<NT1, G1, NT2, G2, 1, X3, H2, NWV>(P, c64, st);
+    case 2: return spersist_launch_t<NT1, G1, NT2, G2, 2, X3, H2, NWV>(P, c64, st);
+    case 4: return spersist_launch_t<NT1, G1, NT2, G2, 4, X3, H2, NWV>(P, c64, st);
+    case 8: return spersist_launch_t<NT1, G1, NT2, G2, 8, X3, H2, NWV>(P, c64, st);
+    case 16: return spersist_launch_t<NT1, G1, NT2, G2, 16, X3, H2, NWV>(P, c64, st);
+    default: return spersist_launch_t<NT1, G1, NT2, G2, 64, X3, H2, NWV>(P, c64, st);
     }
 }
 

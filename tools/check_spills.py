@@ -36,6 +36,8 @@ ALLOWED = [
     # the eight-wave bf16x3 form (the N = 256 default): 256 registers per wave; loop-invariant
     # addresses and constants reloaded outside the GEMMs
     (r'_ZN3amp12vamp_persistILi4ELi(1|2|4|8|16|64)ELi8ELi[124]ELb1ELi1ELb0ELb0E', 'eight-wave bf16x3 at N = 256'),
+    # the eight-wave bf16x3 SCAMP form (cfg3's shape), the same kind of loop invariants
+    (r'_ZN3amp13scamp_persistILi4ELi16ELi2ELi32ELi(1|2|4|8|16|64)ELb1ELb0ELi8E', 'eight-wave bf16x3 SCAMP'),
 ]
 
 
