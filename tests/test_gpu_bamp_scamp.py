@@ -250,3 +250,23 @@ def test_scamp_fused_decision_equals_standalone(device, alph, ebn0, B, shape):
         a, b = getattr(fused, f), getattr(sep, f)
         assert (a == b) or abs(a - b) <= 1e-12 * max(abs(a), abs(b)) or (a != a and b != b), (f, a, b)
     assert int(L.loss['T']) == int(T.status().T)
+
+
+@pytest.mark.parametrize('name', ['cfg3_scamp_16qam', 'cfg3_scamp_qpsk'])
+def test_scamp_persistent_reproducible(device, name):
+    """cfg3's shape runs the SCAMP engine with eight waves per workgroup (two per SIMD; 16-QAM
+    keeps the packed product-grid denoiser there): five forwards of the same batch
+    give the same T and every Loss value, bit for bit."""
+    from scamp import SCAMP
+    ent = CURVES[name]
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    inp = _regen_inputs(cfg, 1, 8.0, svd=False)
+    det = SCAMP(cfg, engine=2)
+    first = None
+    for rep in range(5):
+        L = det(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        got = {k: float(np.asarray(v)) for k, v in L.loss.items() if np.asarray(v).ndim == 0}
+        if first is None:
+            first = got
+        else:
+            assert got == first, rep
