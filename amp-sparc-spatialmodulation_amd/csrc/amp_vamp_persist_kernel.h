@@ -19,6 +19,9 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #ifndef AMP_KK4_DU
 #define AMP_KK4_DU 4                    // QPSK sections in flight per lane group (diagnostic builds vary it)
 #endif
+#ifndef AMP_X3_W8_PIN
+#define AMP_X3_W8_PIN 0
+#endif
 #ifndef AMP_X3_W8_PKGRID
 #define AMP_X3_W8_PKGRID 1              // the eight-wave bf16x3 form keeps 16-QAM's packed grid denoiser
 #endif
@@ -72,7 +75,7 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // exponents); the results come out of the GEMM fully scaled.
 template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
-    static_assert(!X3 || ((NWV == 4 || (NWV == 8 && !H2 && !I8 && OCC == 1)) && NT % 2 == 0),
+    static_assert(!X3 || ((NWV == 4 || (NWV == 8 && !H2 && OCC == 1)) && NT % 2 == 0),
                   "X3: four waves (eight for the bf16x3 two-waves-per-SIMD form), whole complex tiles");
     static_assert(!(H2 && I8) && (!I8 || X3), "I8: a split-precision form of its own");
     // packed denoiser at one wave per SIMD; with two (OCC = 2, or the eight-wave bf16x3 form) only
@@ -83,6 +86,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
     constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
     constexpr int X3R = 1;                     // weight groups in flight (gemm_x3)
+    // eight waves: no A-fragment prefetch in gemm_x3 (the partner wave covers the LDS reads;
+    // 24 registers fewer) when AMP_X3_W8_PIN (A/B builds)
+    constexpr bool X3PIN = NWV == 8 && AMP_X3_W8_PIN;
     const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         } else if constexpr (H2)
             gemm_h2<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
         else if constexpr (X3)
-            gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx1, cc0, cr, ci);
+            gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, P.Wx1, cc0, cr, ci);
         else
             gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
         float hsc[4];                                 // H2: 2^-(e_row + H2_EX) of this lane's rows
@@ -576,7 +582,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
                     for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
             } else {
-                gemm_x3<NC, G3, X3R>(sP, ldx, P.Wx2, cc0, cr, ci);
+                gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, P.Wx2, cc0, cr, ci);
             }
             // the lane index pinned here: the 4 NC LDS addresses below are then formed in this
             // epilogue instead of being hoisted out of the iteration loop (and kept live across it)

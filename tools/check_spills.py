@@ -32,7 +32,7 @@ ALLOWED = [
     (r'_ZN3amp12vamp_persistILi8ELi64ELi4ELi1ELb[01]ELi1ELb[01]E', '64-point alphabet at N = 256'),
     # the int8x4 engine at N = 256: loop-invariant values stored once in the prologue and reloaded
     # outside the GEMMs (none inside them)
-    (r'_ZN3amp12vamp_persistILi8ELi(1|2|4|8|16|64)ELi4ELi[124]ELb1ELi1ELb0ELb1E', 'int8x4 at N = 256'),
+    (r'_ZN3amp12vamp_persistILi(8|4)ELi(1|2|4|8|16|64)ELi(4|8)ELi[124]ELb1ELi1ELb0ELb1E', 'int8x4 at N = 256 (opt-in)'),
     # the eight-wave bf16x3 form (the N = 256 default): 256 registers per wave; loop-invariant
     # addresses and constants reloaded outside the GEMMs
     (r'_ZN3amp12vamp_persistILi4ELi(1|2|4|8|16|64)ELi8ELi[124]ELb1ELi1ELb0ELb0E', 'eight-wave bf16x3 at N = 256'),

@@ -24,6 +24,10 @@ for s in ${STEPS:-bench}; do
     bench_w8) run bench_w8 300 env AMP_VAMP_X3_WAVES=8 python3 bench.py --no-cpu-baseline ;;
     trace_w8) run trace_w8 300 env AMP_VAMP_X3_WAVES=8 python3 tools/trace_persist.py --config cfg4 ;;
     tests_w8) run tests_w8 900 env AMP_VAMP_X3_WAVES=8 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2 and not i8" ;;
+    ab_w8) run ab_def 300 python3 bench.py --no-cpu-baseline &&
+           run ab_pin 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_w8pin.so python3 bench.py --no-cpu-baseline &&
+           run ab_du1 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_w8du1.so python3 bench.py --no-cpu-baseline &&
+           run ab_def2 300 python3 bench.py --no-cpu-baseline ;;
     bench_i8) run bench_i8 300 python3 bench.py --no-cpu-baseline --gemm i8 ;;
     trace_i8) run trace_i8 300 env AMP_VAMP_GEMM=i8 python3 tools/trace_persist.py --config cfg4 ;;
     tests_i8) run tests_i8 900 $PYT tests/test_gpu_vamp.py -m gpu -k "i8 or split_engines" ;;
