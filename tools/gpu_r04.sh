@@ -42,6 +42,10 @@ for s in ${STEPS:-bench}; do
     tests_cfg5) run tests_cfg5 900 $PYT tests/test_gpu_cfg5.py -m gpu ;;
     tests_bs) run tests_bs 900 $PYT tests/test_gpu_bamp_scamp.py -m gpu ;;
     tests) run tests 1100 $PYT tests -m gpu ;;
+    # occ2 needs the diagnostic libraries, built in the container first:
+    #   make -C amp-sparc-spatialmodulation_amd/csrc SPILLCHECK=true OBJDIR=../build_diag2 \
+    #     OUT=../lib_diag/libampsparc_pk_du2.so CXXFLAGS="<Makefile flags> -DAMP_OCC2_PK=1 -DAMP_KK4_DU=2" \
+    #     ../lib_diag/libampsparc_pk_du2.so        (and the same with DU=4 -> _pk_du4)
     occ2) run occ2_prod 300 python3 tools/occ2_repro.py 10 &&
           run occ2_pk4 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du4.so python3 tools/occ2_repro.py 10 &&
           run occ2_pk2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pk_du2.so python3 tools/occ2_repro.py 10 ;;
