@@ -24,8 +24,8 @@ constexpr int BRWG = 1024;
 
 struct alignas(16) BampIter {
     int32_t stopped, T, fixed, fixed_all;
-    // exact float64 fix-up of iteration T-1 pending (set by bamp_r, done by bamp_fix_sec, settled
-    // by bamp_fin): the exact batch max |xi| G, the float32 estimate's slack, the allclose count
+    // exact float64 fix-up of iteration T-1 pending (set by bamp_r, done and settled by
+    // bamp_fixall): the exact batch max |xi| G, the float32 estimate's slack, the allclose count
     // before the fix-up
     double G, slack;
     uint32_t notclose;
@@ -68,6 +68,8 @@ struct BampK {
     int h2, rows_pad;
     unsigned short* ap;    // [4 planes][rows_pad][max(N, n)] fp16
     int* rexp;             // [rows_pad] row exponents
+    // launch engine: rcnt[1] is bamp_fixall's arrival counter (zeroed by bamp_init_kernel)
+    unsigned* rcnt;
 };
 
 // BAMP's fp16x2 operator scale exponent (the opt-in AMP_GEMM_H2 form): every operator piece is
@@ -126,6 +128,7 @@ struct BampWs {
     float *secmax, *secabs;
     Partial* parts;
     BampIter* iters;
+    unsigned* rcnt;
     size_t bytes;
 };
 
@@ -163,6 +166,7 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.band[2] = cv.take<int>((size_t)2 * (P.ncpB1 / 128));
     w.band[3] = cv.take<int>((size_t)2 * (P.ncpB2 / P.bn));
     w.xs = cv.take<XState>(1);
+    w.rcnt = cv.take<unsigned>(16);
     w.ap = nullptr;
     w.rexp = nullptr;
     if (bamp_h2_shape(d)) {
@@ -359,10 +363,11 @@ __device__ __forceinline__ void bamp_finish(const BampK& P, int t, uint32_t notc
 // Reduction and allclose decision (bamp.py:140).  The rare exact-float64 path (a section's
 // normaliser out of the float64 range against the batch-global shift, amp_denoise.h) is spread
 // over the grid as SCAMP's is: this workgroup only settles the exact batch max |xi| G over the
-// candidate sections and leaves a pending record; bamp_fix_sec recomputes the out-of-range
+// candidate sections and leaves a pending record; bamp_fix_sec_body recomputes the out-of-range
 // sections (a grid kernel: at 64-QAM on a failing detector most sections of the batch take this
 // path every iteration, 314 ms per cfg5 detection when one workgroup recomputed them all), and
-// bamp_fin adds the per-block counts and decides the early exit.
+// bamp_fin adds the per-block counts and decides the early exit (both in one launch, bamp_fixall,
+// in the whole-batch engine; the trial-sharded stages split this work, bamp_xr*).
 __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
     __shared__ __attribute__((aligned(16))) float lds[512];
     __shared__ double s_d[BRWG / 64];
@@ -406,7 +411,8 @@ __global__ __launch_bounds__(BRWG) void bamp_r(BampK P, Const64 c64, int t) {
     }
 }
 
-// per-block counts of bamp_fix_sec, written over iteration t's partials (consumed by bamp_r):
+// per-block counts of bamp_fix_sec_body, written over iteration t's partials (consumed by
+// bamp_r):
 // slot i = {sections fixed, allclose delta} of block i
 __device__ __forceinline__ int2* bamp_fix_counts(const BampK& P, int t) {
     return reinterpret_cast<int2*>(P.parts + (size_t)t * P.nblk);
@@ -424,10 +430,8 @@ __device__ __forceinline__ int bamp_block_sum_int(int v, int* s_i) {
 
 // the out-of-range sections of a pending record, recomputed with the reference's exact float64
 // op sequence (exact_section_f64): xmmse, var and the allclose delta against the previous var
-__global__ __launch_bounds__(AMP_WG) void bamp_fix_sec(BampK P, Const64 c64, int t) {
-    __shared__ int s_i[AMP_WG / 64];
-    const BampIter pend = P.iters[t + 1];
-    if (!pend.active || P.iters[t].stopped) return;
+__device__ __forceinline__ void bamp_fix_sec_body(const BampK& P, const Const64& c64, int t, const BampIter& pend,
+                                                  int* s_i) {
     const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
     float2* x2 = reinterpret_cast<float2*>(P.xm);
     const float* cov = P.cov;
@@ -456,16 +460,20 @@ __global__ __launch_bounds__(AMP_WG) void bamp_fix_sec(BampK P, Const64 c64, int
     if (threadIdx.x == 0) bamp_fix_counts(P, t)[blockIdx.x] = make_int2(cnt, dnc);
 }
 
-__global__ __launch_bounds__(AMP_WG) void bamp_fin(BampK P, int t, int nfix) {
+// bamp_fix_sec_body, then (last workgroup to arrive) bamp_fin's count and exit decision: one launch
+__global__ __launch_bounds__(AMP_WG) void bamp_fixall(BampK P, Const64 c64, int t) {
     __shared__ int s_i[AMP_WG / 64];
     const BampIter pend = P.iters[t + 1];
     if (!pend.active || P.iters[t].stopped) return;
-    const int2* c = bamp_fix_counts(P, t);
-    int fixed = 0, dnc = 0;
-    for (int i = threadIdx.x; i < nfix; i += blockDim.x) { fixed += c[i].x; dnc += c[i].y; }
-    fixed = bamp_block_sum_int(fixed, s_i);
-    dnc = bamp_block_sum_int(dnc, s_i);
-    if (threadIdx.x == 0) bamp_finish(P, t, (uint32_t)((int)pend.notclose + dnc), fixed);
+    bamp_fix_sec_body(P, c64, t, pend, s_i);
+    if (last_arrival(P.rcnt + 1, gridDim.x)) {
+        const int2* c = bamp_fix_counts(P, t);
+        int fixed = 0, dnc = 0;
+        for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) { fixed += c[i].x; dnc += c[i].y; }
+        fixed = bamp_block_sum_int(fixed, s_i);
+        dnc = bamp_block_sum_int(dnc, s_i);
+        if (threadIdx.x == 0) bamp_finish(P, t, (uint32_t)((int)pend.notclose + dnc), fixed);
+    }
 }
 
 // Tracker (bamp.py:13-25): xmmse = 0, var(prev) = 1, z = y, u = 0 + sigma2 -> 1/u.
@@ -627,6 +635,7 @@ __global__ void bamp_init_kernel(BampK P) {
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        P.rcnt[0] = 0u; P.rcnt[1] = 0u;
         BampIter it{};
         it.stopped = 0; it.T = 0; it.fixed = 0; it.fixed_all = 0;
         P.iters[0] = it;
@@ -735,6 +744,7 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.secmax = w.secmax; P.secabs = w.secabs; P.parts = w.parts; P.iters = w.iters; P.status = (amp_status*)a->status;
     P.c = to_const(c);
     P.xs = w.xs;
+    P.rcnt = w.rcnt;
     {
         // block-banded H: the ranges are formed by the prepare launch sequence (AMP_BAND_GEMM=0: off)
         const char* e = getenv("AMP_BAND_GEMM");
@@ -845,14 +855,13 @@ static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st
 }
 
 // One BAMPLayer.forward (bamp.py:48-64) + the allclose test of bamp.py:140 (no-op once stopped).
+// bamp_fixall is a no-op unless bamp_r left a pending record (nfix blocks' counts fit the
+// iteration's nblk partial slots).
 static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStream_t st) {
     bamp_gemms(P, c64, t, st);
     hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
-    // the rare path's grid fix-up: no-ops unless bamp_r left a pending record (nfix blocks'
-    // counts fit the iteration's nblk partial slots)
     const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
-    hipLaunchKernelGGL(bamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
-    hipLaunchKernelGGL(bamp_fin, dim3(1), dim3(AMP_WG), 0, st, P, t, nfix);
+    hipLaunchKernelGGL(bamp_fixall, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("bamp iteration");
     return AMP_OK;
 }

@@ -285,6 +285,28 @@ __device__ __forceinline__ PartAcc part_reduce_all(const Partial* src, int nblk,
     return o;
 }
 
+// True in the workgroup that arrives last at `cnt` among the launch's `nblk` workgroups (the
+// launch engines' "last block" fold: the batch reduction runs there instead of in a launch of its
+// own).  Every workgroup's global stores before the call are visible to the last one (agent-scope
+// release on arrival, acquire in the last); the last resets the counter for the next launch.
+// Every workgroup of the launch must call it (or none: an early-exiting launch leaves it at 0).
+__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned nblk) {
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = k + 1 == nblk;
+        if (last) {
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
 // A section whose max logit lies more than |AMP_DANGER| below the batch max|xi| leaves the
 // normal float64 range in the reference's softmax exp(xi - max|xi|) (vamp.py:112): its
 // normaliser Z is denormal or zero, so c128 / Z (= * (1/Z)) overflows to inf/NaN, and for

@@ -168,38 +168,59 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         wcol[j] = reinterpret_cast<const float4*>(wp) + ((size_t)((col0 >> 5) + wave * C::NACC + j) * G) * 64 + lane;
 
     if (ke < 0) ke = kap;
+    const int glast = (ke >> 3) - 1;   // last group of the range
+    // The W ring runs across the chunks: a slot refilled GRING groups ahead past the end of a
+    // chunk already holds the next chunk's group (every chunk is a whole number of rings), so a
+    // chunk starts without waiting on its first operator loads.
+    float4 ring[GRING][C::NACC];
+#pragma unroll
+    for (int d = 0; d < GRING; ++d)
+#pragma unroll
+        for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)((kb >> 3) + d) * 64];
+    // A chunk staging: all loads of a batch in flight before its LDS stores.  Short chunks
+    // (KC <= 256: 8 float4 per thread) load the NEXT chunk into registers while this one's MFMAs
+    // run; 512-wide chunks stage in two half-batches between the chunks.
+    constexpr int PER = GBM * (KC / 4) / AMP_WG;    // float4 per thread for a full chunk
+    constexpr bool PF = PER <= 8;
+    float4 nxt[PF ? PER : 1];
+    auto load_chunk = [&](int c0, float4* t4, int h, int cnt) {
+        const int q4 = min(KC, ke - c0) >> 2, nq = GBM * q4;
+#pragma unroll
+        for (int i = 0; i < cnt; ++i) {
+            const int e = tid + (h + i) * AMP_WG;
+            const int row = e / q4, k4 = e - row * q4;
+            t4[i] = (e < nq) ? al(row0 + row, c0 + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store_chunk = [&](int c0, const float4* t4, int h, int cnt) {
+        const int q4 = min(KC, ke - c0) >> 2, nq = GBM * q4;
+#pragma unroll
+        for (int i = 0; i < cnt; ++i) {
+            const int e = tid + (h + i) * AMP_WG;
+            const int row = e / q4, k4 = e - row * q4;
+            if (e < nq) *reinterpret_cast<float4*>(lds + row * LDA + 4 * k4) = t4[i];
+        }
+    };
+    if constexpr (PF) {
+        load_chunk(kb, nxt, 0, PER);
+        store_chunk(kb, nxt, 0, PER);
+    }
     for (int kc0 = kb; kc0 < ke; kc0 += KC) {
         const int kc = min(KC, ke - kc0);
-        const int q4 = kc >> 2;   // float4 per A row in this chunk
         const int g0 = kc0 >> 3, gc = kc >> 3;   // gc % GRING == 0 (kap % 64 == 0)
-        // W ring first: its latency overlaps the A staging
-        float4 ring[GRING][C::NACC];
+        if constexpr (PF) {
+            __syncthreads();   // this chunk's LDS stores are visible
+            if (kc0 + KC < ke) load_chunk(kc0 + KC, nxt, 0, PER);
+        } else {
+            if (kc0 > kb) __syncthreads();   // every wave is done with the previous chunk
 #pragma unroll
-        for (int d = 0; d < GRING; ++d)
-#pragma unroll
-            for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)(g0 + d) * 64];
-        if (kc0 > kb) __syncthreads();   // every wave is done with the previous chunk
-        // stage A[row0 .. row0+32) x [kc0, kc0+kc) (the loader forms fused prologues): all loads
-        // of a half-batch in flight before its LDS stores
-        constexpr int PER = GBM * (KC / 4) / AMP_WG;    // float4 per thread for a full chunk
-        const int nq = GBM * q4;
-#pragma unroll
-        for (int h = 0; h < PER; h += PER / 2) {
-            float4 t4[PER / 2];
-#pragma unroll
-            for (int i = 0; i < PER / 2; ++i) {
-                const int e = tid + (h + i) * AMP_WG;
-                const int row = e / q4, k4 = e - row * q4;
-                t4[i] = (e < nq) ? al(row0 + row, kc0 + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int h = 0; h < PER; h += PER / 2) {
+                float4 t4[PER / 2];
+                load_chunk(kc0, t4, h, PER / 2);
+                store_chunk(kc0, t4, h, PER / 2);
             }
-#pragma unroll
-            for (int i = 0; i < PER / 2; ++i) {
-                const int e = tid + (h + i) * AMP_WG;
-                const int row = e / q4, k4 = e - row * q4;
-                if (e < nq) *reinterpret_cast<float4*>(lds + row * LDA + 4 * k4) = t4[i];
-            }
+            __syncthreads();
         }
-        __syncthreads();
         // Per group: read the NEXT group's A fragment, issue this group's MFMAs, then refill this
         // ring slot GRING groups ahead.  The scheduling barrier pins that order (left alone, the
         // scheduler sinks all refills behind the MFMAs and drains them at once).
@@ -217,12 +238,19 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
                     acc[j] = mfma32x32x2(acur.z, ring[d][j].z, acc[j]);
                     acc[j] = mfma32x32x2(acur.w, ring[d][j].w, acc[j]);
                 }
-                // refill GRING groups ahead (clamped: the tail re-reads its last group)
-                const int gn = min(g + GRING, gc - 1);
+                // refill GRING groups ahead, into the next chunk (clamped: the tail of the range
+                // re-reads its last group)
+                const int gn = min(g0 + g + GRING, glast);
 #pragma unroll
-                for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)(g0 + gn) * 64];
+                for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)gn * 64];
                 acur = anext;
                 __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (PF) {
+            if (kc0 + KC < ke) {
+                __syncthreads();   // every wave is done with this chunk
+                store_chunk(kc0 + KC, nxt, 0, PER);
             }
         }
     }

@@ -21,8 +21,8 @@ constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in register
 
 struct alignas(16) ScampIter {
     int32_t stopped, T, fixed, fixed_all;
-    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done by scamp_fix_*,
-    // settled by scamp_fin): the exact batch max |xi| G, the float32 estimate's slack, and the
+    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done and settled by
+    // scamp_fixall; scamp_fix_* and scamp_sxr* in the trial-sharded stages): the exact batch max |xi| G, the float32 estimate's slack, and the
     // allclose count before the fix-up
     double G, slack;
     uint32_t notclose;
@@ -77,6 +77,8 @@ struct ScampK {
     DecWG* dwg;            // [nwg] per-workgroup records
     amp_counts* counts;    // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_scamp_persist_trace), else null
+    // launch engine: rcnt[1] is scamp_fixall's arrival counter (zeroed by scamp_init_kernel)
+    unsigned* rcnt;
     Const c;
 };
 

@@ -60,6 +60,13 @@ for s in ${STEPS:-bench}; do
     tests_model) run tests_model 600 $PYT tests/test_gpu_vamp.py -m gpu -k "device or random or model" ;;
     tprobe) run tprobe 300 python3 tools/t_probe.py ;;
     tests_vdef) run tests_vdef 900 $PYT tests/test_gpu_vamp.py -m gpu -k "persistent and not f32 and not h2" ;;
+    isi) run isi 300 python3 tools/isi_bench.py 512 50 ;;
+    isi_bn256) run isi_bn256 300 env AMP_SECTION_BN=256 python3 tools/isi_bench.py 512 50 ;;
+    isiprofB) run isiprof256 300 rocprofv3 --kernel-trace --stats -d "$OUT/isiprof256" -o isi --output-format csv -- python3 tools/isi_bench.py 256 50 &&
+              run isiprof1024 300 rocprofv3 --kernel-trace --stats -d "$OUT/isiprof1024" -o isi --output-format csv -- python3 tools/isi_bench.py 1024 50 ;;
+    isipmc) run isipmc 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/isipmc" -o pmc --output-format csv -- python3 tools/isi_bench.py 512 10 ;;
+    isiprof) run isiprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/isiprof" -o isi --output-format csv -- python3 tools/isi_bench.py 512 50 ;;
+    tests_launch) run tests_launch 1100 $PYT tests/test_gpu_bamp_scamp.py tests/test_gpu_cfg5.py tests/test_gpu_published.py tests/test_gpu_shard_trials.py tests/test_gpu_rescue.py tests/test_gpu_isi_model.py tests/test_gpu_segmented.py tests/test_gpu_random.py -m gpu ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     profile) run profile 900 bash tools/profile.sh ;;
     ubench) run ubench 300 bash tools/ubench/run.sh ;;
