@@ -67,6 +67,9 @@ for s in ${STEPS:-bench}; do
     isipmc) run isipmc 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/isipmc" -o pmc --output-format csv -- python3 tools/isi_bench.py 512 10 ;;
     isitcc) run isitcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE -d "$OUT/isitcc" -o tcc --output-format csv -- python3 tools/isi_bench.py 512 10 ;;
     isi_ka4) run isi_ka4 300 env AMP_SCAMP_KA_WAVES=4 python3 tools/isi_bench.py 512 50 ;;
+    isi_wnt) run isi_def 300 python3 tools/isi_bench.py 512 50 &&
+             run isi_wnt 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_wnt.so python3 tools/isi_bench.py 512 50 &&
+             run isi_def2 300 python3 tools/isi_bench.py 512 50 ;;
     isiprof) run isiprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/isiprof" -o isi --output-format csv -- python3 tools/isi_bench.py 512 50 ;;
     tests_launch) run tests_launch 1100 $PYT tests/test_gpu_bamp_scamp.py tests/test_gpu_cfg5.py tests/test_gpu_published.py tests/test_gpu_shard_trials.py tests/test_gpu_rescue.py tests/test_gpu_isi_model.py tests/test_gpu_segmented.py tests/test_gpu_random.py -m gpu ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
