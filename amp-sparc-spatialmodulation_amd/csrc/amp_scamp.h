@@ -21,8 +21,9 @@ constexpr int SMAXLIN = 64;     // coupling blocks per trial handled in register
 
 struct alignas(16) ScampIter {
     int32_t stopped, T, fixed, fixed_all;
-    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done and settled by
-    // scamp_fixall; scamp_fix_* and scamp_sxr* in the trial-sharded stages): the exact batch max |xi| G, the float32 estimate's slack, and the
+    // exact float64 fix-up of iteration T-1 pending (set by scamp_r, done by scamp_fix_sec and
+    // scamp_fix_psi_fin, settled by the latter; scamp_fix_* and scamp_sxr* in the trial-sharded
+    // stages): the exact batch max |xi| G, the float32 estimate's slack, and the
     // allclose count before the fix-up
     double G, slack;
     uint32_t notclose;
@@ -77,7 +78,7 @@ struct ScampK {
     DecWG* dwg;            // [nwg] per-workgroup records
     amp_counts* counts;    // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_scamp_persist_trace), else null
-    // launch engine: rcnt[1] is scamp_fixall's arrival counter (zeroed by scamp_init_kernel)
+    // launch engine: rcnt[1] is scamp_fix_psi_fin's arrival counter (zeroed by scamp_init_kernel)
     unsigned* rcnt;
     Const c;
 };

@@ -236,10 +236,11 @@ __global__ __launch_bounds__(AMP_WG) void scamp_psi(ScampK P, int t) {
 
 // Rare path (float64 fix-up) spread over the grid.  scamp_r reduces the partials and, when some
 // section may leave the float64 range, settles the exact batch max |xi| G (one workgroup: few
-// candidate sections); scamp_fixall recomputes the out-of-range sections with the reference's exact
-// arithmetic and their coupling blocks' psi (and the allclose delta), and its last workgroup adds
-// the counts and decides the early exit.  Without a pending fix-up it returns at once.  The
-// trial-sharded stages split the same work over scamp_fix_sec / scamp_fix_psi.  (Before: one
+// candidate sections); scamp_fix_sec recomputes the out-of-range sections with the reference's
+// exact arithmetic, scamp_fix_psi_fin their coupling blocks' psi (and the allclose delta), each a
+// grid kernel, and the last workgroup of the second adds the per-block counts and decides the
+// early exit.  Without a pending fix-up both return at once.  The trial-sharded stages run
+// scamp_fix_sec / scamp_fix_psi and settle the counts across ranks.  (Before: one
 // workgroup recomputed every such section, 267 us per iteration at cfg3's NaN onset.)
 __device__ __forceinline__ void scamp_finish(const ScampK& P, int t, uint32_t notclose, int fixed, int fixed_all) {
     ScampIter nx;
@@ -355,10 +356,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_fix_sec(ScampK P, Const64 c64, i
     if (threadIdx.x == 0) scamp_fix_counts(P, t)[blockIdx.x].x = cnt;
 }
 
-__global__ __launch_bounds__(AMP_WG) void scamp_fix_psi(ScampK P, int t) {
-    __shared__ int s_i[AMP_WG / 64];
-    const ScampIter pend = P.iters[t + 1];
-    if (!pend.active || P.iters[t].stopped) return;
+__device__ __forceinline__ void scamp_fix_psi_body(const ScampK& P, int t, const ScampIter& pend, int* s_i) {
     const float* psi_prev = spsi(P, t + 1);
     float* psi_new = spsi(P, t);
     const int spb = P.Nt / P.M;   // sections per coupling block
@@ -382,57 +380,21 @@ __global__ __launch_bounds__(AMP_WG) void scamp_fix_psi(ScampK P, int t) {
     if (threadIdx.x == 0) scamp_fix_counts(P, t)[blockIdx.x].y = dnc;
 }
 
-// scamp_fix_sec + scamp_fix_psi + scamp_fin in one launch (the whole-batch launch engine): one
-// wavefront per (trial, coupling block), its lanes over the block's sections, so the block's psi
-// (lane 0, scamp_fix_psi's serial float64 sum) follows its own sections' fix-up without a grid
-// barrier; the last workgroup to arrive adds the counts and settles the exit (scamp_fin).
-__global__ __launch_bounds__(AMP_WG) void scamp_fixall(ScampK P, Const64 c64, int t) {
+__global__ __launch_bounds__(AMP_WG) void scamp_fix_psi(ScampK P, int t) {
     __shared__ int s_i[AMP_WG / 64];
     const ScampIter pend = P.iters[t + 1];
     if (!pend.active || P.iters[t].stopped) return;
-    const float2* xp2 = reinterpret_cast<const float2*>(P.xmap);
-    float2* x2 = reinterpret_cast<float2*>(P.xm);
-    const int M = P.M, Nt = P.Nt, Lin = P.Lin, spb = P.Nt / P.M;
-    const float* psi_prev = spsi(P, t + 1);
-    float* psi_new = spsi(P, t);
-    const int lane = threadIdx.x & 63, nwave = gridDim.x * (AMP_WG / 64);
-    int cnt = 0, dnc = 0;
-    for (int blk = blockIdx.x * (AMP_WG / 64) + (threadIdx.x >> 6); blk < P.B * Lin; blk += nwave) {
-        int hit = 0;
-        for (int j = lane; j < spb; j += 64) {
-            const int sct = blk * spb + j;
-            if (!((double)P.secmax[sct] - pend.G < AMP_DANGER + pend.slack)) continue;
-            const size_t o0 = (size_t)sct * M;
-            const float tv = P.tau[blk];   // blk = b * Lin + lc
-            auto ld = [=](int m, float& rr, float& ri, float& it) {
-                const float2 v = xp2[o0 + m];
-                rr = v.x; ri = v.y; it = 1.0f / (tv * 0.5f);
-            };
-            auto st = [=](int m, float xr, float xi, float) { x2[o0 + m] = make_float2(xr, xi); };
-            exact_section_f64<false>(ld, st, M, c64, pend.G);
-            ++cnt;
-            hit = 1;
-        }
-        if (__any(hit)) {   // wave-uniform: the block's psi from its fixed sections (lane 0)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (lane == 0) {
-                const float2* xr = reinterpret_cast<const float2*>(P.xm) + (size_t)blk * Nt;
-                double ssum = 0.0;
-                for (int m = 0; m < Nt; ++m) {
-                    const float a = (float)sqrt((double)xr[m].x * xr[m].x + (double)xr[m].y * xr[m].y);
-                    ssum += (double)(a * a);
-                }
-                const float ps = 1.0f - (float)ssum / (float)P.Na;
-                dnc += (torch_close(ps, psi_prev[blk]) ? 0 : 1) - (torch_close(psi_new[blk], psi_prev[blk]) ? 0 : 1);
-                psi_new[blk] = ps;
-            }
-        }
-    }
-    cnt = block_sum_int(cnt, s_i);
-    dnc = block_sum_int(dnc, s_i);
-    if (threadIdx.x == 0) scamp_fix_counts(P, t)[blockIdx.x] = make_int2(cnt, dnc);
+    scamp_fix_psi_body(P, t, pend, s_i);
+}
+
+// scamp_fix_psi, then (last workgroup to arrive) scamp_fin's count and exit decision over both
+// fix-up launches' per-block counts: one launch fewer per iteration.  scamp_fix_sec stays a launch
+// of its own (one thread per section: the exact float64 recompute is the rare path's cost).
+__global__ __launch_bounds__(AMP_WG) void scamp_fix_psi_fin(ScampK P, int t) {
+    __shared__ int s_i[AMP_WG / 64];
+    const ScampIter pend = P.iters[t + 1];
+    if (!pend.active || P.iters[t].stopped) return;
+    scamp_fix_psi_body(P, t, pend, s_i);
     if (last_arrival(P.rcnt + 1, gridDim.x)) {
         const int2* c = scamp_fix_counts(P, t);
         int fixed = 0, d = 0;
@@ -777,22 +739,22 @@ static int scamp_prepare_impl(const ScampK& P, const amp_scamp_args* a, hipStrea
 
 // One SCAMPLayer.forward (scamp.py:43-59) + the allclose(psi) test of scamp.py:105: the two GEMM
 // launches (+ scamp_psi when a tile holds part of a coupling block), the batch reduction and the
-// rare path's fix-up with its exit decision (scamp_fixall: it returns at once unless scamp_r left
-// a pending record).  The reduction keeps a launch of its own: folded into the last workgroup of
+// rare path's fix-up with its exit decision (scamp_fix_sec, scamp_fix_psi_fin: they return at once
+// unless scamp_r left a pending record).  The reduction keeps a launch of its own: folded into the last workgroup of
 // the GEMM launch it needs an agent-scope release per workgroup (an L2 write-back on every XCD),
 // which cost more than the launch (scamp_psi 6.9 -> 40 us at the ISI shape).
 static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStream_t st) {
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
-    // fix-up grid: a wavefront per (trial, coupling block), one count slot per workgroup in
-    // iteration t's partials (consumed by then)
-    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.Lin, AMP_WG / 64)));
+    // fix-up grid: one slot per block in iteration t's partials (consumed by then)
+    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
     launch_ka(P, gr, t, st);
     launch_kb(P, gr, ldsB, t, st);
     if (P.psi_split)
         hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);
     hipLaunchKernelGGL(scamp_r, dim3(1), dim3(SRWG), 0, st, P, c64, t);
-    hipLaunchKernelGGL(scamp_fixall, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(scamp_fix_sec, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
+    hipLaunchKernelGGL(scamp_fix_psi_fin, dim3(nfix), dim3(AMP_WG), 0, st, P, t);
     AMP_LAUNCH_CHECK("scamp iteration");
     return AMP_OK;
 }

@@ -35,6 +35,8 @@ for s in ${STEPS:-bench}; do
     trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;
     trace_h2) run trace_h2 300 env AMP_VAMP_GEMM=h2 python3 tools/trace_persist.py --config cfg4 ;;
     configs) run configs 600 python3 tools/configs_bench.py ;;
+    cfg5) run cfg5 600 python3 tools/cfg5_bench.py ;;
+    cfg3l) run cfg3l 300 python3 tools/configs_bench.py cfg3-launches ;;
     cfg3) run cfg3 300 python3 tools/configs_bench.py cfg3 cfg3-qpsk ;;
     cfg3w4) run cfg3w4 300 env AMP_SCAMP_X3_WAVES=4 python3 tools/configs_bench.py cfg3 cfg3-qpsk ;;
     tests_vamp) run tests_vamp 900 $PYT tests/test_gpu_vamp.py -m gpu ;;
