@@ -72,6 +72,8 @@ for s in ${STEPS:-bench}; do
     isi_wnt) run isi_def 300 python3 tools/isi_bench.py 512 50 &&
              run isi_wnt 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_wnt.so python3 tools/isi_bench.py 512 50 &&
              run isi_def2 300 python3 tools/isi_bench.py 512 50 ;;
+    isi_bkc) run isi_bkc256 300 python3 tools/isi_bench.py 512 50 &&
+             run isi_bkc512 300 env AMP_BAMP_KC=512 python3 tools/isi_bench.py 512 50 ;;
     isiprof) run isiprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/isiprof" -o isi --output-format csv -- python3 tools/isi_bench.py 512 50 ;;
     tests_launch) run tests_launch 1100 $PYT tests/test_gpu_bamp_scamp.py tests/test_gpu_cfg5.py tests/test_gpu_published.py tests/test_gpu_shard_trials.py tests/test_gpu_rescue.py tests/test_gpu_isi_model.py tests/test_gpu_segmented.py tests/test_gpu_random.py -m gpu ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
