@@ -114,6 +114,8 @@ SIGNATURES = {
     'amp_map_decide_count_rows': (C.c_int, [_D, _K, _P, _P, _P, _P, _P, _I, C.c_int64, _P, _P, _P, C.c_size_t, _P]),
     'amp_vamp_detect_count_epochs': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
                                                _P]),
+    'amp_vamp_detect_count_epochs_ch': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
+                                                  C.c_int64, C.c_int64, C.c_int64, _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_bamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
@@ -186,7 +188,11 @@ def lib():
                                'there is no CPU fallback)')
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None:
+                if os.environ.get('AMP_LIB_PATH'):   # an A/B build that predates this entry point
+                    continue
+                raise AttributeError(f'{LIB_PATH}: undefined symbol {name} (stale build: run __graft_entry__.build())')
             f.restype = res
             f.argtypes = args
         _lib = L

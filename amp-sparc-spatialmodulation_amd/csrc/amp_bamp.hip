@@ -184,18 +184,22 @@ __device__ __forceinline__ float* bvar(const BampK& P, int t) { return (t & 1) ?
 __device__ __forceinline__ int bkb(const BampK& P, int w, int cb) { return P.band[w] ? P.band[w][2 * cb] : 0; }
 __device__ __forceinline__ int bke(const BampK& P, int w, int cb) { return P.band[w] ? P.band[w][2 * cb + 1] : -1; }
 
+// KC: the A chunk of the f32 tile (GKC; 256 for the block-banded H, whose short reduction ranges
+// need no longer chunks: 33 KB of LDS, four tiles per CU instead of two; the fp16x2 tile only in
+// the GKC instantiations).  The chunking does not change the MFMA order: the same bits.
 // v = |H|^2 var (bamp.py:59)
+template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (P.h2)
+    if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds, bkb(P, 0, tile.cb),
                                        bke(P, 0, tile.cb));
     else
-        gemm_tile<128>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds,
-                       bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
+        gemm_tile<128, ALoadPlain, KC>(ALoadPlain{bvar(P, t + 1), P.N, P.B, P.N}, P.Wabs2, P.kapA1, row0, col0, lds,
+                                       bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -205,18 +209,19 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
 }
 
 // z = H xmmse - v (y - z) / u ; u = v + sigma2 ; s = (y - z) / u   (bamp.py:60-63)
+template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (P.h2)
+    if (KC == GKC && P.h2)
         gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds, bkb(P, 1, tile.cb),
                                        bke(P, 1, tile.cb));
     else
-        gemm_tile<128>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds, bkb(P, 1, tile.cb),
-                       bke(P, 1, tile.cb));
+        gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds,
+                                       bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
         const int rho = e >> 6, cp = e & 63;           // complex column pair
@@ -238,17 +243,18 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
 }
 
 // cov = 1 / (|H|^2^T (1/u))   (bamp.py:62)
+template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (P.h2)
+    if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds, bkb(P, 2, tile.cb),
                                        bke(P, 2, tile.cb));
     else
-        gemm_tile<128>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds, bkb(P, 2, tile.cb),
-                       bke(P, 2, tile.cb));
+        gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.invu, P.n, P.B, P.n}, P.Wabs2T, P.kapB1, row0, col0, lds,
+                                       bkb(P, 2, tile.cb), bke(P, 2, tile.cb));
     using C = GemmCfg<128>;
     for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
         const int rho = e >> 7, cc = e & 127;
@@ -290,20 +296,20 @@ struct BampDenoisePolicy {
 };
 
 // xmap = xmmse + cov (H^H s) ; xmmse, var = denoiser(xmap, cov/2)   (bamp.py:63-64)
-template <int BN, int KK>
+template <int BN, int KK, int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    using C = GemmCfg<BN>;
-    const GemmTile tile = P.h2 ? xcd_tile_rows() : xcd_tile();
+    using C = GemmCfg<BN, KC>;
+    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (P.h2)
+    if (KC == GKC && P.h2)
         gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds, bkb(P, 3, tile.cb),
                                bke(P, 3, tile.cb));
     else
-        gemm_tile<BN>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds, bkb(P, 3, tile.cb),
-                      bke(P, 3, tile.cb));
+        gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds,
+                                      bkb(P, 3, tile.cb), bke(P, 3, tile.cb));
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
         const int rho = e / BN, cc = e % BN;
@@ -666,11 +672,27 @@ static int bamp_lds_attr(const void* fn) {
 template <int KK>
 static int bamp_kb2_attrs() {
     int rc = bamp_lds_attr((const void*)bamp_kb2<128, KK>);
-    return rc ? rc : bamp_lds_attr((const void*)bamp_kb2<256, KK>);
+    return rc ? rc : bamp_lds_attr((const void*)bamp_kb2<256, KK>);   // the KC = 256 forms fit the default 64 KB
+}
+
+// The f32 tiles stage 256-wide A chunks (33 KB of LDS: four tiles per CU instead of two, the
+// chunk loaded one ahead); AMP_BAMP_KC=512 keeps 512 (A/B runs).  The chunking does not change
+// the MFMA order: the same bits.
+constexpr size_t BSKC_LDS = GemmCfg<128, 256>::LDS_BYTES;
+static bool bamp_short_chunks(const BampK& P) {
+    static const bool off = [] {
+        const char* e = getenv("AMP_BAMP_KC");
+        return e && atoi(e) == 512;
+    }();
+    return !P.h2 && !off;
 }
 
 template <int KK>
 static void launch_kb2_kk(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
+    if (P.bn == 128 && bamp_short_chunks(P)) {
+        hipLaunchKernelGGL((bamp_kb2<128, KK, 256>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BSKC_LDS, st, P, c64, t);
+        return;
+    }
     if (P.bn == 128)
         hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BLDS, st, P,
                            c64, t);
@@ -695,9 +717,9 @@ static int g_bamp_rc = 0;
 
 static int bamp_attrs() {
     std::call_once(g_bamp_once, [] {
-        g_bamp_rc = bamp_lds_attr((const void*)bamp_ka1);
-        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_ka2);
-        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_kb1);
+        g_bamp_rc = bamp_lds_attr((const void*)bamp_ka1<>);
+        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_ka2<>);
+        if (!g_bamp_rc) g_bamp_rc = bamp_lds_attr((const void*)bamp_kb1<>);
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<1>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<2>();
         if (!g_bamp_rc) g_bamp_rc = bamp_kb2_attrs<4>();
@@ -845,11 +867,15 @@ static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st
     const int gr = cdiv(P.B, GBM);
     // the host reads bvar(P, t + 1) as the device does: (t + 1) & 1 picks var1, else var0
     if (P.h2) bamp_split(P, ((t + 1) & 1) ? P.var1 : P.var0, P.N, P.N, false, t, st);
-    hipLaunchKernelGGL(bamp_ka1, dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    const bool skc = bamp_short_chunks(P);
+    if (skc) hipLaunchKernelGGL((bamp_ka1<256>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
+    else hipLaunchKernelGGL((bamp_ka1<>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2) bamp_split(P, P.xm, 2 * P.N, P.N, true, t, st);
-    hipLaunchKernelGGL(bamp_ka2, dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    if (skc) hipLaunchKernelGGL((bamp_ka2<256>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
+    else hipLaunchKernelGGL((bamp_ka2<>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2) bamp_split(P, P.invu, P.n, P.n, false, t, st);
-    hipLaunchKernelGGL(bamp_kb1, dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BLDS, st, P, t);
+    if (skc) hipLaunchKernelGGL((bamp_kb1<256>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
+    else hipLaunchKernelGGL((bamp_kb1<>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2) bamp_split(P, P.s, 2 * P.n, P.n, true, t, st);
     launch_kb2(P, c64, gr, t, st);
 }

@@ -19,7 +19,7 @@ namespace amp {
 // row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
 // (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
 template <int PWG, int KK, class PK>
-__device__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
+__device__ __forceinline__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
                                 int lrow0, int nrows, float* sT, void* lab_lds, int lab_cap, void* scr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int M = P.M, L = P.L, N = P.N;

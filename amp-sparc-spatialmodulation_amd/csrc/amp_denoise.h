@@ -30,6 +30,32 @@ namespace amp {
 
 #define AMP_LOG2E 1.44269504088896340736f
 
+// Diagnostic precision switches (default 0: the product arithmetic).  AMP_DEN_EXACT_EXP: every
+// softmax weight as float(exp(double(x) - double(m))) (correctly rounded); AMP_DEN_DIV: 1 / Z by
+// an IEEE division instead of v_rcp_f32.  tools/den_isolate.py measures their effect on the
+// early exit.
+#ifndef AMP_DEN_EXACT_EXP
+#define AMP_DEN_EXACT_EXP 0
+#endif
+#ifndef AMP_DEN_DIV
+#define AMP_DEN_DIV 0
+#endif
+// exp(x - m) for a logit x and its shift m (natural units)
+__device__ __forceinline__ float den_exp(float x, float m) {
+#if AMP_DEN_EXACT_EXP
+    return (float)exp((double)x - (double)m);
+#else
+    return __builtin_amdgcn_exp2f((x - m) * AMP_LOG2E);
+#endif
+}
+__device__ __forceinline__ float den_rcp(float z) {
+#if AMP_DEN_DIV
+    return 1.0f / z;
+#else
+    return __builtin_amdgcn_rcpf(z);
+#endif
+}
+
 // Which waves of the workgroup share a denoiser call: this wave's index among them and their
 // count (default: every wave of the workgroup).  The wave-specialized engine
 // (amp_vamp_persist_kernel.h, WS) hands half the sections to a subset of its waves.
@@ -106,7 +132,7 @@ __device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const
             float zm = 0.f, a = 0.f, b = 0.f;
 #pragma unroll
             for (int k = 0; k < KK; ++k) {
-                const float e = __builtin_amdgcn_exp2f((xk[u][k] - smax[u]) * AMP_LOG2E);
+                const float e = den_exp(xk[u][k], smax[u]);
                 xk[u][k] = e;
                 zm += e;
                 a = fmaf(cre[k], e, a);
@@ -118,7 +144,7 @@ __device__ __forceinline__ void denoise_sections_g(const P& pol, int nsec, const
         for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float iz = __builtin_amdgcn_rcpf(zt[u]);
+            const float iz = den_rcp(zt[u]);
             const float xr = sr[u] * iz, xi = si[u] * iz;
             float var = 0.f;
             if (kVar) {
@@ -234,8 +260,13 @@ __device__ __forceinline__ void denoise_step_gp(const P& pol, int base, int nsec
         f32x2 z2 = f32x2{0.f, 0.f}, a2 = f32x2{0.f, 0.f};
 #pragma unroll
         for (int h = 0; h < KH; ++h) {
+#if AMP_DEN_EXACT_EXP
+            const f32x2 e = f32x2{den_exp(xk[u][h].x, smax[u]), den_exp(xk[u][h].y, smax[u])};
+            (void)m2; (void)l2;
+#else
             const f32x2 d = (xk[u][h] - m2) * l2;
             const f32x2 e = f32x2{__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+#endif
             xk[u][h] = e;
             z2 += e;
             a2 = __builtin_elementwise_fma(R.sym[2 * h], f32x2{e.x, e.x}, a2);
@@ -247,7 +278,7 @@ __device__ __forceinline__ void denoise_step_gp(const P& pol, int base, int nsec
     for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const float iz = __builtin_amdgcn_rcpf(zt[u]);
+        const float iz = den_rcp(zt[u]);
         const f32x2 x2 = s2[u] * f32x2{iz, iz};
         float var = 0.f;
         if (kVar) {
@@ -355,11 +386,11 @@ __device__ __forceinline__ void denoise_step_grid(const P& pol, int base, int ns
     float SI[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        f[u] = __builtin_amdgcn_exp2f((lmx[u] - smax[u]) * AMP_LOG2E);
+        f[u] = den_exp(lmx[u], smax[u]);
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            er[u][i] = __builtin_amdgcn_exp2f((X[u][i] - mx[u]) * AMP_LOG2E);
-            ei[u][i] = __builtin_amdgcn_exp2f((Y[u][i] - my[u]) * AMP_LOG2E);
+            er[u][i] = den_exp(X[u][i], mx[u]);
+            ei[u][i] = den_exp(Y[u][i], my[u]);
         }
         if constexpr (FULLG) {
             float sr = 0.f, si = 0.f, a = 0.f, b = 0.f;
@@ -402,7 +433,7 @@ __device__ __forceinline__ void denoise_step_grid(const P& pol, int base, int ns
     for (int u = 0; u < U; ++u) group_sum_excl_c<G>(zt[u], ze[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const float iz = __builtin_amdgcn_rcpf(zt[u]);
+        const float iz = den_rcp(zt[u]);
         const float xr = ar[u] * iz, xi = ai[u] * iz;
         float var = 0.f;
         if (kVar) {
@@ -498,14 +529,23 @@ __device__ __forceinline__ void denoise_step_grid2(const P& pol, int base, int n
         sabs[u] = group_fmax_c<G>(fmaxf(lmx[u], -(nx + ny)));   // max |logit|
     }
     const f2v l2e = f2splat(AMP_LOG2E);
+#if AMP_DEN_EXACT_EXP
+    f2v f = {den_exp(lmx.x, smax.x), den_exp(lmx.y, smax.y)};
+#else
     f2v targ = (lmx - smax) * l2e;
     f2v f = {__builtin_amdgcn_exp2f(targ.x), __builtin_amdgcn_exp2f(targ.y)};
+#endif
     f2v er[R], ei[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
+#if AMP_DEN_EXACT_EXP
+        er[i] = f2v{den_exp(X[i].x, mx.x), den_exp(X[i].y, mx.y)};
+        ei[i] = f2v{den_exp(Y[i].x, my.x), den_exp(Y[i].y, my.y)};
+#else
         const f2v xa = (X[i] - mx) * l2e, ya = (Y[i] - my) * l2e;
         er[i] = f2v{__builtin_amdgcn_exp2f(xa.x), __builtin_amdgcn_exp2f(xa.y)};
         ei[i] = f2v{__builtin_amdgcn_exp2f(ya.x), __builtin_amdgcn_exp2f(ya.y)};
+#endif
     }
     f2v zt, ar, ai, SI = f2splat(0.f);
     f2v Sr[FULLG ? 1 : R];
@@ -547,7 +587,7 @@ __device__ __forceinline__ void denoise_step_grid2(const P& pol, int base, int n
     float ze[2] = {0.f, 0.f}, zt1[2] = {zt.x, zt.y};
 #pragma unroll
     for (int u = 0; u < 2; ++u) group_sum_excl_c<G>(zt1[u], ze[u]);
-    const f2v iz = {__builtin_amdgcn_rcpf(zt1[0]), __builtin_amdgcn_rcpf(zt1[1])};
+    const f2v iz = {den_rcp(zt1[0]), den_rcp(zt1[1])};
     const f2v xr = ar * iz, xi = ai * iz;
     f2v var = f2splat(0.f);
     if (kVar) {
@@ -655,22 +695,28 @@ __device__ __forceinline__ void denoise_sections_gp(const P& pol, int nsec, cons
     S.fold(pa);
 }
 
-// Runtime M (a power of two <= 64) -> the compile-time group size; PK selects the packed-math
-// forms (v_pk_*_f32).  PK = false keeps every float32 operation scalar (the product grid still
-// applies): the engines that place two waves on one SIMD use it, because there the packed
-// variance accumulation of denoise_step_gp was measured to lose one half of a v_pk_fma_f32 result
-// in lanes 48-63 now and then (results not reproducible run to run; the scalar
-// form was bit-identical in every run).
-template <bool kVar, int KK, int U, int G, bool PK, class P>
+// Which float32 forms run on the packed VALU (v_pk_*_f32):
+//   PK_NONE  every float32 operation scalar (the product grid still applies);
+//   PK_ALL   the packed per-point form (denoise_step_gp) and the packed product grid (grid2);
+//   PK_GRID  the packed product grid only; alphabets that are not a grid of the compile-time
+//            size (16PSK at KK = 16, QPSK {1, j, -1, -j}) run the scalar per-point form.
+// The engines that place two waves on one SIMD use PK_NONE or PK_GRID, because there the packed
+// per-point variance accumulation of denoise_step_gp was measured to lose one half of a
+// v_pk_fma_f32 result in lanes 48-63 now and then (results not reproducible run to
+// run; the scalar form was bit-identical in every run).  PK_ALL == true keeps the old bool callers.
+enum { PK_NONE = 0, PK_ALL = 1, PK_GRID = 2 };
+
+// Runtime M (a power of two <= 64) -> the compile-time group size.
+template <bool kVar, int KK, int U, int G, int PK, class P>
 __device__ __forceinline__ void denoise_sections_sel(const P& pol, int nsec, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
-    if constexpr (PK && KK % 2 == 0) {
+    if constexpr (PK == PK_ALL && KK % 2 == 0) {
         denoise_sections_gp<kVar, KK, U, G>(pol, nsec, c, pa, dw);
     } else {
-        if (denoise_sections_grid<kVar, KK, U, G, false>(pol, nsec, c, pa, dw)) return;
+        if (denoise_sections_grid<kVar, KK, U, G, PK == PK_GRID>(pol, nsec, c, pa, dw)) return;
         denoise_sections_g<kVar, KK, U, G>(pol, nsec, c, pa, dw);
     }
 }
-template <bool kVar, int KK, int U, bool PK = true, class P>
+template <bool kVar, int KK, int U, int PK = PK_ALL, class P>
 __device__ __forceinline__ void denoise_sections_u(const P& pol, int nsec, int M, const Const& c, PartAcc& pa, DenWaves dw = DenWaves::block()) {
     switch (M) {
     case 64: denoise_sections_sel<kVar, KK, U, 64, PK>(pol, nsec, c, pa, dw); break;
@@ -732,7 +778,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float cr = s_cre[k0 + j], ci = s_cim[k0 + j];
-                const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
+                const float e = den_exp(fmaf(ur, cr, ui * ci), smax);
                 zm += e;
                 a = fmaf(cr, e, a);
                 b = fmaf(ci, e, b);
@@ -740,7 +786,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
         }
         float zt = zm, ze = 0.f;
         group_sum_excl_c<G>(zt, ze);
-        const float iz = __builtin_amdgcn_rcpf(zt);
+        const float iz = den_rcp(zt);
         const float xr = a * iz, xi = b * iz;
         float var = 0.f;
         if (kVar) {
@@ -750,7 +796,7 @@ __device__ __forceinline__ void denoise_sections_wide(const P& pol, int nsec, co
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float cr = s_cre[k0 + j], ci = s_cim[k0 + j];
-                    const float e = __builtin_amdgcn_exp2f((fmaf(ur, cr, ui * ci) - smax) * AMP_LOG2E);
+                    const float e = den_exp(fmaf(ur, cr, ui * ci), smax);
                     const float dr = xr - cr, di = xi - ci;
                     vs = fmaf(fmaf(dr, dr, di * di), e, vs);
                 }

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
         if constexpr (KK > 16)
             denoise_sections_wide_m<false, KK>(pol, nrows * spr, M, P.c, pa);
         else
-            denoise_sections_u<false, KK, (KK >= 8 ? 2 : 4), (NWV == 4 || KK == 16)>(pol, nrows * spr, M, P.c, pa);
+            denoise_sections_u<false, KK, (KK >= 8 ? 2 : 4), (NWV == 4 ? PK_ALL : KK == 16 ? PK_GRID : PK_NONE)>(pol, nrows * spr, M, P.c, pa);
         __syncthreads();
         stamp(t, 5);
         unsigned nc = 0;

@@ -63,6 +63,11 @@ struct VampK {
     const void* Wx2;             // V  X3- / H2-packed (O = N, J = k)
     XState* xs;                  // trial-sharded exchange words (amp_vamp_run_sharded)
     float* dump;                 // diagnostic per-iteration state dump (amp_vamp_debug_dump), else null
+    // side-by-side epochs with one channel per epoch (amp_vamp_detect_count_epochs_ch): epoch e's
+    // split-precision operators at Wx1 / Wx2 + e * wch bytes and its singular values at s + e * sch
+    // (0, 0: one channel shared by every epoch)
+    long long wch;
+    int sch;
     Const c;
 };
 
@@ -91,7 +96,9 @@ static void vamp_geometry(const amp_dims* d, int k, VampK& P) {
     P.nblk2 = cdiv(d->B, GBM) * (P.ncp2 / P.bn2);
 }
 
-static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
+// chans: channel-dependent operator sets (Wq0 / Wx1 / Wx2) to hold — one per epoch for side-by-side
+// epochs with a channel each (amp_vamp_epochs_workspace_bytes carves `epochs` of them).
+static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base, int chans = 1) {
     VampK P;
     vamp_geometry(d, k, P);
     Carve cv(base);
@@ -108,11 +115,11 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base) {
     w.parts = cv.take<Partial>((size_t)max_iter * P.nblk2);
     w.iters = cv.take<VampIter>((size_t)max_iter + 1);
     const int nwg = cdiv(d->B, 16);
-    w.Wq0 = cv.take<float>((size_t)2 * k * 2 * d->n);
+    w.Wq0 = cv.take<float>((size_t)2 * k * 2 * d->n * chans);
     w.Wq1 = cv.take<float>((size_t)2 * k * 2 * d->N);
     w.Wq2 = cv.take<float>((size_t)2 * d->N * 2 * k);
-    w.Wx1 = cv.take<float>((size_t)3 * k * d->N);      // 6 bf16 per complex entry
-    w.Wx2 = cv.take<float>((size_t)3 * k * d->N);
+    w.Wx1 = cv.take<float>((size_t)3 * k * d->N * chans);      // 6 bf16 per complex entry
+    w.Wx2 = cv.take<float>((size_t)3 * k * d->N * chans);
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(PBAR_WORDS);                  // barrier words (zeroed per launch); the
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // granules carry generation tags
@@ -133,13 +140,13 @@ __device__ __forceinline__ float* var_buf(const VampK& P, int t) { return (t & 1
 struct S2Lane {
     float v[4];
 };
-__device__ inline S2Lane s2_lane(const VampK& P) {
+__device__ inline S2Lane s2_lane(const VampK& P, const float* s) {
     S2Lane a;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i = lane + 64 * j;
-        a.v[j] = i < P.k ? P.s[i] * P.s[i] : 0.f;
+        a.v[j] = i < P.k ? s[i] * s[i] : 0.f;
     }
     return a;
 }
@@ -266,6 +273,22 @@ __device__ __forceinline__ void den_debug(const PDenoisePolicy& p, int sec, int 
         p.dbg[row * 2 * p.N + sj * p.M + m] = ze;
         p.dbg[row * 2 * p.N + p.N + sj * p.M + m] = vs;
     }
+}
+
+// PDenoisePolicy over half of every row's sections (the staggered eight-wave engine, DESIGN.md
+// §3.1): local section s is section off + (s & (2^lsh - 1)) of row s >> lsh.
+struct PHalfPolicy {
+    PDenoisePolicy p;
+    int lsh, off;
+    __device__ __forceinline__ int gsec(int s) const { return ((s >> lsh) << p.lspr) + off + (s & ((1 << lsh) - 1)); }
+    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const { p.load(gsec(sec), m, rr, ri, it); }
+    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
+        p.store(gsec(sec), m, xr, xi, var, pa);
+    }
+    __device__ __forceinline__ void section(int sec, float smax, float sabs) const { p.section(gsec(sec), smax, sabs); }
+};
+__device__ __forceinline__ void den_debug(const PHalfPolicy& h, int sec, int m, float ze, float vs) {
+    den_debug(h.p, h.gsec(sec), m, ze, vs);
 }
 
 constexpr int PBM = 16;   // trials per workgroup

@@ -444,7 +444,8 @@ int vamp_gemm_select(const amp_dims* d, int k, int gemm) {
     return vamp_gemm_mode(gemm, fits);
 }
 
-static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64) {
+static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, VampK& P, Const64& c64,
+                      int chans = 1) {
     int rc = check_dims(d, c);
     if (rc) return rc;
     AMP_REQUIRE(a && a->U && a->s && a->Vh && a->y && a->r && a->xmmse && a->var && a->status && a->ws,
@@ -452,7 +453,7 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     AMP_REQUIRE(a->k > 0 && a->k <= d->N && a->k <= d->n && a->k % 2 == 0, "amp_vamp: k = %d must be min(n, N), even",
                 a->k);
     AMP_REQUIRE(a->max_iter > 0, "amp_vamp: max_iter must be positive");
-    const VampWs w = vamp_carve(d, a->k, a->max_iter, a->ws);
+    const VampWs w = vamp_carve(d, a->k, a->max_iter, a->ws, chans);
     AMP_REQUIRE(a->ws_bytes >= w.bytes, "amp_vamp: workspace %zu < %zu bytes", a->ws_bytes, w.bytes);
     vamp_geometry(d, a->k, P);
     P.max_iter = a->max_iter;
@@ -486,6 +487,8 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.x3 = vamp_gemm_mode(a->gemm, x3_fits);
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.dump = debug_dump_ptr();
+    P.wch = 0;
+    P.sch = 0;
     return AMP_OK;
 }
 
@@ -582,9 +585,41 @@ static bool ytil_x3_env() {
 bool ytil_x3_fits(int n, int k);
 int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st);
 
-static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st) {
+// Side-by-side epochs with a channel each (P.wch != 0): every epoch's split-precision operators
+// (Vh, V, s Uh) from its own U / s / Vh (a->U + e * ch.U, ...), then y~ per epoch.
+struct EpochChannels {
+    long long U = 0, s = 0, Vh = 0;   // elements between epochs' U (c64), s (f32), Vh (c64)
+};
+static int vamp_persist_prepare_ch(VampK& P, const amp_vamp_args* a, const EpochChannels& ch, hipStream_t st) {
+    const int pk = P.x3 == 3 ? WPACKI8 : WPACKX3;
+    const long long q0 = (long long)16 * P.k * P.n;   // bytes between epochs' s Uh (the carve's f32 stride)
+    for (int e = 0; e < P.E; ++e) {
+        const float2* U = (const float2*)a->U + e * ch.U;
+        const float2* Vh = (const float2*)a->Vh + e * ch.Vh;
+        const float* sv = (const float*)a->s + e * ch.s;
+        char* wx1 = (char*)P.Wx1 + e * P.wch;
+        char* wx2 = (char*)P.Wx2 + e * P.wch;
+        char* wq0 = (char*)P.Wq0 + e * q0;
+        CWeightJob j[3];
+        j[0] = CWeightJob{Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)wx1, P.N, P.k, pk};
+        j[1] = CWeightJob{Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)wx2, P.k, P.N, pk};
+        j[2] = CWeightJob{U, 1, P.k, 1, sv, P.k, P.n, (float*)wq0, P.n, P.k, WPACKX3};
+        int rc = build_cweights(j, 3, e == 0 ? P.pbar : nullptr, PBAR_WORDS, st);
+        if (rc) return rc;
+        rc = ytil_x3_launch((const float*)a->y + (size_t)e * P.B * 2 * P.n, P.n, P.B, wq0,
+                            P.ytil + (size_t)e * P.B * 2 * P.k, P.k, st);
+        if (rc) return rc;
+    }
+    return AMP_OK;
+}
+
+static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st, const EpochChannels* ch = nullptr) {
     static std::atomic<unsigned> gen{0};
     P.gen = ++gen;
+    if (ch && P.wch) {
+        P.ytil_in_kernel = 0;
+        return vamp_persist_prepare_ch(P, a, *ch, st);
+    }
     const int env = ytil_in_kernel_env();
     if (P.x3 == 2)
         P.ytil_in_kernel = (env != 0 && vamp_persist_ytil_h2(P)) ? 1 : 0;
@@ -687,7 +722,8 @@ int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
 // Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
 // boundary: trace[(wg * max_iter + t) * 10 + phase], phases = start, r~ built, GEMM1, w stored,
 // GEMM2 + r, partial published, barrier passed, scalars ready, (unused), denoiser done; then per
-// workgroup [nwg * max_iter * 10 + 2 * wg] = s_memtime / s_memrealtime at kernel start.
+// workgroup [nwg * max_iter * 10 + 2 * wg] = s_memtime / s_memrealtime at kernel start and
+// [nwg * max_iter * 10 + 2 * nwg + 2 * wg] the same pair at its end (trace: 4 nwg more words).
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
                            void* stream) {
     VampK P;
@@ -816,8 +852,9 @@ int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
 size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs) {
     if (!d || k <= 0 || max_iter <= 0 || epochs < 1 || (long)d->B * epochs > (1L << 30)) return 0;
     amp_dims de = *d;
-    de.B = d->B * epochs;   // the carve holds every epoch's rows and one granule pair per workgroup
-    return vamp_carve(&de, k, max_iter, nullptr).bytes;
+    de.B = d->B * epochs;   // the carve holds every epoch's rows, one granule pair per workgroup and
+                            // one operator set per epoch (amp_vamp_detect_count_epochs_ch)
+    return vamp_carve(&de, k, max_iter, nullptr, epochs).bytes;
 }
 
 int amp_vamp_debug_dump(void* buf) {
@@ -838,8 +875,9 @@ int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32
     return AMP_OK;
 }
 
-int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
-                                 const amp_vamp_decide_args* dec, int32_t epochs, void* stream) {
+static int detect_count_epochs_impl(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                    const amp_vamp_decide_args* dec, int32_t epochs, const EpochChannels& ch,
+                                    void* stream) {
     AMP_REQUIRE(d && epochs >= 1 && (long)d->B * epochs <= (1L << 30), "amp_vamp_detect_count_epochs: epochs = %d",
                 epochs);
     const int ncu = device_cu_count();
@@ -851,8 +889,18 @@ int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, 
     de.B = d->B * epochs;
     VampK P;
     Const64 c64;
-    int rc = vamp_setup(&de, c, a, P, c64);   // carve and buffers over all epochs' rows
+    int rc = vamp_setup(&de, c, a, P, c64, epochs);   // carve and buffers over all epochs' rows and channels
     if (rc) return rc;
+    const bool per = ch.U || ch.s || ch.Vh;
+    AMP_REQUIRE(!per || (ch.U > 0 && ch.s > 0 && ch.Vh > 0),
+                "amp_vamp_detect_count_epochs_ch: strides must be all zero (one channel) or all positive");
+    AMP_REQUIRE(!per || ((P.x3 == 1 || P.x3 == 3) && ytil_x3_fits(P.n, P.k)),
+                "amp_vamp_detect_count_epochs_ch: a channel per epoch needs the bf16x3 or int8x4 engine and n == 2 k "
+                "(gemm %d, n %d, k %d)", a->gemm, P.n, P.k);
+    if (per) {
+        P.wch = (long long)12 * P.k * P.N;    // the carve's stride of the X3 / I8 operators (3 k N floats)
+        P.sch = (int)ch.s;
+    }
     P.B = d->B;                               // the batch of one epoch (mean var, vamp.py:85)
     P.Bmean = d->B;
     P.E = epochs;
@@ -865,7 +913,7 @@ int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, 
     AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_vamp_detect_count_epochs: ibits_trunc");
     AMP_REQUIRE(d->Lin * d->Na * d->M == d->N, "amp_vamp_detect_count_epochs: inconsistent dims");
     hipStream_t st = (hipStream_t)stream;
-    rc = vamp_persist_prepare(P, a, st);
+    rc = vamp_persist_prepare(P, a, st, &ch);
     if (rc) return rc;
     P.dec_on = 1;
     P.ibits = dec->ibits_trunc;
@@ -874,6 +922,20 @@ int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, 
     P.idx = (const long long*)dec->idx;
     P.counts = (amp_counts*)dec->counts;
     return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
+}
+
+int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                 const amp_vamp_decide_args* dec, int32_t epochs, void* stream) {
+    return detect_count_epochs_impl(d, c, a, dec, epochs, EpochChannels{}, stream);
+}
+
+int amp_vamp_detect_count_epochs_ch(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                    const amp_vamp_decide_args* dec, int32_t epochs, int64_t U_stride,
+                                    int64_t s_stride, int64_t Vh_stride, void* stream) {
+    AMP_REQUIRE(U_stride >= 0 && s_stride >= 0 && Vh_stride >= 0, "amp_vamp_detect_count_epochs_ch: negative stride");
+    EpochChannels ch;
+    ch.U = U_stride; ch.s = s_stride; ch.Vh = Vh_stride;
+    return detect_count_epochs_impl(d, c, a, dec, epochs, ch, stream);
 }
 
 // Measurement helper (bench.py): one full forward with hipEvents between the launches on

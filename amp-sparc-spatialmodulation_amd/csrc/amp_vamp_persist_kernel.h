@@ -6,6 +6,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "amp_decide_fused.h"
 #include "amp_persist.h"
 #include "amp_vamp.h"
@@ -24,6 +26,12 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #endif
 #ifndef AMP_X3_W8_PKGRID
 #define AMP_X3_W8_PKGRID 1              // the eight-wave bf16x3 form keeps 16-QAM's packed grid denoiser
+#endif
+#ifndef AMP_X3_STAGGER
+#define AMP_X3_STAGGER 0                // 1: staggered GEMM2 / denoiser (A/B: slower)
+#endif
+#ifndef AMP_X3_STG_RING
+#define AMP_X3_STG_RING 1               // weight groups in flight of the staggered second-half GEMM2
 #endif
 #ifndef AMP_X3_DU
 #define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
@@ -78,10 +86,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     static_assert(!X3 || ((NWV == 4 || (NWV == 8 && !H2 && OCC == 1)) && NT % 2 == 0),
                   "X3: four waves (eight for the bf16x3 two-waves-per-SIMD form), whole complex tiles");
     static_assert(!(H2 && I8) && (!I8 || X3), "I8: a split-precision form of its own");
-    // packed denoiser at one wave per SIMD; with two (OCC = 2, or the eight-wave bf16x3 form) only
-    // the packed product-grid form for 16-point alphabets (AMP_X3_W8_PKGRID; the per-point packed
-    // form lost results there)
-    constexpr bool PKDEN = (OCC * NWV / 4 == 1) || AMP_OCC2_PK || (NWV == 8 && KK == 16 && AMP_X3_W8_PKGRID);
+    // packed denoiser at one wave per SIMD; with two (OCC = 2, or the eight-wave bf16x3 form) at most
+    // the packed product-grid form, for 16-QAM (AMP_X3_W8_PKGRID; 16PSK, not a grid, runs the scalar
+    // per-point form: the packed per-point form lost results there)
+    constexpr int PKDEN = ((OCC * NWV / 4 == 1) || AMP_OCC2_PK) ? PK_ALL
+                          : (NWV == 8 && KK == 16 && AMP_X3_W8_PKGRID) ? PK_GRID : PK_NONE;
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
     constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
@@ -89,6 +98,13 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     // eight waves: no A-fragment prefetch in gemm_x3 (the partner wave covers the LDS reads;
     // 24 registers fewer) when AMP_X3_W8_PIN (A/B builds)
     constexpr bool X3PIN = NWV == 8 && AMP_X3_W8_PIN;
+    // Staggered GEMM2 / denoiser (eight-wave bf16x3 form, 2 NWV complex column tiles: N = 256).  Waves
+    // w and w + 4 share a SIMD.  (1) every wave forms r for ONE tile of the first half of the columns;
+    // (2) waves 0-3 denoise the first half's sections (VALU) while waves 4-7 form r for the second
+    // half (two tiles each: L2 stream + MFMA); (3) all eight waves denoise the second half.  One SIMD
+    // then runs one wave's denoiser beside its partner's GEMM instead of the two waves reaching the
+    // same phase together.
+    constexpr bool STG = X3 && !H2 && !I8 && NWV == 8 && NC == 2 && KK <= 16 && AMP_X3_STAGGER;
     const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
@@ -111,6 +127,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     const int row0 = ep * P.B + lrow0, nrows = min(PBM, P.B - lrow0);
     unsigned* ebar = P.pbar + (P.E > 1 ? PBAR_EPOCH + ep : 0);   // this epoch's arrival counter
     const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
+    // this epoch's channel (one per epoch, or one shared: wch = sch = 0)
+    const float* const sv_ep = P.s + (size_t)ep * P.sch;
+    const void* const Wx1 = (const char*)P.Wx1 + ep * P.wch;
+    const void* const Wx2 = (const char*)P.Wx2 + ep * P.wch;
     const int ldr = Y.ldr, lda = Y.lda;
     const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
     const int cc0 = wave * NC;                 // X3: this wave's complex 16-column tiles
@@ -125,7 +145,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int col = X3 ? 2 * (16 * (cc0 + (t < NC ? t : 0)) + (lane & 15)) : 16 * (ct0 + t) + (lane & 15);
-        const float sv = P.s[col >> 1];
+        const float sv = sv_ep[col >> 1];
         s2c[t] = sv * sv;                                   // vamp.py:17
     }
     if (H2 && P.ytil_in_kernel) {
@@ -227,7 +247,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             }
         }
     }
-    const S2Lane s2l = s2_lane(P);            // s^2 in registers for the per-iteration LMMSE sum
+    const S2Lane s2l = s2_lane(P, sv_ep);     // s^2 in registers for the per-iteration LMMSE sum
     VampIter cur = vamp_first_iter(P, scr, &s2l);   // vamp.py:26, 66-82 at t = 0
     // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
     {
@@ -441,11 +461,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             float rowf[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) rowf[r] = i8_row_factor(s_hexp[4 * (lane >> 4) + r]);
-            gemm_i8<NC, G3 / 2>(sB, ldb, P.Wx1, N, cc0, rowf, cr, ci);   // 64-deep groups: N / 64
+            gemm_i8<NC, G3 / 2>(sB, ldb, Wx1, N, cc0, rowf, cr, ci);   // 64-deep groups: N / 64
         } else if constexpr (H2)
-            gemm_h2<NC, G3>(sP, ldx, P.Wx1, cc0, cr, ci);
+            gemm_h2<NC, G3>(sP, ldx, Wx1, cc0, cr, ci);
         else if constexpr (X3)
-            gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, P.Wx1, cc0, cr, ci);
+            gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx1, cc0, cr, ci);
         else
             gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
         float hsc[4];                                 // H2: 2^-(e_row + H2_EX) of this lane's rows
@@ -572,30 +592,21 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         __syncthreads();
         stamp(t, 3);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
-        if constexpr (X3) {
-            if constexpr (I8) {
-                gemm_i8<NC, G3 / 2>(sB, ldb, P.Wx2, N, cc0, hsc, cr, ci);   // hsc: the w rows' factors
-            } else if constexpr (H2) {
-                gemm_h2<NC, G3>(sP, ldx, P.Wx2, cc0, cr, ci);
-#pragma unroll
-                for (int t2 = 0; t2 < NC; ++t2)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
-            } else {
-                gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, P.Wx2, cc0, cr, ci);
-            }
-            // the lane index pinned here: the 4 NC LDS addresses below are then formed in this
-            // epilogue instead of being hoisted out of the iteration loop (and kept live across it)
+        // r = (x~ - alpha r~) / (1 - alpha) for the complex column tiles ccs ... of this wave.  The
+        // lane index pinned here: the 4 NC LDS addresses below are then formed in this epilogue
+        // instead of being hoisted out of the iteration loop (and kept live across it)
+        auto r_epi = [&](int ccs, auto& er, auto& ei) __attribute__((always_inline)) {
+            constexpr int NCX = std::extent<std::remove_reference_t<decltype(er)>>::value;
             const int lnr = (I8 || NWV == 8) ? pl_opaque(lane) : lane;
 #pragma unroll
-            for (int t2 = 0; t2 < NC; ++t2) {
-                const int o = 16 * (cc0 + t2) + (lnr & 15);
+            for (int t2 = 0; t2 < NCX; ++t2) {
+                const int o = 16 * (ccs + t2) + (lnr & 15);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int b = (4 * (lnr >> 4) + r) * ldr + 2 * o;
                     const float rtr = (sX[b] - cur.dxdr_prev * sR[b]) * cur.ns_prev;
                     const float rti = (sX[b + 1] - cur.dxdr_prev * sR[b + 1]) * cur.ns_prev;
-                    const float xtr = cr[t2][r] + rtr, xti = ci[t2][r] + rti;
+                    const float xtr = er[t2][r] + rtr, xti = ei[t2][r] + rti;
                     sR[b] = (xtr - cur.alpha * rtr) * cur.inv1ma;
                     sR[b + 1] = (xti - cur.alpha * rti) * cur.inv1ma;
                     if (P.dump) {
@@ -604,6 +615,25 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                         dp[(4 * (lane >> 4) + r) * twoN + 2 * o + 1] = sR[b + 1];
                     }
                 }
+            }
+        };
+        if constexpr (X3) {
+            if constexpr (I8) {
+                gemm_i8<NC, G3 / 2>(sB, ldb, Wx2, N, cc0, hsc, cr, ci);   // hsc: the w rows' factors
+            } else if constexpr (H2) {
+                gemm_h2<NC, G3>(sP, ldx, Wx2, cc0, cr, ci);
+#pragma unroll
+                for (int t2 = 0; t2 < NC; ++t2)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
+            }
+            if constexpr (STG) {
+                f32x4 hr[1], hi[1];
+                gemm_x3<1, G3, X3R, X3PIN>(sP, ldx, Wx2, wave, hr, hi);   // (1) first half: tile `wave`
+                r_epi(wave, hr, hi);
+            } else {
+                if constexpr (!I8 && !H2) gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx2, cc0, cr, ci);
+                r_epi(cc0, cr, ci);
             }
         } else {
         gemm16<NT, NT * NWV>(sA, lda, P.Wq2, ct0, acc);
@@ -620,15 +650,34 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         }
         }
         __syncthreads();
-        stamp(t, 4);
         // 4. denoiser (vamp.py:84)
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         if (P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
         PartAcc pa;
-        if constexpr (KK > 16)
-            denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
-        else
-            denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
+        if constexpr (STG) {
+            // sections per row half: spr / 2 (M divides N / 2 for every power-of-two M <= 64 at N = 256)
+            const int lsh = 31 - __builtin_clz(spr) - 1;
+            const int wvu = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform branch (not exec-masked)
+            if (wvu < 4) {    // (2) the first half's sections on waves 0-3 ...
+                PHalfPolicy hp{pol, lsh, 0};
+                denoise_sections_u<true, KK, DU, PKDEN>(hp, nrows * (spr >> 1), M, P.c, pa, DenWaves{wvu, 4});
+            } else {          // ... beside the second half's GEMM2 on waves 4-7 (tiles NWV + 2 (wave - 4) ...)
+                // one GEMM wave per SIMD here: two weight groups in flight (the ring of both waves
+                // of the SIMD in the unstaggered form)
+                gemm_x3<NC, G3, AMP_X3_STG_RING, AMP_X3_STG_RING == 2>(sP, ldx, Wx2, NWV + 2 * (wvu - 4), cr, ci);
+                r_epi(NWV + 2 * (wvu - 4), cr, ci);
+            }
+            __syncthreads();
+            stamp(t, 4);
+            PHalfPolicy hp{pol, lsh, spr >> 1};   // (3) the second half's sections on all eight waves
+            denoise_sections_u<true, KK, DU, PKDEN>(hp, nrows * (spr >> 1), M, P.c, pa);
+        } else {
+            stamp(t, 4);
+            if constexpr (KK > 16)
+                denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
+            else
+                denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
+        }
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
@@ -651,6 +700,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         cur = nx;
     }
     __syncthreads();
+    if (trc && tid == 0) {   // end stamps: per-workgroup clock rate against the global 100 MHz clock
+        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * nwg + 2 * wg] = __builtin_amdgcn_s_memtime();
+        trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * nwg + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+    }
     // outputs: r (decision input, vamp.py:187), xmmse, var of the last executed iteration
     const float* vlast = lds + ((last_t & 1) ? Y.offV1 : Y.offV0);
     for (int e = tid; e < nrows * twoN; e += PWG) {

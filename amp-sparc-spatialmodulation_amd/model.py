@@ -93,8 +93,9 @@ class Model(nn.Module):
         (parity mode).  rng='device': channel, messages and noise drawn on the GPU and the SVD
         on the GPU through the Gram matrix's eigendecomposition (svd_gram; throughput mode: same
         distributions, different streams).
-        group_epochs: VAMP detects the epochs of one `res` block (one channel) side by side in
-        one persistent launch (VAMP.forward_epochs; same results, fills the GPU at small B).
+        group_epochs: VAMP detects up to max_epochs of its epochs side by side in one persistent
+        launch (VAMP.forward_epochs: one channel per epoch, or one per `res` block; same results,
+        fills the GPU at small B).
         shard (with torch.distributed): 'epochs' (default) gives each rank whole epochs with its
         own random stream and merges the metrics once per SNR point; 'trials' (SURVEY §8(e)
         exact-compat, VAMP / BAMP / SCAMP) gives every rank the SAME epochs (one seed) and splits each batch's
@@ -159,19 +160,27 @@ class Model(nn.Module):
             return self.amp(self._A, y, SNR, x, sym, idx)
         return self.amp(self._W, self._A, y, SNR, x, sym, idx)
 
-    def _block(self, SNR: float, n: int) -> list:
-        """n epochs of one `res` block (one channel, drawn first) with VAMP's side-by-side
-        launch (VAMP.forward_epochs): every epoch's inputs are drawn in the reference's call
-        order (channel, then message + noise per epoch), then the epochs are detected in chunks
-        that fit one persistent grid.  Results equal n sequential _epoch calls."""
-        inputs = [self._inputs(SNR, i == 0) for i in range(n)]
-        U, s, Vh = self._svd
+    def _group(self, SNR: float, ids: list, res: int) -> list:
+        """The epochs `ids` (this rank's, in order) detected side by side with VAMP's persistent
+        launch (VAMP.forward_epochs): every epoch's inputs are drawn in the reference's call order
+        (the channel first when i % res == 0, then message + noise), then the epochs are
+        detected in chunks that fit one persistent grid — with one channel per epoch where the
+        chunk spans several channels (the reference's default res = 1 redraws it every epoch).
+        Results equal the sequential _epoch calls."""
         cap = max(1, self.group_cap)
         out = []
-        for c0 in range(0, n, cap):
-            ch = inputs[c0:c0 + cap]
-            out += self.amp.forward_epochs(U, s, Vh, [v[3] for v in ch], SNR, [v[0] for v in ch],
-                                           [v[1] for v in ch], [v[2] for v in ch])
+        for c0 in range(0, len(ids), cap):
+            chunk = []
+            for i in ids[c0:c0 + cap]:
+                x, sym, idx, y = self._inputs(SNR, i % res == 0)
+                chunk.append((x, sym, idx, y, self._svd))
+            chans = [v[4] for v in chunk]
+            if all(c is chans[0] for c in chans):
+                U, s, Vh = chans[0]
+            else:
+                U, s, Vh = [c[0] for c in chans], [c[1] for c in chans], [c[2] for c in chans]
+            out += self.amp.forward_epochs(U, s, Vh, [v[3] for v in chunk], SNR, [v[0] for v in chunk],
+                                           [v[1] for v in chunk], [v[2] for v in chunk])
         return out
 
     def _inputs(self, SNR: float, new_channel: bool):
@@ -230,16 +239,15 @@ class Model(nn.Module):
             if self.rank == 0:
                 print(f'EbN0dB={EbN0dB}')
             SNR = 10 ** (SNRdB / 10)
-            for i in range(epochs):
-                if (i // res) % self._epoch_world != self.rank % self._epoch_world:   # blocks of `res` share a channel
-                    continue
-                if self.group_cap > 1 and res > 1:
-                    if i % res == 0:                          # the whole block at once
-                        for loss in self._block(SNR, min(res, epochs - i)):
-                            self.loss.accumulate(loss)
-                    continue
-                loss = self._epoch(SNR, i % res == 0)
-                self.loss.accumulate(loss)
+            # blocks of `res` epochs share a channel and go to one rank
+            mine = [i for i in range(epochs) if (i // res) % self._epoch_world == self.rank % self._epoch_world]
+            if self.group_cap > 1:
+                for loss in self._group(SNR, mine, res):      # side by side, chunks of group_cap epochs
+                    self.loss.accumulate(loss)
+            else:
+                for i in mine:
+                    loss = self._epoch(SNR, i % res == 0)
+                    self.loss.accumulate(loss)
             if 'fer' not in self.loss.loss:                   # a rank without epochs at this point
                 for k in self.loss.keys:
                     self.loss.loss[k] = np.float64(0.0)

@@ -9,6 +9,7 @@ the host reads back one 128-byte record per forward.
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 import os
 
 import numpy as np
@@ -209,7 +210,8 @@ class LazyResult:
             L.record(L.rates_from_counts(counts), int(status.T))
         L._pending = finish
 
-    grid_rescues = 0
+    grid_rescues = 0         # rescues of this detector
+    rescues_total = 0        # every rescue in this process (LazyResult.rescues_total; tests/conftest.py)
     # Test-only hook (tests/test_gpu_rescue.py): a callable that may rewrite a resolved persistent
     # status record (e.g. report the grid as lost) before it is checked; None in production.
     status_hook = None
@@ -221,6 +223,9 @@ class LazyResult:
             return status, counts
         if rescue is not None:
             self.grid_rescues += 1
+            LazyResult.rescues_total += 1
+            warnings.warn(f'{what}: persistent grid lost (a grid exchange timed out); the forward is re-run '
+                          'on the launch engine', RuntimeWarning, stacklevel=2)
             status, counts = rescue()
             if status.nan_state >= 0:
                 return status, counts
@@ -327,11 +332,13 @@ class VAMP(LazyResult, nn.Module):
         return 1 <= epochs <= self.max_epochs(k)
 
     def forward_epochs(self, U, s, Vh, ys, SNR: float, xs, symbols, indices) -> list:
-        """E epochs that share ONE channel (U, s, Vh) — the epochs of one `res` block of
-        Model.simulate (vamp_model.py:55-61 redraws the channel only when i % res == 0) —
-        detected side by side in one persistent launch (amp_vamp_detect_count_epochs).  Every
-        epoch keeps its own batch-global scalars and early exit (vamp.py:85, 112, 185), so the
-        returned Loss objects (one per epoch, in order) equal E sequential forward() calls.
+        """E epochs detected side by side in one persistent launch (amp_vamp_detect_count_epochs_ch).
+        (U, s, Vh) is either ONE channel shared by every epoch — the epochs of one `res` block of
+        Model.simulate (vamp_model.py:55-61 redraws the channel only when i % res == 0) — or one
+        channel per epoch (sequences of E tensors, or stacked [E, ...] tensors: the reference's
+        default res = 1 redraws it every epoch).  Every epoch keeps its own batch-global scalars
+        and early exit (vamp.py:85, 112, 185), so the returned Loss objects (one per epoch, in
+        order) equal E sequential forward() calls.
         ys / xs: sequences of the epochs' y [B, n, 1] and x [B, N, 1], or stacked [E, B, ...]
         tensors (used without a copy); symbols / indices: sequences of their label arrays or
         stacked label tensors.  The Losses resolve lazily (no host stall inside the call)."""
@@ -344,14 +351,36 @@ class VAMP(LazyResult, nn.Module):
         with torch.cuda.device(dev):
             return self._forward_epochs(U, s, Vh, ys, SNR, xs, symbols, indices, E, dev)
 
+    @staticmethod
+    def _epoch_channels(U, s, Vh, E):
+        """(U [n, k], s [k], Vh [k, N]) of one shared channel, or per-epoch channels stacked into
+        contiguous [E, n, k] / [E, k] / [E, k, N]; returns (Uc, sc, Vhc, per_epoch)."""
+        seq = lambda v: isinstance(v, (list, tuple))   # noqa: E731
+        per = seq(U) or (isinstance(U, torch.Tensor) and U.dim() == 3 and U.shape[0] == E and E > 1)
+        if not per:
+            n, k = U.shape[-2], U.shape[-1]
+            N = Vh.shape[-1]
+            return (_c64(U, (n, k)), s.reshape(k).to(torch.float32).resolve_neg().contiguous(), _c64(Vh, (k, N)),
+                    False)
+        Us = list(U) if seq(U) else [U[e] for e in range(E)]
+        ss = list(s) if seq(s) else [s[e] for e in range(E)]
+        Vhs = list(Vh) if seq(Vh) else [Vh[e] for e in range(E)]
+        if not (len(Us) == len(ss) == len(Vhs) == E):
+            raise ValueError(f'forward_epochs: {E} epochs need {E} channels (U, s, Vh), got '
+                             f'{len(Us)}, {len(ss)}, {len(Vhs)}')
+        n, k = Us[0].shape[-2], Us[0].shape[-1]
+        N = Vhs[0].shape[-1]
+        Uc = torch.stack([_c64(u, (n, k)) for u in Us]).contiguous()
+        sc = torch.stack([v.reshape(k).to(torch.float32).resolve_neg() for v in ss]).contiguous()
+        Vhc = torch.stack([_c64(v, (k, N)) for v in Vhs]).contiguous()
+        return Uc, sc, Vhc, True
+
     def _forward_epochs(self, U, s, Vh, ys, SNR, xs, symbols, indices, E, dev):
         from loss import _as_device_labels, _flat_c64
         cfg = self.config
         B = cfg.B
-        n, k = U.shape[0], U.shape[1]
-        N = Vh.shape[1]
-        Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
-        sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
+        Uc, sc, Vhc, per = self._epoch_channels(U, s, Vh, E)
+        n, k, N = Uc.shape[-2], Uc.shape[-1], Vhc.shape[-1]
         # a stacked [E, B, ...] tensor is used as it lies (no copy); a sequence is concatenated
         stack = lambda v, f: (f(v, E) if isinstance(v, torch.Tensor) else torch.cat([f(u, 1) for u in v]))  # noqa: E731
         y = stack(ys, lambda v, e: _c64(v, (e * B, n))).contiguous()
@@ -383,8 +412,13 @@ class VAMP(LazyResult, nn.Module):
         dec.x, dec.sym, dec.idx = nat.dptr(x, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices')
         dec.ibits_trunc = self.L._ibits
         dec.counts = nat.dptr(res) + E * st_sz
-        nat.check(lib.amp_vamp_detect_count_epochs(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), E,
-                                                   nat.stream_ptr(dev)), 'amp_vamp_detect_count_epochs')
+        if per:
+            strides = (n * k, k, k * N)     # elements between epochs' channels
+            nat.check(lib.amp_vamp_detect_count_epochs_ch(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), E,
+                                                          *strides, nat.stream_ptr(dev)), 'amp_vamp_detect_count_epochs_ch')
+        else:
+            nat.check(lib.amp_vamp_detect_count_epochs(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), E,
+                                                       nat.stream_ptr(dev)), 'amp_vamp_detect_count_epochs')
         # the records come back asynchronously: each Loss resolves on first access, and the
         # previous call's Losses are resolved here, after this call's launches are queued
         host[:res.numel()].copy_(res, non_blocking=True)
@@ -399,8 +433,9 @@ class VAMP(LazyResult, nn.Module):
             raw = host.numpy()
             status = nat.AmpStatus.from_buffer_copy(raw[e * st_sz:(e + 1) * st_sz].tobytes())
             counts = nat.AmpCounts.from_buffer_copy(raw[E * st_sz + e * ct_sz:E * st_sz + (e + 1) * ct_sz].tobytes())
+            ch = (Uc[e], sc[e], Vhc[e]) if per else (Uc, sc, Vhc)
             status, counts = self._check_grid(
-                status, counts, lambda: self._rescue_forward(Uc, sc, Vhc, y[e * B:(e + 1) * B], SNR,
+                status, counts, lambda: self._rescue_forward(ch[0], ch[1], ch[2], y[e * B:(e + 1) * B], SNR,
                                                              x[e * B:(e + 1) * B], sym[e * B * cfg.L:(e + 1) * B * cfg.L],
                                                              idx[e * B * cfg.L:(e + 1) * B * cfg.L]),
                 'amp_vamp_detect_count_epochs')

@@ -340,6 +340,7 @@ def main():
                    'trial_iterations_per_s': gb * T / (el / args.steps),
                    'engine': 'persistent' if persistent else 'launches', 'kernel_ms': kms,
                    'arithmetic': arith,
+                   'grid_rescues': int(getattr(det, 'grid_rescues', 0)),
                    'prewarm': {'ms': args.prewarm_ms, 'steps': npre,
                                'why': 'untimed steps before --warmup: the clocks ramp over the first ~25 ms'}},
         'roofline': {'bound': 'mfma', 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',

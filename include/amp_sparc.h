@@ -145,7 +145,7 @@ int amp_vamp_select_engine(const amp_dims* d, int32_t k, int32_t engine);
  * AMP_GEMM_I8 or AMP_GEMM_F32 (AMP_E_ARG when `gemm` is X3 / H2 / I8 and the shape does not fit). */
 int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* Diagnostic: a persistent-engine forward that stamps s_memtime per workgroup, iteration and
- * phase into trace (device, nwg * max_iter * 10 + 2 * nwg uint64; layout in amp_vamp.hip). */
+ * phase into trace (device, nwg * max_iter * 10 + 4 * nwg uint64; layout in amp_vamp.hip). */
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
                            void* stream);
 size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter);
@@ -222,6 +222,15 @@ int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
 int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                  const amp_vamp_decide_args* dec, int32_t epochs, void* stream);
+/* The same with ONE CHANNEL PER EPOCH — Model.simulate at the reference's default res = 1
+ * (vamp_model.py:45, 56-58: a new channel and its SVD every epoch): epoch e reads U at
+ * a->U + e * U_stride, s at a->s + e * s_stride and Vh at a->Vh + e * Vh_stride (elements: complex64
+ * for U / Vh, float for s; all zero = one shared channel, as amp_vamp_detect_count_epochs).  Needs the
+ * bf16x3 (AUTO) or int8x4 engine; workspace: amp_vamp_epochs_workspace_bytes (it always holds one
+ * operator set per epoch).  Replaces `epochs` calls of VAMP.forward with their own channels. */
+int amp_vamp_detect_count_epochs_ch(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                    const amp_vamp_decide_args* dec, int32_t epochs, int64_t U_stride,
+                                    int64_t s_stride, int64_t Vh_stride, void* stream);
 /* Measurement helper (not graph-safe: synchronises): one forward with hipEvents between the
  * launches, in milliseconds.  LAUNCHES engine: ms_out[4] = mean GEMM1 / GEMM2+denoiser /
  * reduction kernel time per executed iteration and the whole forward.  PERSISTENT engine

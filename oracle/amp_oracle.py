@@ -234,7 +234,8 @@ def block_denoise_f32(r: np.ndarray, tau, cfg: OracleConfig):
 # ----------------------------------------------------------------------------
 # detectors
 # ----------------------------------------------------------------------------
-def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None = None, den32: bool = False):
+def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None = None, den32: bool = False,
+                mm=None):
     """VAMP (SVD form): Tracker (vamp.py:12-28), VAMPLayer.forward (vamp.py:56-94),
     VAMP.forward loop + early exit (vamp.py:159-187).
 
@@ -242,7 +243,10 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
     Returns dict(r, xmmse, var, T) where ``r`` is the decision input (vamp.py:187).
     den32: the denoiser in the GPU engines' float32 arithmetic (block_denoise_f32) instead of
     the reference's float64 — a rounding model, not the reference.
+    mm: the c64 matrix product of the two per-iteration GEMMs (vamp.py:67, 72), default numpy's
+    (BLAS); diagnostics pass other summation orders (tools/gemm_order_probe.py).
     """
+    mm = mm or (lambda a, b: a @ b)
     U = np.asarray(U, C64); Vh = np.asarray(Vh, C64); y = np.asarray(y, C64)
     s = np.asarray(s, F32)
     B = y.shape[0]
@@ -265,11 +269,11 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
         first = isinstance(s2t, float)
         # vamp.py:66 — python/python at t=0, else reciprocal(tensor)*python
         vr = F32(noise_var / s2t) if first else F32(_recip(s2t) * F32(noise_var))
-        q = (rt @ Vh.T).astype(C64)                               # vamp.py:67
+        q = mm(rt, Vh.T).astype(C64)                              # vamp.py:67
         scale = _recip(s2 + vr)                                   # vamp.py:68
         xt = (scale * (ytil + vr * q)).astype(C64)                # vamp.py:70
         varL = F32(F32(np.sum(scale, dtype=np.float64) / scale.size) * F32(noise_var))   # vamp.py:71
-        xt = ((xt - q) @ Vt + rt).astype(C64)                     # vamp.py:72
+        xt = (mm((xt - q).astype(C64), Vt) + rt).astype(C64)      # vamp.py:72
         if first:                                                 # vamp.py:73
             xtv = F32(F32(eta) * varL + F32((1 - eta) * s2t))
             alpha = F32(xtv / F32(s2t))                           # vamp.py:75

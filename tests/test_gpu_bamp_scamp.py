@@ -252,14 +252,17 @@ def test_scamp_fused_decision_equals_standalone(device, alph, ebn0, B, shape):
     assert int(L.loss['T']) == int(T.status().T)
 
 
-@pytest.mark.parametrize('name', ['cfg3_scamp_16qam', 'cfg3_scamp_qpsk'])
-def test_scamp_persistent_reproducible(device, name):
+@pytest.mark.parametrize('name,alphabet', [('cfg3_scamp_16qam', None), ('cfg3_scamp_qpsk', None),
+                                           ('cfg3_scamp_16qam', '16PSK')])
+def test_scamp_persistent_reproducible(device, name, alphabet):
     """cfg3's shape runs the SCAMP engine with eight waves per workgroup (two per SIMD; 16-QAM
-    keeps the packed product-grid denoiser there): five forwards of the same batch
-    give the same T and every Loss value, bit for bit."""
+    keeps the packed product-grid denoiser there; 16PSK, not a grid, the scalar
+    per-point form): five forwards of the same batch give the same T and every Loss value, bit for
+    bit."""
     from scamp import SCAMP
     ent = CURVES[name]
-    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], alphabet or ent['alphabet'],
+                  iterations=ent['iterations'])
     inp = _regen_inputs(cfg, 1, 8.0, svd=False)
     det = SCAMP(cfg, engine=2)
     first = None

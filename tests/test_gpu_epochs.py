@@ -89,6 +89,100 @@ def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0, E):
         assert torch.equal(r2[e].view(torch.int32), r[e].view(torch.int32)), e
 
 
+@pytest.mark.parametrize('alphabet,ebn0', [('16QAM', 8.0), ('16PSK', 10.0), ('QPSK', 4.0)])
+def test_epochs_equal_sequential_n256(device, alphabet, ebn0):
+    """The eight-wave N = 256 engine (two waves per SIMD; cfg4's shape at B = 1024, 64 workgroups
+    per epoch): 4 epochs side by side equal 4 sequential forwards bit for bit, in three
+    repetitions of the grouped launch."""
+    cfg = _cfg(256, 8, 512, 1024, alphabet)
+    chan, SNR, eps = _epochs(cfg, 4, ebn0, seed=7)
+    det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
+    mv = lambda t: t.to(device).contiguous()  # noqa: E731
+    U, s, Vh = (mv(t) for t in chan)
+    for rep in range(3):
+        if rep:
+            grp = det.forward_epochs(U, s, Vh, [mv(e[3]) for e in eps], SNR, [mv(e[0]) for e in eps],
+                                     [e[1] for e in eps], [e[2] for e in eps])
+        r, xm, var = det.last_epochs
+        for e, (ls, st, r0, x0, v0) in enumerate(seq):
+            assert int(grp[e].loss['T']) == int(ls['T']), (rep, e)
+            assert torch.equal(r[e].view(torch.int32), r0.view(torch.int32)), (rep, e)
+            assert torch.equal(xm[e].view(torch.int32), x0.view(torch.int32)), (rep, e)
+            assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), (rep, e)
+
+
+def _epochs_per_channel(cfg, E, ebn0, seed):
+    """E epochs with a channel each, in the reference's call order at res = 1 (vamp_model.py:55-61:
+    channel + SVD, then message + noise, every epoch)."""
+    from channel import Channel
+    from data import Data
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    c = _cfg(cfg.Nt, cfg.Na, cfg.Nr, cfg.B, cfg.alphabet, device='cpu', iterations=cfg.N_Layers)
+    ch, da = Channel(c), Data(c)
+    SNR = c.snr(ebn0)
+    out = []
+    for e in range(E):
+        _, A = ch.generate_as_sparc()
+        U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+        x, sym, idx = da.generate_message()
+        y = A @ x + ch.awgn(SNR)
+        out.append(((U, s, Vh), (x, sym, idx, y)))
+    return SNR, out
+
+
+@pytest.mark.parametrize('Nt,Na,Nr,B,alphabet,ebn0,E', [(64, 4, 128, 1024, '16QAM', 8.0, 8),
+                                                        (64, 4, 128, 1024, 'QPSK', 4.0, 8),
+                                                        (256, 8, 512, 1024, '16QAM', 10.0, 4),
+                                                        (256, 8, 512, 1024, 'QPSK', 2.0, 4)])
+def test_epochs_per_channel_equal_sequential(device, Nt, Na, Nr, B, alphabet, ebn0, E):
+    """One channel per epoch (the reference's default res = 1, vamp_model.py:45, 56-58) in ONE
+    persistent launch (amp_vamp_detect_count_epochs_ch): every epoch equals its own sequential
+    forward bit for bit — T, every Loss value, r / xmmse / var."""
+    from vamp import VAMP
+    cfg = _cfg(Nt, Na, Nr, B, alphabet)
+    SNR, eps = _epochs_per_channel(cfg, E, ebn0, seed=13)
+    mv = lambda t: t.to(device).contiguous()  # noqa: E731
+    det = VAMP(cfg)
+    assert det.max_epochs(Nt) >= E
+    seq = []
+    for (U, s, Vh), (x, sym, idx, y) in eps:
+        L = det(mv(U), mv(s), mv(Vh), mv(y), SNR, mv(x), sym, idx)
+        seq.append((dict(L.loss), det.last.r.clone(), det.last.xmmse.clone(), det.last.var.clone()))
+    Us = [mv(e[0][0]) for e in eps]
+    ss = [mv(e[0][1]) for e in eps]
+    Vhs = [mv(e[0][2]) for e in eps]
+    for rep in range(2):
+        grp = det.forward_epochs(Us if rep == 0 else torch.stack(Us), ss if rep == 0 else torch.stack(ss),
+                                 Vhs if rep == 0 else torch.stack(Vhs), [mv(e[1][3]) for e in eps], SNR,
+                                 [mv(e[1][0]) for e in eps], [e[1][1] for e in eps], [e[1][2] for e in eps])
+        r, xm, var = det.last_epochs
+        for e, (ls, r0, x0, v0) in enumerate(seq):
+            lg = grp[e].loss
+            assert int(lg['T']) == int(ls['T']), (rep, e, lg['T'], ls['T'])
+            for k in ls:
+                assert np.array_equal(np.asarray(lg[k]), np.asarray(ls[k]), equal_nan=True), (rep, e, k)
+            assert torch.equal(r[e].view(torch.int32), r0.view(torch.int32)), (rep, e)
+            assert torch.equal(xm[e].view(torch.int32), x0.view(torch.int32)), (rep, e)
+            assert torch.equal(var[e].view(torch.int32), v0.view(torch.int32)), (rep, e)
+
+
+def test_simulate_group_epochs_res1_identical(device, tmp_path):
+    """Model.simulate at the reference's default res = 1 with group_epochs=True (one channel per
+    epoch, side by side) writes the same points as the per-epoch loop."""
+    from model import Model
+    cfg = _cfg(64, 4, 128, 1024, '16QAM')
+    outs = []
+    for grouped in (False, True):
+        m = Model(cfg, 'vamp', path=str(tmp_path / f'r{int(grouped)}'), seed=5, group_epochs=grouped)
+        outs.append(m.simulate(epochs=10, start=6.0, final=8.0, step=2.0, res=1))
+    assert len(outs[0]) == len(outs[1])
+    for a, b in zip(*outs):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+
+
 def test_epochs_independent_rare_path(device):
     """One epoch driven into the exact float64 rare path (its y scaled up: logits beyond the
     float64 range of the global shift) while the others are not: the per-epoch barrier counters

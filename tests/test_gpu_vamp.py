@@ -461,14 +461,18 @@ def test_vamp_accepts_lazy_conj_views(device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['cfg4_vamp_16qam', 'cfg4_vamp_qpsk'])
-def test_persistent_n256_reproducible(device, name):
-    """The N = 256 bf16x3 engine runs eight waves per workgroup (two per SIMD; the 16-point
-    alphabets keep the packed product-grid denoiser there): five forwards
-    of the same cfg4 batch give the same r / xmmse / var bits and T every time."""
+@pytest.mark.parametrize('name,alphabet', [('cfg4_vamp_16qam', None), ('cfg4_vamp_qpsk', None),
+                                           ('cfg4_vamp_16qam', '16PSK')])
+def test_persistent_n256_reproducible(device, name, alphabet):
+    """The N = 256 bf16x3 engine runs eight waves per workgroup (two per SIMD; 16-QAM keeps the
+    packed product-grid denoiser there; 16PSK, a 16-point alphabet that is
+    not a grid, must run the scalar per-point form, never the packed one that lost results at two
+    waves per SIMD): five forwards of the same cfg4-shape batch give the same r / xmmse / var bits
+    and T every time."""
     from vamp import VAMP
     ent = CURVES[name]
-    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], ent['alphabet'], iterations=ent['iterations'])
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], ent['B'], alphabet or ent['alphabet'],
+                  iterations=ent['iterations'])
     inp = _regen_inputs(cfg, 1, 8.0)
     det = VAMP(cfg, engine=2)
     first = None

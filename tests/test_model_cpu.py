@@ -143,3 +143,68 @@ def test_simulate_trial_shard_two_ranks_gloo(tmp_path):
     assert [p['EbN0dB'] for p in r0['res']] == [0.0, 1.0, 2.0]
     assert r0['res'] == r1['res']
     assert [p['fer'] for p in r0['res']] == [1.0, 1.0, 0.0]
+
+
+class FakeGroupedAmp(FakeAmp):
+    """Also stands in for VAMP.forward_epochs / max_epochs: records each grouped call's channels
+    (one shared channel, or one per epoch) and returns one Loss per epoch, the values a function
+    of the epoch's y, so grouped and sequential sweeps can be compared."""
+
+    def __init__(self, config, cap):
+        super().__init__(config)
+        self.cap = cap
+        self.groups = []
+
+    def max_epochs(self, k):
+        return self.cap
+
+    def _one(self, y):
+        L = Loss(self.L.config) if hasattr(self.L, 'config') else Loss(_cfg())
+        v = float(torch.view_as_real(y).double().abs().sum())
+        L.dump()
+        L.loss = {'T': 0}
+        L.record([1.0] + [v] * 13, 3)
+        return L
+
+    def __call__(self, U, s, Vh, y, SNR, x, sym, idx):
+        self.calls += 1
+        self.seq_U = getattr(self, 'seq_U', []) + [U]
+        return self._one(y)
+
+    def forward_epochs(self, U, s, Vh, ys, SNR, xs, syms, idxs):
+        per = isinstance(U, (list, tuple))
+        self.groups.append((len(ys), per, U if per else [U] * len(ys)))
+        return [self._one(y) for y in ys]
+
+
+@pytest.mark.parametrize('res,cap', [(1, 4), (4, 3), (2, 8)])
+def test_simulate_group_epochs_host_logic(tmp_path, res, cap):
+    """Model.simulate(group_epochs=True) draws the epochs' inputs in the reference's call order
+    (vamp_model.py:55-61: a channel when i % res == 0), hands chunks of at most max_epochs epochs to
+    forward_epochs — one channel per epoch when the chunk spans channels (res = 1), the shared one
+    otherwise — and writes the same points as the sequential sweep."""
+    from model import Model
+    cfg = _cfg()
+    outs, amps = [], []
+    for grouped in (False, True):
+        amp = FakeGroupedAmp(cfg, cap)
+        m = Model(cfg, 'vamp', path=str(tmp_path / f'g{int(grouped)}'), amp=amp, seed=3, group_epochs=grouped)
+        outs.append(m.simulate(epochs=10, start=0, final=1.0, step=1, res=res))
+        amps.append(amp)
+    seq, grp = amps
+    assert seq.groups == [] and grp.calls == 0
+    assert sum(n for n, _, _ in grp.groups) == 20 and max(n for n, _, _ in grp.groups) <= cap
+    for n, per, Us in grp.groups:
+        distinct = len({id(u) for u in Us})
+        assert per == (distinct > 1), (n, per, distinct)
+        if res == 1:
+            assert distinct == n          # a channel per epoch
+    # the channels each epoch was detected with: the same matrices in both sweeps
+    grouped_U = [u for _, _, Us in grp.groups for u in Us]
+    assert len(grouped_U) == len(seq.seq_U) == 20
+    for a, b in zip(grouped_U, seq.seq_U):
+        assert torch.equal(a, b)
+    for a, b in zip(*outs):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k

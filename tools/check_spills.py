@@ -25,8 +25,9 @@ ALLOWED = [
     # vamp_persist<NT=2, KK=16, NWV=4, DU=2, X3, OCC=2, H2?>: the cfg2 two-per-CU build (256 VGPRs),
     # 12 / 25 spilled values = the per-lane s^2 / y~ registers kept across the loop
     (r'_ZN3amp12vamp_persistILi2ELi16ELi4ELi2ELb1ELi2ELb[01]E', 'cfg2 16-QAM two-per-CU build'),
-    # the other two-per-CU alphabets (QPSK / 8-PSK / 64-QAM at N = 64, side-by-side epochs)
-    (r'_ZN3amp12vamp_persistILi2ELi(4|8|64)ELi4ELi[124]ELb1ELi2ELb[01]E', 'N = 64 two-per-CU builds'),
+    # the other two-per-CU alphabets (BPSK / QPSK / 8-PSK / 64-QAM at N = 64, side-by-side epochs;
+    # the fp16x2 BPSK build keeps 2 values since the fused decision is force-inlined)
+    (r'_ZN3amp12vamp_persistILi2ELi(1|2|4|8|64)ELi4ELi[124]ELb1ELi2ELb[01]E', 'N = 64 two-per-CU builds'),
     # 64-point alphabets at N = 256 (no BASELINE VAMP config): the wide denoiser's chunked table
     # beside the N = 256 GEMM registers, 12 values reloaded once per iteration
     (r'_ZN3amp12vamp_persistILi8ELi64ELi4ELi1ELb[01]ELi1ELb[01]E', '64-point alphabet at N = 256'),
@@ -36,6 +37,9 @@ ALLOWED = [
     # the eight-wave bf16x3 form (the N = 256 default): 256 registers per wave; loop-invariant
     # addresses and constants reloaded outside the GEMMs
     (r'_ZN3amp12vamp_persistILi4ELi(1|2|4|8|16|64)ELi8ELi[124]ELb1ELi1ELb0ELb0E', 'eight-wave bf16x3 at N = 256'),
+    # the four-wave bf16x3 form at N = 256 (AMP_VAMP_X3_WAVES=4, A/B runs only): the per-epoch
+    # channel pointers and the force-inlined decision cost BPSK 12 loop-invariant values
+    (r'_ZN3amp12vamp_persistILi8ELi(1|2)ELi4ELi[124]ELb1ELi1ELb0ELb0E', 'four-wave bf16x3 at N = 256 (A/B form)'),
     # the eight-wave bf16x3 SCAMP form (cfg3's shape), the same kind of loop invariants
     (r'_ZN3amp13scamp_persistILi4ELi16ELi2ELi32ELi(1|2|4|8|16|64)ELb1ELb0ELi8E', 'eight-wave bf16x3 SCAMP'),
 ]

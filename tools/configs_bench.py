@@ -41,8 +41,11 @@ CFGS = {
     'cfg2-epochs4': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
     # 8 epochs: two workgroups per CU (AMP_PERSIST_WG2, the N = 64 default since round 3)
     'cfg2-epochs8': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
+    # cfg2 at the reference's default res = 1: 8 epochs with a channel each side by side
+    # (amp_vamp_detect_count_epochs_ch); the inputs include each epoch's own SVD factors
+    'cfg2-res1': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
 }
-EPOCHS = {'cfg2-epochs4': 4, 'cfg2-epochs8': 8}
+EPOCHS = {'cfg2-epochs4': 4, 'cfg2-epochs8': 8, 'cfg2-res1': 8}
 
 
 def main(steps=50, warmup=30, only=None):
@@ -65,11 +68,19 @@ def main(steps=50, warmup=30, only=None):
         sym, idx = lab(sym), lab(idx)
         E = EPOCHS.get(name, 1)
         if E > 1:
+            res1 = name.endswith('res1')
             eps = [(x, sym, idx, y)]
+            chans = [torch.linalg.svd(A, full_matrices=False)]
             for _ in range(E - 1):
+                if res1:
+                    _, A = ch.generate_as_sparc()
+                    chans.append(torch.linalg.svd(A, full_matrices=False))
                 xe, se, ie = da.generate_message()
                 eps.append((xe, lab(se), lab(ie), A @ xe + ch.awgn(SNR)))
-            U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+            if res1:   # stacked [E, ...] channel factors: one channel per epoch
+                U, s, Vh = (torch.stack([c[i] for c in chans]) for i in range(3))
+            else:
+                U, s, Vh = chans[0]
             det = VAMP(cfg)
             # the epochs' inputs stacked [E, B, ...] in HBM (forward_epochs uses them without a copy)
             ea = (mv(U), mv(s), mv(Vh), torch.stack([mv(e[3]) for e in eps]), SNR,
@@ -87,6 +98,7 @@ def main(steps=50, warmup=30, only=None):
             Ts = [int(L.loss['T']) for L in Ls]
             tf = B * sum(Ts) * flop / (ms * 1e-3) / 1e12
             print(json.dumps({'config': name, 'algo': algo, 'engine': 'persistent (side-by-side epochs)',
+                              'channels': E if res1 else 1,
                               'epochs_per_launch': E, 'Nt': Nt, 'Nr': Nr, 'Na': Na, 'alphabet': alph, 'B': B,
                               'EbN0': ebn0, 'T': Ts, 'ser': [float(L.loss['ser']) for L in Ls],
                               'ms_per_launch': round(ms, 4), 'ms_per_epoch': round(ms / E, 4),

@@ -1,11 +1,11 @@
 #!/usr/bin/env bash
-# Round-4 GPU session driver (run from the repo root on the box).  STEPS names the steps to run,
+# GPU session driver (run from the repo root on the box).  STEPS names the steps to run,
 # in order, e.g. STEPS="bench bench_h2 trace tests_vamp".  Each GPU step has its own time limit;
 # any non-zero exit ends the session (no retries).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-r04}
+OUT=gpurun_out/${TAG:-r05}
 mkdir -p "$OUT"
 run() {
     local name=$1 lim=$2; shift 2
@@ -79,6 +79,26 @@ for s in ${STEPS:-bench}; do
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     profile) run profile 900 bash tools/profile.sh ;;
     ubench) run ubench 300 bash tools/ubench/run.sh ;;
+    # round 5: denoiser precision diagnostics (libraries built in the container: -DAMP_DEN_EXACT_EXP=1,
+    # -DAMP_DEN_DIV=1, both; lib_diag/libampsparc_{exp,div,expdiv}.so) and the PKGRID A/B
+    deniso) run deniso_def 600 python3 tools/den_isolate.py --oracle &&
+            for v in ${DIAGS:-expdiv exp div}; do
+                run deniso_$v 600 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_$v.so python3 tools/den_isolate.py || exit 1
+            done ;;
+    tprobe_diag) for v in ${DIAGS:-expdiv}; do
+                run tprobe_$v 600 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_$v.so python3 tools/t_probe.py || exit 1
+            done ;;
+    ab_pkg0) run ab_def 300 python3 bench.py --no-cpu-baseline &&
+             run ab_pkg0 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pkg0.so python3 bench.py --no-cpu-baseline &&
+             run ab_def2 300 python3 bench.py --no-cpu-baseline &&
+             run ab_pkg0_2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pkg0.so python3 bench.py --no-cpu-baseline &&
+             run ab_cfg3 300 python3 tools/configs_bench.py cfg3 cfg3-qpsk &&
+             run ab_cfg3_pkg0 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_pkg0.so python3 tools/configs_bench.py cfg3 cfg3-qpsk ;;
+    ab_stg) run ab_stg_def 300 python3 bench.py --no-cpu-baseline &&
+            run ab_stg0 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_stg0.so python3 bench.py --no-cpu-baseline &&
+            run ab_stg_def2 300 python3 bench.py --no-cpu-baseline &&
+            run ab_stg0_2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_stg0.so python3 bench.py --no-cpu-baseline ;;
+    tests_repro) run tests_repro 600 $PYT tests/test_gpu_vamp.py tests/test_gpu_bamp_scamp.py tests/test_gpu_epochs.py -m gpu -k "reproducible or n256 or g2_denoiser or per_channel or res1" ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -91,7 +91,7 @@ def main():
         det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     nwg = (B + 15) // 16
-    tr = torch.zeros(nwg * iters * STRIDE + 2 * nwg, dtype=torch.int64, device=dev)
+    tr = torch.zeros(nwg * iters * STRIDE + 4 * nwg, dtype=torch.int64, device=dev)
     s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0.record()
     nat.check(nat.lib().amp_vamp_persist_trace(C.byref(T.dims), C.byref(T.const), C.byref(T.args), nat.dptr(tr),
@@ -112,11 +112,40 @@ def main():
         v = d[:, 1:, i] if Tn > 1 else d[:, :, i]
         print(f'  {name:22s} median {np.median(v):9.0f}  p10 {np.percentile(v, 10):9.0f}  p90 {np.percentile(v, 90):9.0f}'
               f'  ({100 * np.median(v) / per_it:5.1f} %)' if per_it else '')
-    # arrival skew at the barrier: spread of stamp 5 across workgroups per iteration (same clock
-    # domain only within an XCD; reported as a rough indicator)
-    print('  barrier arrival spread (max - min of stamp 5, cycles, median over t):',
-          np.median(st[:, 1:, 6].max(0) - st[:, 1:, 6].min(0)) if Tn > 1 else 0)
+    arrival_spread(a, st, nwg, iters, Tn)
 
+
+def arrival_spread(a, st, nwg, iters, Tn):
+    """Spread of the workgroups' arrival at the batch exchange (the stamp after the partial publish)
+    per iteration, in cycles.  s_memtime counts each XCD's own clock (its own origin), so stamps
+    are put on one time base with the per-workgroup (s_memtime, s_memrealtime) pairs taken at
+    kernel start and end: rate = d memtime / d realtime (cycles per 10 ns tick), and
+    t = realtime_start + (memtime - memtime_start) / rate.  Within one XCD (workgroups wg, wg + 8,
+    ... on round-robin dispatch) the raw s_memtime values are compared directly as a check."""
+    base = nwg * iters * STRIDE
+    m0, r0 = a[base:base + 2 * nwg:2].astype(np.float64), a[base + 1:base + 2 * nwg:2].astype(np.float64)
+    m1, r1 = a[base + 2 * nwg::2].astype(np.float64), a[base + 2 * nwg + 1::2].astype(np.float64)
+    if Tn < 2 or not (np.all(r1 > r0) and np.all(m1 > m0)):
+        print('  barrier arrival spread: no valid end stamps (old library?) '
+              f'm0 {m0[:3]} m1 {m1[:3]} r0 {r0[:3]} r1 {r1[:3]}')
+        return
+    rate = (m1 - m0) / (r1 - r0)                          # cycles per realtime tick, per workgroup
+    arr = st[:, 1:, 6].astype(np.float64)                 # [nwg, T-1]: publish done
+    g = r0[:, None] + (arr - m0[:, None]) / rate[:, None]  # realtime ticks
+    cyc = np.median(rate)
+    spread = (g.max(0) - g.min(0)) * cyc
+    lag = (g - g.min(0)) * cyc                            # [nwg, T-1] cycles behind the first arrival
+    late = np.argsort(-lag.mean(1))[:4]
+    # per XCD (workgroup wg runs on XCD wg % 8: round-robin dispatch): mean lag and clock
+    xl = [float(lag[x::8].mean()) for x in range(8)]
+    xc = [float(np.median(rate[x::8]) * 100) for x in range(8)]
+    print(f'  clock: {cyc * 100:.0f} MHz median (min {rate.min() * 100:.0f}, max {rate.max() * 100:.0f})')
+    print(f'  barrier arrival spread, all workgroups (realtime-aligned, cycles): median {np.median(spread):.0f} '
+          f'p10 {np.percentile(spread, 10):.0f} p90 {np.percentile(spread, 90):.0f}')
+    print('  mean arrival lag per XCD (cycles): ' + ' '.join(f'{v:.0f}' for v in xl))
+    print('  clock per XCD (MHz, median of its workgroups): ' + ' '.join(f'{v:.0f}' for v in xc))
+    print(f'  latest workgroups on average: {list(map(int, late))} '
+          f'(mean lag {[round(float((g[w] - g.min(0)).mean() * cyc)) for w in late]} cycles)')
 
 if __name__ == '__main__':
     main()
