@@ -64,6 +64,11 @@ class AmpVampDecideArgs(C.Structure):
                 ('pad', C.c_int32), ('counts', C.c_void_p)]
 
 
+class AmpVampShard(C.Structure):
+    _fields_ = [('xbuf', C.c_void_p), ('xbuf_bytes', C.c_size_t), ('B_global', C.c_int32), ('row_offset', C.c_int32),
+                ('gen', C.c_uint32), ('pad', C.c_int32)]
+
+
 class AmpBampArgs(C.Structure):
     _fields_ = [('H', C.c_void_p), ('y', C.c_void_p), ('max_iter', C.c_int32), ('denoiser', C.c_int32),
                 ('noise_var', C.c_double), ('xmap', C.c_void_p), ('xmmse', C.c_void_p), ('var', C.c_void_p),
@@ -116,6 +121,10 @@ SIGNATURES = {
                                                _P]),
     'amp_vamp_detect_count_epochs_ch': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
                                                   C.c_int64, C.c_int64, C.c_int64, _P]),
+    'amp_vamp_shard_xbuf_bytes': (C.c_size_t, [_I, _I]),
+    'amp_vamp_shard_reset': (C.c_int, [_P, _P]),
+    'amp_vamp_detect_count_shard': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs),
+                                              C.POINTER(AmpVampShard), _P]),
     'amp_bamp_workspace_bytes': (C.c_size_t, [_D, _I]),
     'amp_bamp_run': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),
     'amp_bamp_prepare': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _P]),

@@ -214,7 +214,9 @@ struct CWeightJob {
     int packed;
     int ex = 14;        // WPACKH2: the operator's scale exponent (amp_persist.h H2_EX; SCAMP: SH2_EX)
 };
-// Up to 4 jobs in ONE launch; the same launch zeroes `nzero` words at `zero` (or none).
+// Up to CW_MAX_JOBS jobs in ONE launch (blockIdx.y = job; the side-by-side epochs with a channel
+// each build three per epoch); the same launch zeroes `nzero` words at `zero` (or none).
+constexpr int CW_MAX_JOBS = 24;
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st);

@@ -68,6 +68,10 @@ struct VampK {
     // (0, 0: one channel shared by every epoch)
     long long wch;
     int sch;
+    // trial sharding of one batch over several persistent grids (amp_vamp_detect_count_shard):
+    // this grid's first workgroup in the shared exchange, the exchange's workgroups, and its first
+    // trial (0, nwg, 0 for a whole batch or side-by-side epochs)
+    int wg_off, nwg_x, row_off;
     Const c;
 };
 

@@ -489,6 +489,9 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.dump = debug_dump_ptr();
     P.wch = 0;
     P.sch = 0;
+    P.wg_off = 0;
+    P.nwg_x = P.nwg;
+    P.row_off = 0;
     return AMP_OK;
 }
 
@@ -583,7 +586,8 @@ static bool ytil_x3_env() {
     return v;
 }
 bool ytil_x3_fits(int n, int k);
-int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st);
+int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st,
+                   int rows_per_op = 0, long long wq_stride = 0);
 
 // Side-by-side epochs with a channel each (P.wch != 0): every epoch's split-precision operators
 // (Vh, V, s Uh) from its own U / s / Vh (a->U + e * ch.U, ...), then y~ per epoch.
@@ -593,24 +597,25 @@ struct EpochChannels {
 static int vamp_persist_prepare_ch(VampK& P, const amp_vamp_args* a, const EpochChannels& ch, hipStream_t st) {
     const int pk = P.x3 == 3 ? WPACKI8 : WPACKX3;
     const long long q0 = (long long)16 * P.k * P.n;   // bytes between epochs' s Uh (the carve's f32 stride)
-    for (int e = 0; e < P.E; ++e) {
-        const float2* U = (const float2*)a->U + e * ch.U;
-        const float2* Vh = (const float2*)a->Vh + e * ch.Vh;
-        const float* sv = (const float*)a->s + e * ch.s;
-        char* wx1 = (char*)P.Wx1 + e * P.wch;
-        char* wx2 = (char*)P.Wx2 + e * P.wch;
-        char* wq0 = (char*)P.Wq0 + e * q0;
-        CWeightJob j[3];
-        j[0] = CWeightJob{Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)wx1, P.N, P.k, pk};
-        j[1] = CWeightJob{Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)wx2, P.k, P.N, pk};
-        j[2] = CWeightJob{U, 1, P.k, 1, sv, P.k, P.n, (float*)wq0, P.n, P.k, WPACKX3};
-        int rc = build_cweights(j, 3, e == 0 ? P.pbar : nullptr, PBAR_WORDS, st);
-        if (rc) return rc;
-        rc = ytil_x3_launch((const float*)a->y + (size_t)e * P.B * 2 * P.n, P.n, P.B, wq0,
-                            P.ytil + (size_t)e * P.B * 2 * P.k, P.k, st);
+    // every epoch's three operators, CW_MAX_JOBS / 3 epochs per launch (the first zeroes the barrier words)
+    constexpr int EPL = CW_MAX_JOBS / 3;
+    for (int e0 = 0; e0 < P.E; e0 += EPL) {
+        CWeightJob j[CW_MAX_JOBS];
+        const int ne = std::min(EPL, P.E - e0);
+        for (int i = 0; i < ne; ++i) {
+            const int e = e0 + i;
+            const float2* U = (const float2*)a->U + e * ch.U;
+            const float2* Vh = (const float2*)a->Vh + e * ch.Vh;
+            const float* sv = (const float*)a->s + e * ch.s;
+            j[3 * i + 0] = CWeightJob{Vh, P.N, 1, 0, nullptr, P.k, P.N, (float*)((char*)P.Wx1 + e * P.wch), P.N, P.k, pk};
+            j[3 * i + 1] = CWeightJob{Vh, 1, P.N, 1, nullptr, P.N, P.k, (float*)((char*)P.Wx2 + e * P.wch), P.k, P.N, pk};
+            j[3 * i + 2] = CWeightJob{U, 1, P.k, 1, sv, P.k, P.n, (float*)((char*)P.Wq0 + e * q0), P.n, P.k, WPACKX3};
+        }
+        const int rc = build_cweights(j, 3 * ne, e0 == 0 ? P.pbar : nullptr, PBAR_WORDS, st);
         if (rc) return rc;
     }
-    return AMP_OK;
+    // y~ of every epoch in one launch, each row block with its epoch's s Uh
+    return ytil_x3_launch((const float*)a->y, P.n, P.B * P.E, P.Wq0, P.ytil, P.k, st, P.B, q0);
 }
 
 static int vamp_persist_prepare(VampK& P, const amp_vamp_args* a, hipStream_t st, const EpochChannels* ch = nullptr) {
@@ -906,6 +911,7 @@ static int detect_count_epochs_impl(const amp_dims* d, const amp_constellation* 
     P.E = epochs;
     P.wpe = cdiv(d->B, PBM);
     P.nwg = P.E * P.wpe;
+    P.nwg_x = P.nwg;
     AMP_REQUIRE(P.x3 || P.nwg <= ncu, "amp_vamp_detect_count_epochs: %d workgroups need two per CU, which only the "
                 "bf16x3 engine runs (gemm = AMP_GEMM_F32 holds at most %d epochs)", P.nwg, ncu / P.wpe);
     AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts,
@@ -936,6 +942,83 @@ int amp_vamp_detect_count_epochs_ch(const amp_dims* d, const amp_constellation* 
     EpochChannels ch;
     ch.U = U_stride; ch.s = s_stride; ch.Vh = Vh_stride;
     return detect_count_epochs_impl(d, c, a, dec, epochs, ch, stream);
+}
+
+// ---- one batch's trials over several persistent grids (SURVEY §8(e) exact-compat mode) ----
+// The shared exchange buffer: barrier words, the rare path's float64 words and the per-iteration
+// granule pairs of every workgroup of the batch (the same carve on every rank).
+struct ShardX {
+    unsigned* pbar;
+    double* pxch;
+    Partial* pparts;
+    size_t bytes;
+};
+static ShardX shard_carve(void* base, int nwx, int max_iter) {
+    Carve cv(base);
+    ShardX x;
+    x.pbar = cv.take<unsigned>(PBAR_WORDS);
+    x.pxch = cv.take<double>((size_t)max_iter * nwx * 4);
+    x.pparts = cv.take<Partial>((size_t)max_iter * nwx);
+    x.bytes = cv.off;
+    return x;
+}
+
+size_t amp_vamp_shard_xbuf_bytes(int32_t B_global, int32_t max_iter) {
+    if (B_global <= 0 || max_iter <= 0) return 0;
+    return shard_carve(nullptr, cdiv(B_global, PBM), max_iter).bytes;
+}
+
+int amp_vamp_shard_reset(void* xbuf, void* stream) {
+    AMP_REQUIRE(xbuf, "amp_vamp_shard_reset: null buffer");
+    const hipError_t e = hipMemsetAsync(xbuf, 0, PBAR_WORDS * sizeof(unsigned), (hipStream_t)stream);
+    AMP_REQUIRE(e == hipSuccess, "amp_vamp_shard_reset: %s", hipGetErrorString(e));
+    return AMP_OK;
+}
+
+int amp_vamp_detect_count_shard(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                const amp_vamp_decide_args* dec, const amp_vamp_shard* sh, void* stream) {
+    AMP_REQUIRE(d && sh && sh->xbuf, "amp_vamp_detect_count_shard: null argument");
+    AMP_REQUIRE(sh->row_offset >= 0 && sh->row_offset % PBM == 0 && sh->row_offset + d->B <= sh->B_global &&
+                    (d->B % PBM == 0 || sh->row_offset + d->B == sh->B_global),
+                "amp_vamp_detect_count_shard: rows [%d, %d) of %d (a shard starts at a multiple of %d trials and "
+                "only the last may end off it)", sh->row_offset, sh->row_offset + d->B, sh->B_global, PBM);
+    const int ncu = device_cu_count();
+    AMP_REQUIRE(a && a->engine != AMP_ENGINE_LAUNCHES && vamp_persist_eligible(d, a->k, ncu, 1, a->gemm),
+                "amp_vamp_detect_count_shard: needs the persistent engine for this shard's shape");
+    AMP_REQUIRE(dec && dec->x && dec->sym && dec->idx && dec->counts, "amp_vamp_detect_count_shard: null pointer argument");
+    AMP_REQUIRE(dec->ibits_trunc >= 0 && dec->ibits_trunc < 64, "amp_vamp_detect_count_shard: ibits_trunc");
+    AMP_REQUIRE(d->Lin * d->Na * d->M == d->N, "amp_vamp_detect_count_shard: inconsistent dims");
+    const int nwx = cdiv(sh->B_global, PBM);
+    const ShardX x = shard_carve(sh->xbuf, nwx, a->max_iter);
+    AMP_REQUIRE(sh->xbuf_bytes >= x.bytes, "amp_vamp_detect_count_shard: exchange buffer %zu < %zu bytes",
+                sh->xbuf_bytes, x.bytes);
+    VampK P;
+    Const64 c64;
+    int rc = vamp_setup(d, c, a, P, c64);     // this shard's rows: workspace, operators, y~
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    rc = vamp_persist_prepare(P, a, st);
+    if (rc) return rc;
+    // the batch's exchange: this grid's workgroups at their global index, the batch's size for
+    // var.mean() (vamp.py:85), the shared generation for the granule tags
+    P.wg_off = sh->row_offset / PBM;
+    P.nwg_x = nwx;
+    P.wpe = nwx;
+    P.E = 1;
+    P.row_off = sh->row_offset;
+    P.B = sh->B_global;
+    P.Bmean = sh->B_global;
+    P.pbar = x.pbar;
+    P.pxch = x.pxch;
+    P.pparts = x.pparts;
+    P.gen = sh->gen;
+    P.dec_on = 1;
+    P.ibits = dec->ibits_trunc;
+    P.xtrue = (const float2*)dec->x;
+    P.sym = (const long long*)dec->sym;
+    P.idx = (const long long*)dec->idx;
+    P.counts = (amp_counts*)dec->counts;
+    return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 
 // Measurement helper (bench.py): one full forward with hipEvents between the launches on

@@ -122,7 +122,8 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
     static_cast<Const64&>(d2) = c64;
     int rc = persist_dispatch(P, d2, st);
     if (rc || !P.dec_on) return rc;
-    hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.wpe, P.counts);
+    // one block per epoch folds this launch's workgroup records (a shard: its own workgroups)
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg / P.E, P.counts);
     AMP_LAUNCH_CHECK("vamp_decide_fold");
     return AMP_OK;
 }

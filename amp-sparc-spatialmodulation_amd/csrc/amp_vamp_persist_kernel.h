@@ -120,11 +120,16 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     float* scr = lds + Y.offScr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wg = blockIdx.x, nwg = gridDim.x;
+    // the exchange: workgroup wgx of nwx (a trial-sharded batch, amp_vamp_detect_count_shard: every
+    // rank's grid publishes into one shared granule array at its global workgroup index, so the
+    // batch scalars are reduced in the whole batch's order; else wgx = wg, nwx = nwg)
+    const int wgx = wg + P.wg_off, nwx = P.nwg_x;
     // side-by-side epochs: workgroups [ep * wpe, (ep + 1) * wpe) hold epoch ep's B trials and
     // exchange its batch scalars among themselves only
-    const int ep = wg / P.wpe, wl = wg - ep * P.wpe, wg0 = ep * P.wpe;
-    const int lrow0 = wl * PBM;                       // first trial within the epoch
-    const int row0 = ep * P.B + lrow0, nrows = min(PBM, P.B - lrow0);
+    const int ep = wgx / P.wpe, wl = wgx - ep * P.wpe, wg0 = ep * P.wpe;
+    const int lrow0 = wl * PBM;                       // first trial within the epoch (the batch's index)
+    // its row in this launch's arrays (a shard holds rows [row_off, row_off + its B) of the batch)
+    const int row0 = ep * P.B + lrow0 - P.row_off, nrows = min(PBM, P.B - lrow0);
     unsigned* ebar = P.pbar + (P.E > 1 ? PBAR_EPOCH + ep : 0);   // this epoch's arrival counter
     const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
     // this epoch's channel (one per epoch, or one shared: wch = sch = 0)
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
     }
     unsigned nbar = 0;
-    const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwg) * 32u);
+    const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwx) * 32u);
     int fixed = 0, last_t = 0, aborted = 0;
     VampIter nx = cur;
     // 5. batch scalars of iteration te (its partials published): every workgroup gathers and reduces
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     auto exchange = [&](int te, float* vnew, const float* vprev) -> bool {
             PartAcc g;
             const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)te + 1u;
-            if (!part_gather(grs, ((unsigned)te * nwg + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) return false;
+            if (!part_gather(grs, ((unsigned)te * nwx + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) return false;
             stamp(te, 6);
             fixed = 0;
             if (part_allnan(g)) {
@@ -311,11 +316,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 if (tid == 0) {
                     double m4 = 0.0;
                     for (int w = 0; w < PWG / 64; ++w) m4 = fmax(m4, s_d[w][0]);
-                    P.pxch[((size_t)te * nwg + wg) * 4 + 0] = m4;
+                    P.pxch[((size_t)te * nwx + wgx) * 4 + 0] = m4;
                 }
                 if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) return false;
                 double G = 0.0;
-                for (int w = wg0; w < wg0 + P.wpe; ++w) G = fmax(G, P.pxch[((size_t)te * nwg + w) * 4 + 0]);
+                for (int w = wg0; w < wg0 + P.wpe; ++w) G = fmax(G, P.pxch[((size_t)te * nwx + w) * 4 + 0]);
                 // (b) exact recompute of this workgroup's sections below the danger line
                 double dsum = 0.0;
                 int dnc = 0, cnt = 0;
@@ -343,14 +348,14 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
                 if (tid == 0) {
                     double a = 0.0, b = 0.0, c = 0.0;
                     for (int w = 0; w < PWG / 64; ++w) { a += s_d[w][1]; b += s_d[w][2]; c += s_d[w][3]; }
-                    P.pxch[((size_t)te * nwg + wg) * 4 + 1] = a;
-                    P.pxch[((size_t)te * nwg + wg) * 4 + 2] = b;
-                    P.pxch[((size_t)te * nwg + wg) * 4 + 3] = c;
+                    P.pxch[((size_t)te * nwx + wgx) * 4 + 1] = a;
+                    P.pxch[((size_t)te * nwx + wgx) * 4 + 2] = b;
+                    P.pxch[((size_t)te * nwx + wgx) * 4 + 3] = c;
                 }
                 if (!grid_sync_on(ebar, P.pbar + 1, ++nbar * (unsigned)P.wpe, &s_flag)) return false;
                 double a = 0.0, b = 0.0, c = 0.0;
                 for (int w = wg0; w < wg0 + P.wpe; ++w) {
-                    const double* q = P.pxch + ((size_t)te * nwg + w) * 4;
+                    const double* q = P.pxch + ((size_t)te * nwx + w) * 4;
                     a += q[1]; b += q[2]; c += q[3];
                 }
                 g.sumvar += a;   // (sum - old) + new, in float64
@@ -680,7 +685,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         }
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
-        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
+        part_publish(pa, grs, ((unsigned)t * nwx + wgx) * 32u, tag, scr);
         if (P.dump) {   // xmmse and var after the denoiser (part_publish's barrier ordered the LDS writes)
             float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 2) * PBM * twoN;
             for (int e = tid; e < PBM * twoN; e += PWG) dp[e] = sX[(e / twoN) * ldr + e % twoN];
@@ -712,7 +717,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldr + col];
     }
     for (int e = tid; e < nrows * N; e += PWG) P.var0[(size_t)row0 * N + e] = vlast[e];
-    if (wl == 0 && tid == 0) {
+    if (wl == P.wg_off && tid == 0) {   // this launch's first workgroup of the epoch
         amp_status s = vamp_make_status(P, cur, nx, fixed);
         if (aborted) s.nan_state = -1;
         P.status[ep] = s;

@@ -40,9 +40,12 @@ namespace amp {
 // split into six bf16 planes in LDS (n complex per row), the operator s Uh x3-packed (K = n,
 // O = k), the result in the accumulator layout straight to ytil.  Replaces the f32-MFMA
 // gemm_store launch (47.7 us per cfg4 step at 0.56 of the f32 peak, profiles/r04_cfg4_vamp_x3.txt).
+// rows_per_op / wq_stride: side-by-side epochs with a channel each use the operator of their
+// epoch, wq + (row / rows_per_op) * wq_stride bytes (rows_per_op a multiple of PBM).
 template <int NC, int G, int NWV = 4>
 __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __restrict__ y, int rows, const void* wq,
-                                                               float* __restrict__ ytil, int k) {
+                                                               float* __restrict__ ytil, int k, int rows_per_op,
+                                                               long long wq_stride) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     unsigned short* sP = reinterpret_cast<unsigned short*>(lds);
     constexpr int n = 32 * G;
@@ -62,7 +65,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
     }
     __syncthreads();
     f32x4 cr[NC], ci[NC];
-    gemm_x3<NC, G, 1>(sP, ldx, wq, wave * NC, cr, ci);
+    const void* wop = (const char*)wq + (long long)(row0 / rows_per_op) * wq_stride;
+    gemm_x3<NC, G, 1>(sP, ldx, wop, wave * NC, cr, ci);
 #pragma unroll
     for (int t = 0; t < NC; ++t) {
         const int o = 16 * (wave * NC + t) + (lane & 15);
@@ -75,7 +79,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
 }
 
 template <int NC, int G, int NWV = 4>
-static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* ytil, int k, hipStream_t st) {
+static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* ytil, int k, int rows_per_op,
+                            long long wq_stride, hipStream_t st) {
     const void* fn = (const void*)ytil_x3_kernel<NC, G, NWV>;
     const size_t lds = (size_t)6 * PBM * pl_ldx(32 * G) * 2;
     static int attr = -1;   // once per instantiation (single-threaded host use, like the rest of the ABI)
@@ -87,7 +92,8 @@ static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* yti
         }
         attr = 1;
     }
-    hipLaunchKernelGGL((ytil_x3_kernel<NC, G, NWV>), dim3(cdiv(rows, PBM)), dim3(64 * NWV), lds, st, y, rows, wq, ytil, k);
+    hipLaunchKernelGGL((ytil_x3_kernel<NC, G, NWV>), dim3(cdiv(rows, PBM)), dim3(64 * NWV), lds, st, y, rows, wq, ytil, k,
+                       rows_per_op, wq_stride);
     AMP_LAUNCH_CHECK("ytil_x3");
     return AMP_OK;
 }
@@ -95,12 +101,15 @@ static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* yti
 // The shapes of the split-precision engines (k == N, n == 2N): false for any other.
 bool ytil_x3_fits(int n, int k) { return n == 2 * k && (k == 64 || k == 128 || k == 256); }
 
-int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st) {
+int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil, int k, hipStream_t st,
+                   int rows_per_op, long long wq_stride) {
+    if (rows_per_op <= 0) rows_per_op = rows;   // one operator for every row
+    AMP_REQUIRE(rows_per_op % PBM == 0 || rows_per_op >= rows, "ytil_x3: rows per operator %d", rows_per_op);
     switch (k) {
-    case 64: return ytil_x3_launch_t<1, 4>(y, rows, wq, ytil, k, st);
-    case 128: return ytil_x3_launch_t<2, 8>(y, rows, wq, ytil, k, st);
+    case 64: return ytil_x3_launch_t<1, 4>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
+    case 128: return ytil_x3_launch_t<2, 8>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
     case 256:   // eight waves (two per SIMD) hide the operator stream better, as in the engine
-        return ytil_x3_launch_t<2, 16, 8>(y, rows, wq, ytil, k, st);
+        return ytil_x3_launch_t<2, 16, 8>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
     default: break;
     }
     set_error("ytil_x3: n = %d / k = %d not supported", n, k);

@@ -109,7 +109,7 @@ int build_cweight(const float2* src, long so, long sj, int conj, const float* ro
 }
 
 struct CWeightJobs {
-    CWeightJob j[4];
+    CWeightJob j[CW_MAX_JOBS];
     unsigned* zero;
     int nzero;
 };
@@ -265,7 +265,7 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
 }
 
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st) {
-    AMP_REQUIRE(njobs >= 1 && njobs <= 4, "build_cweights: %d jobs", njobs);
+    AMP_REQUIRE(njobs >= 1 && njobs <= CW_MAX_JOBS, "build_cweights: %d jobs", njobs);
     CWeightJobs P;
     long most = 0;
     for (int i = 0; i < njobs; ++i) {

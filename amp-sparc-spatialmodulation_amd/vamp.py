@@ -624,6 +624,76 @@ class ShardedVAMP(ShardHook, VAMP):
         return L
 
 
+class PersistentShard:
+    """One grid of a batch whose trials are split over several PERSISTENT grids that share one
+    exchange buffer (amp_vamp_detect_count_shard, SURVEY §8(e) exact-compat): this shard detects
+    trials [row_offset, row_offset + rows) of the batch `config` describes, publishes its
+    per-iteration partials at its workgroups' global indices and reduces every shard's, so its
+    scalars, T and rows of r / xmmse / var equal the whole-batch forward's bit for bit.  All
+    shards of one forward run concurrently (different streams; on one GPU they must fit on the CUs
+    together) with the same `gen`, after amp_vamp_shard_reset of the buffer; each returns its rows'
+    counters (sum them).  Inputs are this shard's rows (y, x, labels) and the whole channel."""
+
+    def __init__(self, config: Config, row_offset: int, rows: int, gemm: int = nat.GEMM_AUTO) -> None:
+        from loss import Loss
+        self.config, self.row_offset, self.rows, self.gemm = config, row_offset, rows, gemm
+        self.E = config.Na / config.Nr
+        self.sparsity = config.Na / config.Nt
+        self._whole = Loss(config)          # the batch's ibits (flat indices of the whole batch)
+        self._bufs = None
+
+    @staticmethod
+    def xbuf(config: Config, device) -> torch.Tensor:
+        nbytes = nat.lib().amp_vamp_shard_xbuf_bytes(config.B, config.N_Layers)
+        return torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=device)
+
+    def launch(self, U, s, Vh, y, SNR: float, x, symbols, indices, xbuf: torch.Tensor, gen: int) -> torch.Tensor:
+        """Queue this shard's forward on the current stream; returns its 256-byte result buffer
+        (amp_status @0, amp_counts @64; read it after the stream has finished: read_result)."""
+        from loss import _as_device_labels, _flat_c64
+        cfg, Bl = self.config, self.rows
+        n, k = U.shape[0], U.shape[1]
+        N = Vh.shape[1]
+        dev = y.device
+        Uc, Vhc = _c64(U, (n, k)), _c64(Vh, (k, N))
+        sc = s.reshape(k).to(torch.float32).resolve_neg().contiguous()
+        yl = _c64(y, (Bl, n)).contiguous()
+        d, cst = cfg.dims(batch=Bl), cfg.constellation()
+        lib = nat.lib()
+        wsb = lib.amp_vamp_workspace_bytes(C.byref(d), k, cfg.N_Layers)
+        if wsb == 0:
+            raise ValueError('amp_vamp_workspace_bytes: invalid dimensions')
+        self.ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        self.r = torch.empty(Bl, N, dtype=torch.complex64, device=dev)
+        self.xmmse = torch.empty_like(self.r)
+        self.var = torch.empty(Bl, N, dtype=torch.float32, device=dev)
+        res = torch.zeros(256, dtype=torch.uint8, device=dev)
+        a = nat.AmpVampArgs()
+        a.U, a.s, a.Vh, a.y = nat.dptr(Uc, name='U'), nat.dptr(sc, torch.float32, 's'), nat.dptr(Vhc, name='Vh'), \
+            nat.dptr(yl, name='y')
+        a.k, a.max_iter, a.engine, a.gemm = k, cfg.N_Layers, nat.ENGINE_PERSISTENT, self.gemm
+        a.noise_var, a.sparsity = float(self.E / SNR), float(self.sparsity)
+        a.r, a.xmmse, a.var = nat.dptr(self.r), nat.dptr(self.xmmse), nat.dptr(self.var)
+        a.status = nat.dptr(res)
+        a.ws, a.ws_bytes = nat.dptr(self.ws), self.ws.numel()
+        xt = _flat_c64(x, Bl, 'x')
+        sym = _as_device_labels(symbols, dev).reshape(-1)
+        idx = _as_device_labels(indices, dev).reshape(-1)
+        if sym.numel() != Bl * cfg.L or idx.numel() != Bl * cfg.L:
+            raise ValueError(f'expected {Bl * cfg.L} labels/indices for the shard, got {sym.numel()}/{idx.numel()}')
+        dec = nat.AmpVampDecideArgs()
+        dec.x, dec.sym, dec.idx = nat.dptr(xt, name='x'), nat.dptr(sym, name='symbols'), nat.dptr(idx, name='indices')
+        dec.ibits_trunc = self._whole._ibits
+        dec.counts = nat.dptr(res) + 64
+        sh = nat.AmpVampShard()
+        sh.xbuf, sh.xbuf_bytes = nat.dptr(xbuf), xbuf.numel()
+        sh.B_global, sh.row_offset, sh.gen = cfg.B, self.row_offset, gen
+        nat.check(lib.amp_vamp_detect_count_shard(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), C.byref(sh),
+                                                  nat.stream_ptr(dev)), 'amp_vamp_detect_count_shard')
+        self._keep = (Uc, sc, Vhc, yl, xt, sym, idx, res)
+        return res
+
+
 def read_result(res: torch.Tensor):
     """(amp_status, amp_counts) from the 256-byte result buffer (status @0, counts @64)."""
     raw = res.cpu().numpy().tobytes()

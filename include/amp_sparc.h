@@ -198,6 +198,33 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
 enum { AMP_ALLREDUCE_SUM = 0, AMP_ALLREDUCE_MAX = 1 };
 typedef int (*amp_allreduce_fn)(void* buf, int64_t count, int32_t op, void* stream, void* ctx);
 int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx);
+/* The same split on the PERSISTENT engine (one launch per forward, no per-iteration host calls):
+ * every rank's grid publishes its per-iteration batch partials into ONE shared exchange buffer at
+ * its workgroups' global indices and every workgroup of every rank reduces all of them in the
+ * whole batch's order, so every rank derives the whole-batch forward's scalars bit for bit
+ * (vamp.py:85, 112, 185) and its rows of r / xmmse / var equal the whole-batch forward's.
+ * xbuf: device memory every rank's kernel reads and writes (on one GPU: one allocation shared by
+ * grids on different streams, which must be co-resident together; across GPUs it would be
+ * peer-mapped memory, whose coherence this build does not provide: one device only), at least
+ * amp_vamp_shard_xbuf_bytes(B_global, max_iter) bytes; amp_vamp_shard_reset zeroes its barrier
+ * words, once before every forward after every rank's previous forward has finished.  gen: the
+ * same value on every rank, a new one for every forward on this buffer (it tags the exchange
+ * records).  This rank detects trials [row_offset, row_offset + d->B) (row_offset a multiple of 16,
+ * d->B too except for the last rank); y / r / xmmse / var / x / sym / idx hold its rows only;
+ * dec->counts gets its rows' counters (sum them over the ranks).  Replaces amp_vamp_run_sharded
+ * for the shapes the persistent engine takes (vamp.py:159-187). */
+typedef struct {
+    void* xbuf;
+    size_t xbuf_bytes;
+    int32_t B_global;
+    int32_t row_offset;
+    uint32_t gen;
+    int32_t pad;
+} amp_vamp_shard;
+size_t amp_vamp_shard_xbuf_bytes(int32_t B_global, int32_t max_iter);
+int amp_vamp_shard_reset(void* xbuf, void* stream);
+int amp_vamp_detect_count_shard(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
+                                const amp_vamp_decide_args* dec, const amp_vamp_shard* sh, void* stream);
 /* amp_vamp_run on this rank's slice (launch engine) with the batch scalars all-reduced; workspace
  * as amp_vamp_workspace_bytes(d, ...) for the slice.  Decide with amp_map_decide_count_rows. */
 int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, int32_t B_global,

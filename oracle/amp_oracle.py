@@ -201,52 +201,21 @@ def scamp_denoise(r: np.ndarray, tau_half: np.ndarray, cfg: OracleConfig) -> np.
     return xm.astype(C64).reshape(B, -1)
 
 
-def block_denoise_f32(r: np.ndarray, tau, cfg: OracleConfig):
-    """block_denoise evaluated in float32 the way the gfx950 denoiser does it (amp_denoise.h
-    denoise_sections_g): u = r * (1 / tau), logits u.re a.re + u.im a.im, the shift by the
-    SECTION max, Z and Z - Z_m as sums of non-negative terms, x = (sum a eta) / Z by the
-    reciprocal, var = |x|^2 (Z - Z_m) / Z + sum |x - a|^2 eta / Z.  Not the reference's
-    arithmetic (vamp.py:108-119 works in float64): a model of the GPU engines' rounding, used
-    only to bound iteration counts where the reference's own early exit is decided by rounding
-    (tests/golden/make_goldens.py g4pp_f32den).  VAMP's real-division path only (tau 0-dim)."""
-    B = r.shape[0]
-    sv = np.asarray(r, C64).reshape(B, cfg.L, cfg.M)
-    it = F32(1) / F32(tau)
-    ur = (sv.real.astype(F32) * it).astype(F32)
-    ui = (sv.imag.astype(F32) * it).astype(F32)
-    sym = cfg.symbols.astype(np.complex64)
-    cre, cim = sym.real.astype(F32), sym.imag.astype(F32)
-    with np.errstate(under='ignore', invalid='ignore', divide='ignore', over='ignore'):
-        xi = (ur[..., None] * cre + ui[..., None] * cim).astype(F32)            # [B,L,M,K]
-        eta = np.exp((xi - xi.max(axis=(2, 3), keepdims=True)).astype(F32)).astype(F32)
-        zm = eta.sum(axis=-1, dtype=F32)
-        z = zm.sum(axis=2, keepdims=True, dtype=F32)
-        iz = (F32(1) / z).astype(F32)
-        xr = ((eta * cre).sum(axis=-1, dtype=F32) * iz).astype(F32)
-        xim = ((eta * cim).sum(axis=-1, dtype=F32) * iz).astype(F32)
-        ze = (z - zm).astype(F32)
-        dr, di = xr[..., None] - cre, xim[..., None] - cim
-        vs = ((dr * dr + di * di) * eta).sum(axis=-1, dtype=F32)
-        var = ((xr * xr + xim * xim) * (ze * iz) + vs * iz).astype(F32)
-    return (xr + 1j * xim).astype(C64).reshape(B, -1), var.reshape(B, -1)
-
-
 # ----------------------------------------------------------------------------
 # detectors
 # ----------------------------------------------------------------------------
-def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None = None, den32: bool = False,
-                mm=None):
+def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None = None, mm=None, mm_y=None):
     """VAMP (SVD form): Tracker (vamp.py:12-28), VAMPLayer.forward (vamp.py:56-94),
     VAMP.forward loop + early exit (vamp.py:159-187).
 
     U [n,k] c64, s [k] f32, Vh [k,N] c64, y [B,n] c64.
     Returns dict(r, xmmse, var, T) where ``r`` is the decision input (vamp.py:187).
-    den32: the denoiser in the GPU engines' float32 arithmetic (block_denoise_f32) instead of
-    the reference's float64 — a rounding model, not the reference.
-    mm: the c64 matrix product of the two per-iteration GEMMs (vamp.py:67, 72), default numpy's
-    (BLAS); diagnostics pass other summation orders (tools/gemm_order_probe.py).
+    mm / mm_y: the c64 matrix product of the two per-iteration GEMMs (vamp.py:67, 72) / of y~
+    (vamp.py:22), default numpy's (BLAS); diagnostics pass other summation orders
+    (tools/gemm_order_probe.py).
     """
     mm = mm or (lambda a, b: a @ b)
+    mm_y = mm_y or (lambda a, b: a @ b)                          # the y~ product (vamp.py:22)
     U = np.asarray(U, C64); Vh = np.asarray(Vh, C64); y = np.asarray(y, C64)
     s = np.asarray(s, F32)
     B = y.shape[0]
@@ -256,7 +225,7 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
     Uh = np.conj(U).T
     Vt = np.conj(Vh)                                              # x @ V.T with V = Vh^H
     s2 = (s * s).astype(F32)
-    ytil = (y @ ((s[:, None] * Uh).astype(C64)).T).astype(C64)    # vamp.py:22
+    ytil = mm_y(y, ((s[:, None] * Uh).astype(C64)).T).astype(C64)  # vamp.py:22
     r = np.zeros((B, Vh.shape[1]), C64)
     var = np.ones((B, Vh.shape[1]), F32)
     rt = np.full((B, Vh.shape[1]), F32(p), dtype=C64)
@@ -286,7 +255,7 @@ def vamp_detect(U, s, Vh, y, SNR: float, cfg: OracleConfig, trace: list | None =
         r = _div_real(xt - alpha * rt, F32(1) - alpha)            # vamp.py:79
         sigma2 = F32(F32(alpha / (F32(1) - alpha)) * s2t32)       # vamp.py:80
         sigma2 = _clamp(sigma2, VAR_MIN, VAR_MAX)                 # vamp.py:81-82
-        xm, var = (block_denoise_f32 if den32 else block_denoise)(r, sigma2, cfg)   # vamp.py:84
+        xm, var = block_denoise(r, sigma2, cfg)                  # vamp.py:84
         mean_var = F32(np.sum(var, dtype=np.float64) / var.size)
         dxdr = _clamp(F32(mean_var / sigma2), VAR_RATIO_MIN, VAR_RATIO_MAX)   # vamp.py:85-87
         ns = _recip(F32(1) - dxdr)                                # vamp.py:89

@@ -934,38 +934,49 @@ def g4pp_den(names=None):
                 json.dump(db, f, indent=1, sort_keys=True)
 
 
-def g4pp_f32den(names=None):
-    """Where the reference's exit moved: the oracle's restatement of the reference (pinned to it
-    by g1-g4) run once more with its denoiser in the GPU engines' float32 arithmetic
-    (oracle.block_denoise_f32; the reference's denoiser is float64).  At noise-limited points the
-    float32 rounding keeps the batch mean var in a period-2 cycle in its last bits, which the exp
-    of the logits (|xi| ~ 10) amplifies past allclose's rtol in a few dozen elements, so the exit
-    never fires.  `T_f32den` joins `T_span`."""
-    sys.path.insert(0, os.path.join(HERE, '..', '..'))
-    from oracle import OracleConfig
-    from oracle import amp_oracle as O
+def relabel_within_sections(inp, cfg, g):
+    """The same problem with the positions of every section permuted (seeded): Vh's columns and x's
+    rows move together, so A[:, p] x[p] = A x = y unchanged and U, s, Vh[:, p] are exactly the
+    SVD factors of A[:, p].  Only the order of the reference's sums over the positions changes:
+    q = Vh r~ (vamp.py:67) reduces over them, and var.mean() (vamp.py:85) sums them in another
+    order.  Returns (Vh', x')."""
+    M = cfg.Nt // cfg.Na
+    nsec = cfg.Nt * cfg.Lin // M
+    perm = torch.cat([l * M + torch.randperm(M, generator=g) for l in range(nsec)])
+    return inp['Vh'][:, perm].contiguous(), inp['x'][:, perm].contiguous()
+
+
+def g4pr(names=None):
+    """Where the reference's exit moved: eight reruns OF THE REFERENCE on the unperturbed inputs
+    with the positions relabelled within every section (relabel_within_sections; seeded) — the
+    identical problem with the reference's GEMM and var.mean() summation orders changed, which is
+    what any other implementation of the same arithmetic (another BLAS, thread count or a GPU)
+    changes.  T recorded as `T_runs_perm` (the losses of a relabelled run compare positions, so
+    only T is kept); `T_span` = the span of every reference run (T_runs, T_runs_den,
+    T_runs_perm)."""
     path = os.path.join(HERE, 'g4_curves.json')
     db = json.load(open(path))
     for name, (algo, Nt, Na, Nr, B, alph, iters, grid, seeds) in G4_CONFIGS.items():
         if names and name not in names:
             continue
         cfg = cfg_of(Nt, Na, Nr, B, alph, iterations=iters)
-        ocfg = OracleConfig(Nt, Na, Nr, B=B, alphabet=alph, iterations=iters)
         ent = db[name]
         for key in sorted(ent['points'], key=lambda k: (int(k.split('/')[0]), float(k.split('/')[1]))):
             rec = ent['points'][key]
-            if 'T_runs' not in rec or 'T_f32den' in rec:
+            if 'T_runs' not in rec or 'T_runs_perm' in rec:
                 continue
             seed, EbN0 = int(key.split('/')[0]), float(key.split('/')[1])
             inp = gen_inputs(cfg, seed, EbN0, svd=(algo == 'vamp'))
             assert sha(inp['x']) == rec['sha_x'] and algo == 'vamp'
-            c = lambda t: np.asarray(t)[..., 0] if np.asarray(t).ndim == 3 else np.asarray(t)  # noqa: E731
-            out = O.vamp_detect(c(inp['U']), c(inp['s']), c(inp['Vh']), c(inp['y']), float(inp['SNR']), ocfg,
-                                den32=True)
-            rec['T_f32den'] = float(out['T'])
-            Ts = rec['T_runs'] + rec.get('T_runs_den', []) + [rec['T_f32den']]
+            Tp = []
+            for ps in PERT_SEEDS:
+                Vh, x = relabel_within_sections(inp, cfg, torch.Generator().manual_seed(3000 + ps))
+                L = ref_vamp.VAMP(cfg)(inp['U'], inp['s'], Vh, inp['y'], inp['SNR'], x, inp['sym'], inp['idx'])
+                Tp.append(float(np.asarray(L.loss['T'])))
+            rec['T_runs_perm'] = Tp
+            Ts = rec['T_runs'] + rec.get('T_runs_den', []) + Tp
             rec['T_span'] = [min(Ts), max(Ts)]
-            print(name, key, 'T with a float32 denoiser', out['T'], 'span', rec['T_span'], flush=True)
+            print(name, key, 'T runs (relabelled)', Tp, 'span', rec['T_span'], flush=True)
             with open(path, 'w') as f:
                 json.dump(db, f, indent=1, sort_keys=True)
 
@@ -1039,8 +1050,8 @@ if __name__ == '__main__':
             g4pp_elem(names or None)
         elif w == 'g4pd':
             g4pp_den(names or None)
-        elif w == 'g4pf':
-            g4pp_f32den(names or None)
+        elif w == 'g4pr':
+            g4pr(names or None)
         elif w == 'g11':
             g11()
         elif w == 'g12':

@@ -91,3 +91,65 @@ def test_sharded_single_process_is_whole_batch(device, name):
     assert a.keys() == b.keys()
     for k in a:
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), (k, a[k], b[k])
+
+
+# ---- persistent engine: several grids sharing one exchange buffer (amp_vamp_detect_count_shard) ----
+@pytest.mark.parametrize('Nt,Na,Nr,B,alphabet,ebn0,R', [(256, 8, 512, 4096, '16QAM', 8.0, 2),
+                                                        (256, 8, 512, 4096, 'QPSK', 2.0, 2),
+                                                        (256, 8, 512, 2048, '16QAM', 20.0, 4),
+                                                        (64, 4, 128, 1024, '16QAM', 10.0, 4),
+                                                        (64, 4, 128, 1000, 'QPSK', 6.0, 2)])
+def test_persistent_shards_equal_whole_batch(device, Nt, Na, Nr, B, alphabet, ebn0, R):
+    """R persistent grids on R streams of one GPU, each detecting a contiguous slice of ONE batch
+    and exchanging the per-iteration batch partials through one shared buffer (SURVEY §8(e)
+    exact-compat on the persistent engine): every shard's T and status equal the whole-batch
+    persistent forward's, its rows of r / xmmse / var are the same bits, and the shards' counters
+    sum to the whole batch's (the reduction runs over every workgroup of the batch in the same
+    order, so nothing differs, not even the float64 order of var.mean())."""
+    from test_gpu_vamp import _config, _regen_inputs
+    from vamp import VAMP, PersistentShard, read_result
+    cfg = _config(Nt, Na, Nr, B, alphabet, iterations=20)
+    inp = _regen_inputs(cfg, 3, ebn0)
+    det = VAMP(cfg, engine=2)
+    L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    whole = {k: float(np.asarray(v)) for k, v in L.loss.items()}
+    wst, wct = L.last_status, L.last_counts
+    wr, wx, wv = det.last.r.clone(), det.last.xmmse.clone(), det.last.var.clone()
+    # co-resident grids: every shard's workgroups on the CUs at once (16 trials per workgroup)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert (B + 15) // 16 <= (2 if Nt == 64 else 1) * ncu
+    per = ((B + R - 1) // R + 15) // 16 * 16
+    bounds = [(r0, min(B, r0 + per)) for r0 in range(0, B, per)]
+    xbuf = PersistentShard.xbuf(cfg, device)
+    import ctypes as C
+    import amp_native as nat
+    nat.check(nat.lib().amp_vamp_shard_reset(nat.dptr(xbuf), nat.stream_ptr(device)), 'reset')
+    torch.cuda.synchronize()
+    L_ = cfg.L
+    sym = torch.as_tensor(np.asarray(inp['sym'], np.int64)).reshape(B, L_)
+    idx = torch.as_tensor(np.asarray(inp['idx'], np.int64)).reshape(B, L_)
+    streams = [torch.cuda.Stream(device) for _ in bounds]
+    shards, results = [], []
+    for (b0, b1), st in zip(bounds, streams):
+        sh = PersistentShard(cfg, b0, b1 - b0)
+        with torch.cuda.stream(st):
+            results.append(sh.launch(inp['U'], inp['s'], inp['Vh'], inp['y'][b0:b1], inp['SNR'], inp['x'][b0:b1],
+                                     sym[b0:b1], idx[b0:b1], xbuf, gen=0x51A2D000 + B + R))
+        shards.append(sh)
+    torch.cuda.synchronize()
+    tot = {f: 0 for f, _ in nat.AmpCounts._fields_}
+    for (b0, b1), sh, res in zip(bounds, shards, results):
+        st, ct = read_result(res)
+        assert st.nan_state >= 0, 'a shard lost its grid (exchange timed out)'
+        assert (st.T, st.nan_state, st.stopped) == (wst.T, wst.nan_state, wst.stopped), (b0, st.T, wst.T)
+        assert list(st.last_scalar) == list(wst.last_scalar), b0
+        for f, _ in nat.AmpCounts._fields_:
+            tot[f] += getattr(ct, f)
+        for a, w in ((sh.r, wr), (sh.xmmse, wx), (sh.var, wv)):
+            assert torch.equal(a.reshape(b1 - b0, -1).view(torch.int32), w.reshape(B, -1)[b0:b1].view(torch.int32)), b0
+    for f, ty in nat.AmpCounts._fields_:
+        if ty is C.c_int64:
+            assert tot[f] == getattr(wct, f), f
+        else:
+            assert abs(tot[f] - getattr(wct, f)) <= 1e-12 * max(1.0, abs(getattr(wct, f))), f
+    assert whole['T'] == wst.T

@@ -220,6 +220,12 @@ VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 
             'persistent-i8': (2, 4)}
 
 
+# (curve, point, variant) -> measured T where an engine's allclose exit leaves the span of the
+# reference's own reruns (the exit is decided by O(1) elements of 10^6 at
+# these points, and the engines' GEMM accumulation rounding differs from the CPU BLAS's).
+T_DIVERGENCE = {}
+
+
 @pytest.mark.parametrize('variant', sorted(VARIANTS))
 @pytest.mark.parametrize('name,key', VAMP_POINTS)
 def test_vamp_curve_point(device, name, key, variant):
@@ -238,13 +244,11 @@ def test_vamp_curve_point(device, name, key, variant):
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
-    if variant == 'persistent-i8' and (ref['ver'] > 0.5 or ref['T'] >= ent['iterations']):
-        # the opt-in int8x4 arithmetic (31-bit fixed-point GEMM operands, more accurate than the
-        # reference's f32 sums) where the detector has failed (VER > 0.5) or the reference never
-        # met its exit test: its allclose exit is not held to the reference's run there (at
-        # cfg4-QPSK 1 dB seed 0 it stops at 16 where the reference, bf16x3 and f32 run to the
-        # cap) — the goldens hold no rerun evidence for it; VER / SER
-        # are held as everywhere
+    known = T_DIVERGENCE.get((name, key, variant))
+    if known is not None:
+        # a measured exit divergence at a point whose allclose exit is decided by rounding
+        # (DESIGN.md §4 item 5): pinned to the measured T, so any change shows up
+        assert int(got['T']) == known, (int(got['T']), known, ref['T'])
         return
     _check_T(int(got['T']), int(ref['T']), ent['iterations'], ref['ver'], ref.get('T_pert'), ref.get('T_span'))
 
@@ -322,9 +326,9 @@ def _check_T(got, ref, max_iter, ver_ref=0.0, ref_pert=None, ref_span=None):
       span of the evidence the goldens hold for that point (`ref_span`, make_goldens.py g4pp*):
       T of the reference on y scaled by 1, 1 +- 2^-23, 1 +- 2^-22 and on eight seeded element-wise
       one-ulp moves of y; T of the reference with its denoiser's exp moved by a seeded relative
-      +-2^-22 (eight runs); and T of the oracle's restatement with the denoiser in the GPU
-      engines' float32 arithmetic (oracle.block_denoise_f32), which at the 0 dB cfg4-QPSK points
-      keeps the batch mean var in a period-2 cycle in its last bits and never exits.
+      +-2^-22 (eight runs); and T of the reference on the same problem with the positions of
+      every section relabelled (eight seeded permutations: the same arithmetic in other summation
+      orders, make_goldens.py g4pr).  Only runs of the reference itself.
       Else (goldens without the span) the two runs'.
     Without it (goldens that predate the rerun): exact at the end / by 3 iterations, the
     noise-limited range where the detector fails (VER > 0.5), else +-5."""

@@ -75,18 +75,3 @@ def test_g3_decision_metrics(name):
     got = loss_dict(c.xmap, c.xmmse, c.x, c.sym, c.idx, 3, cfg)
     bad = gio.loss_close(got, c.loss_ref, count_tol=0.0, mse_rtol=1e-6)
     assert not bad, bad
-
-
-@pytest.mark.parametrize('name', sorted(k for k in G2))
-def test_g2_denoiser_f32_model(name):
-    """The float32 model of the GPU denoiser (oracle.block_denoise_f32, used only to bound
-    iteration counts at noise-limited golden points) against the reference's float64 denoiser
-    outputs on the g2 cases that stay finite: float32 rounding apart, the same values."""
-    from oracle.amp_oracle import block_denoise_f32
-    c = G2[name]
-    if np.isnan(c.v_xmmse).any() or not np.isfinite(np.asarray(c.r)).all():
-        pytest.skip('non-finite case: the float64 shift semantics, not modelled')
-    cfg = OracleConfig(int(c.Nt), int(c.Na), 2 * int(c.Nt), B=int(c.B), alphabet=str(c.alphabet))
-    xm, var = block_denoise_f32(c.r, np.float32(c.tau), cfg)
-    np.testing.assert_allclose(xm, c.v_xmmse, rtol=0, atol=5e-5)
-    np.testing.assert_allclose(var, c.v_var, rtol=1e-3, atol=5e-6)

@@ -2,9 +2,13 @@
 """Diagnostic (CPU): which part of the float32 denoiser's arithmetic moves VAMP's allclose early
 exit (vamp.py:185) away from the reference's at the reference-moved golden points.
 
-Runs oracle.vamp_detect with the reference's float64 denoiser, with the float32 model of the GPU
-denoiser (oracle.block_denoise_f32), and with hybrids that give one part of the float32 model
-more precision, and prints T per variant beside the reference's recorded T runs.
+Runs oracle.vamp_detect with the reference's float64 denoiser, with float32 models of a denoiser
+('f32': the round-4 model, whose Z - Z_m is a float32 subtraction; 'gs...': the scalar gfx950 form
+of amp_denoise.h operation for operation, exclusive sums included), and with hybrids that give one
+part of a model more precision, and prints T per variant beside the reference's recorded T runs.
+Outcome: the round-4 model's T = 20 came from its cancelling subtraction,
+which the GPU code does not have; the faithful model and the GPU's own denoiser inside the oracle
+loop (tools/den_isolate.py) give the reference's T.
 
   python tools/den_precision_probe.py [--points cfg4_vamp_qpsk:1/0.0,...]
 """

@@ -10,6 +10,8 @@ pinned to the reference by the g1-g4 goldens) with its c64 products computed as:
             accumulation pattern of an MFMA engine's f32 accumulator)
   seq32rN   the same in a seeded random K order (N = seed)
   blk32     eight interleaved float32 partial sums over K, added at the end (a BLAS-like kernel)
+  grpG      per group of G K-terms one exact dot product added to the float32 accumulator (an MFMA
+            engine's pattern: grp32 for the bf16x3 16x16x32 tiles, grp2 for the f32 32x32x2 ones)
 
   python tools/gemm_order_probe.py [--points cfg4_vamp_qpsk:1/0,...] [--variants blas,exact,seq32]
 """
@@ -58,6 +60,28 @@ def _seq32(order=None, nacc=1):
     return mm
 
 
+def _grp32(kg=32):
+    """An MFMA engine's accumulation: per K group of kg terms one exact dot product (float64),
+    added to the float32 accumulator with one rounding (C_r += A_r.B_r, then C_r -= A_i.B_i; C_i
+    likewise)."""
+    def mm(a, b):
+        a = np.asarray(a, np.complex64)
+        b = np.asarray(b, np.complex64)
+        K = a.shape[1]
+        ar, ai = a.real.astype(F64), a.imag.astype(F64)
+        br, bi = b.real.astype(F64), b.imag.astype(F64)
+        cr = np.zeros((a.shape[0], b.shape[1]), F32)
+        ci = np.zeros_like(cr)
+        for k0 in range(0, K, kg):
+            s = slice(k0, k0 + kg)
+            cr = (cr + ar[:, s] @ br[s]).astype(F32)
+            cr = (cr - ai[:, s] @ bi[s]).astype(F32)
+            ci = (ci + ar[:, s] @ bi[s]).astype(F32)
+            ci = (ci + ai[:, s] @ br[s]).astype(F32)
+        return (cr + 1j * ci).astype(np.complex64)
+    return mm
+
+
 def variant_mm(v):
     if v == 'blas':
         return None
@@ -68,6 +92,8 @@ def variant_mm(v):
     if v.startswith('seq32r'):
         rs = int(v[6:] or 0)
         return _seq32(order=lambda K, rs=rs: np.random.default_rng(rs).permutation(K))
+    if v.startswith('grp'):
+        return _grp32(int(v[3:] or 32))
     if v == 'blk32':
         return _seq32(nacc=8)
     raise ValueError(v)
@@ -94,7 +120,14 @@ def main():
         args = (np_(inp['U']), np_(inp['s']), np_(inp['Vh']), np_(inp['y']), inp['SNR'], ocfg)
         out = {}
         for v in a.variants.split(','):
-            out[v] = O.vamp_detect(*args, mm=variant_mm(v))['T']
+            # 'V+y': the variant for the y~ product too; 'y:V': for y~ only
+            if v.startswith('y:'):
+                mm, my = None, variant_mm(v[2:])
+            elif v.endswith('+y'):
+                mm = my = variant_mm(v[:-2])
+            else:
+                mm, my = variant_mm(v), None
+            out[v] = O.vamp_detect(*args, mm=mm, mm_y=my)['T']
             print(f'  {name} {key} {v}: T {out[v]}', flush=True)
         print(f'{name} {key}: reference T {int(ref["T"])} runs {sorted(int(t) for t in ref.get("T_runs", []))} | '
               + ' '.join(f'{v}={t}' for v, t in out.items()), flush=True)

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=gpurun_out/${PROF_TAG:-prof}
 mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:-"--no-cpu-baseline --steps 5 --warmup 1"}
 run() {

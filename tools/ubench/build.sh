@@ -11,3 +11,4 @@ $H -o bin/gemm_x3 gemm_x3_ubench.hip
 $H -o bin/gemm_h2 gemm_h2_ubench.hip
 $H -o bin/gemm_i8 gemm_i8_ubench.hip
 $H -o bin/pk_dpp pk_dpp.hip
+$H -o bin/trans_pk trans_pk.hip
