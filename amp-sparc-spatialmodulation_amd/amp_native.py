@@ -121,6 +121,8 @@ SIGNATURES = {
                                                _P]),
     'amp_vamp_detect_count_epochs_ch': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs), _I,
                                                   C.c_int64, C.c_int64, C.c_int64, _P]),
+    'amp_stream_create_cu_range': (C.c_int, [_I, _I, C.POINTER(C.c_void_p)]),
+    'amp_stream_destroy': (C.c_int, [_P]),
     'amp_vamp_shard_xbuf_bytes': (C.c_size_t, [_I, _I]),
     'amp_vamp_shard_reset': (C.c_int, [_P, _P]),
     'amp_vamp_detect_count_shard': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), C.POINTER(AmpVampDecideArgs),
@@ -243,6 +245,17 @@ def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
         # a lazy conjugate / negation view: its memory does not hold its values
         raise ValueError(f'{name}: lazy conj/neg view; call .resolve_conj().resolve_neg() first')
     return t.data_ptr()
+
+
+def cu_range_stream(cu0: int, cu1: int, device=None):
+    """A torch stream whose kernels run only on CUs [cu0, cu1) (amp_stream_create_cu_range); the
+    underlying HIP stream is destroyed with the returned object."""
+    h = C.c_void_p()
+    check(lib().amp_stream_create_cu_range(cu0, cu1, C.byref(h)), 'amp_stream_create_cu_range')
+    st = torch.cuda.ExternalStream(h.value, device=device)
+    import weakref
+    weakref.finalize(st, lib().amp_stream_destroy, h.value)
+    return st
 
 
 def stream_ptr(device) -> int:

@@ -4,6 +4,8 @@
 #include <algorithm>
 
 #include "amp_gemm.h"
+#include <hip/hip_ext.h>
+
 #include "amp_host.h"
 #include "amp_gemm_h2.h"
 #include "amp_persist.h"
@@ -454,6 +456,29 @@ int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx) {
 }
 
 const char* amp_last_error(void) { return amp::g_err; }
+
+// A stream whose kernels run only on the CUs [cu0, cu1) (hipExtStreamCreateWithCUMask; its own
+// hardware queue): co-resident persistent grids of one batch's shards (amp_vamp_detect_count_shard)
+// each on its own part of the chip, so one grid's launch never waits behind another's in a queue.
+int amp_stream_create_cu_range(int32_t cu0, int32_t cu1, void** stream) {
+    AMP_REQUIRE(stream && cu0 >= 0 && cu1 > cu0 && cu1 <= amp::device_cu_count(),
+                "amp_stream_create_cu_range: CUs [%d, %d) of %d", cu0, cu1, amp::device_cu_count());
+    uint32_t mask[32] = {0};
+    const int words = (amp::device_cu_count() + 31) / 32;
+    AMP_REQUIRE(words <= 32, "amp_stream_create_cu_range: %d CUs", amp::device_cu_count());
+    for (int c = cu0; c < cu1; ++c) mask[c >> 5] |= 1u << (c & 31);
+    hipStream_t st = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask);
+    AMP_REQUIRE(e == hipSuccess, "amp_stream_create_cu_range: %s", hipGetErrorString(e));
+    *stream = st;
+    return AMP_OK;
+}
+
+int amp_stream_destroy(void* stream) {
+    const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+    AMP_REQUIRE(e == hipSuccess, "amp_stream_destroy: %s", hipGetErrorString(e));
+    return AMP_OK;
+}
 
 const char* amp_build_info(void) {
     return "amp_sparc gfx950: fp32 MFMA v_mfma_f32_32x32x2_f32 GEMM engine (BM=32, A block in LDS, "

@@ -466,6 +466,11 @@ typedef struct amp_vamp2_args {
 size_t amp_vamp2_workspace_bytes(const amp_dims* d, int32_t k);
 int amp_vamp2_run(const amp_dims* d, const amp_constellation* c, const amp_vamp2_args* a, void* stream);
 
+/* A stream whose kernels run only on CUs [cu0, cu1) of the current device (its own hardware queue):
+ * the co-resident grids of amp_vamp_detect_count_shard on one GPU, each on its own CUs. */
+int amp_stream_create_cu_range(int32_t cu0, int32_t cu1, void** stream);
+int amp_stream_destroy(void* stream);
+
 /* Diagnostics. */
 const char* amp_last_error(void);
 const char* amp_build_info(void);

@@ -223,7 +223,21 @@ VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 
 # (curve, point, variant) -> measured T where an engine's allclose exit leaves the span of the
 # reference's own reruns (the exit is decided by O(1) elements of 10^6 at
 # these points, and the engines' GEMM accumulation rounding differs from the CPU BLAS's).
-T_DIVERGENCE = {}
+# Measured on MI355X (gpurun_out r5c8, every other g4 point and variant inside its span):
+# * cfg4-QPSK 0 dB seed 1: the reference stops at 12 (its 29 reruns: 12-17); every engine, the
+#   f32-MFMA and launch forms included, runs to the cap (the GEMM
+#   accumulation error, not the denoiser, decides it; the oracle with float32-accumulated GEMMs
+#   also reaches the cap at this point's seed-0 neighbour, tools/gemm_order_probe.py);
+# * the opt-in int8x4 form at three 1 dB points where the reference runs to the cap (its reruns:
+#   20, 18-20 and 20) stops earlier: 18, 16, 14.  VER / SER stay within 1e-3 at all of them.
+T_DIVERGENCE = {
+    ('cfg4_vamp_qpsk', '1/0', 'launches'): 20,
+    ('cfg4_vamp_qpsk', '1/0', 'persistent'): 20,
+    ('cfg4_vamp_qpsk', '1/0', 'persistent-f32'): 20,
+    ('cfg4_vamp_qpsk', '0/1', 'persistent-i8'): 18,
+    ('cfg4_vamp_qpsk', '1/1', 'persistent-i8'): 16,
+    ('cfg4_vamp_qpsk', '2/1', 'persistent-i8'): 14,
+}
 
 
 @pytest.mark.parametrize('variant', sorted(VARIANTS))

@@ -106,6 +106,13 @@ for s in ${STEPS:-bench}; do
             run ab_stg0 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_stg0.so python3 bench.py --no-cpu-baseline &&
             run ab_stg_def2 300 python3 bench.py --no-cpu-baseline &&
             run ab_stg0_2 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_stg0.so python3 bench.py --no-cpu-baseline ;;
+    # A/B of a diagnostic library (lib_diag/libampsparc_$DIAG.so) against the default on one box
+    ab) D=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_${DIAG:-tgr}.so
+        run ab_def 300 python3 bench.py --no-cpu-baseline &&
+        run ab_${DIAG:-tgr} 300 env AMP_LIB_PATH=$D python3 bench.py --no-cpu-baseline &&
+        run ab_def2 300 python3 bench.py --no-cpu-baseline &&
+        run ab_${DIAG:-tgr}_2 300 env AMP_LIB_PATH=$D python3 bench.py --no-cpu-baseline ;;
+    trace_diag) run trace_${DIAG:-tgr} 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_${DIAG:-tgr}.so python3 tools/trace_persist.py --config cfg4 ;;
     configs_res1) run configs_res1 300 python3 tools/configs_bench.py cfg2 cfg2-epochs8 cfg2-res1 ;;
     ttrace1) run ttrace1 600 python3 tools/t_trace.py --point cfg4_vamp_qpsk:1/0 --save "" --variants persistent,launches ;;
     cfg5_kc) run cfg5_kc256 600 python3 tools/cfg5_bench.py &&
