@@ -247,14 +247,22 @@ def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
     return t.data_ptr()
 
 
+_CU_STREAMS = {}
+
+
 def cu_range_stream(cu0: int, cu1: int, device=None):
-    """A torch stream whose kernels run only on CUs [cu0, cu1) (amp_stream_create_cu_range); the
-    underlying HIP stream is destroyed with the returned object."""
-    h = C.c_void_p()
-    check(lib().amp_stream_create_cu_range(cu0, cu1, C.byref(h)), 'amp_stream_create_cu_range')
-    st = torch.cuda.ExternalStream(h.value, device=device)
-    import weakref
-    weakref.finalize(st, lib().amp_stream_destroy, h.value)
+    """A torch stream whose kernels run only on CUs [cu0, cu1) (amp_stream_create_cu_range), one per
+    (range, device) for the life of the process: torch's caching allocator remembers the streams
+    its blocks were used on and queries them when the blocks are freed (down to interpreter exit),
+    so the HIP stream is never destroyed under it."""
+    dev = torch.device('cuda', torch.cuda.current_device()) if device is None else torch.device(device)
+    key = (int(cu0), int(cu1), dev.index)
+    st = _CU_STREAMS.get(key)
+    if st is None:
+        h = C.c_void_p()
+        with torch.cuda.device(dev):
+            check(lib().amp_stream_create_cu_range(cu0, cu1, C.byref(h)), 'amp_stream_create_cu_range')
+        st = _CU_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=dev)
     return st
 
 

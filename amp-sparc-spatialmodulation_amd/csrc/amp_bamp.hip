@@ -223,21 +223,44 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
         gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds,
                                        bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
-    for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
+    // every global load of this thread's elements before any store (the z / invu / s stores may
+    // alias the next element's loads as far as the compiler knows: one memory latency per element
+    // otherwise); each element reads and writes only its own z and invu
+    constexpr int IT = GBM * 64 / AMP_WG;
+    float2 yv[IT], zv[IT];
+    float vv[IT], iuo[IT];
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
         const int rho = e >> 6, cp = e & 63;           // complex column pair
+        const int row = row0 + rho, i = (col0 >> 1) + cp;
+        yv[u] = zv[u] = make_float2(0.f, 0.f);
+        vv[u] = iuo[u] = 0.f;
+        if (row < P.B && i < P.n) {
+            const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
+            yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
+            zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
+            vv[u] = P.v[o];
+            iuo[u] = P.invu[o];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
+        const int rho = e >> 6, cp = e & 63;
         const int row = row0 + rho, i = (col0 >> 1) + cp;
         if (row < P.B && i < P.n) {
             const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
             const float hr = lds[rho * C::LDC + 2 * cp], hi = lds[rho * C::LDC + 2 * cp + 1];
-            const float yr = P.y[oc], yi = P.y[oc + 1];
-            const float vi = P.v[o], iu_old = P.invu[o];
-            const float zr = hr - (vi * (yr - P.z[oc])) * iu_old;
-            const float zi = hi - (vi * (yi - P.z[oc + 1])) * iu_old;
-            const float u = vi + P.sigma2;
-            const float iu = 1.0f / u;
-            P.z[oc] = zr; P.z[oc + 1] = zi;
+            const float yr = yv[u].x, yi = yv[u].y;
+            const float vi = vv[u], iu_old = iuo[u];
+            const float zr = hr - (vi * (yr - zv[u].x)) * iu_old;
+            const float zi = hi - (vi * (yi - zv[u].y)) * iu_old;
+            const float uu = vi + P.sigma2;
+            const float iu = 1.0f / uu;
+            *reinterpret_cast<float2*>(P.z + oc) = make_float2(zr, zi);
             P.invu[o] = iu;
-            P.s[oc] = (yr - zr) * iu; P.s[oc + 1] = (yi - zi) * iu;
+            *reinterpret_cast<float2*>(P.s + oc) = make_float2((yr - zr) * iu, (yi - zi) * iu);
         }
     }
 }
@@ -265,8 +288,8 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
 
 struct BampDenoisePolicy {
     const float* tile;
-    const float* cov;
-    int ldc, spr, M, N, row0, colc0;
+    const float* itile;   // LDS [32][ldi]: 1 / (cov / 2) of the tile's positions (bamp_kb2's xmap pass)
+    int ldc, ldi, spr, M, N, row0, colc0;
     float* xm;
     float* var_new;
     const float* var_prev;
@@ -277,7 +300,7 @@ struct BampDenoisePolicy {
         const int rho = sec / spr, sj = sec - rho * spr;
         const float2 v = *reinterpret_cast<const float2*>(tile + rho * ldc + 2 * (sj * M + m));
         rr = v.x; ri = v.y;
-        it = 1.0f / (cov[(size_t)(row0 + rho) * N + colc0 + sj * M + m] * 0.5f);   // tau = cov/2 (bamp.py:68)
+        it = itile[rho * ldi + sj * M + m];   // 1 / tau, tau = cov / 2 (bamp.py:68)
     }
     __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
         const int rho = sec / spr, sj = sec - rho * spr;
@@ -311,19 +334,37 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
         gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WHH, P.kapB2, row0, col0, lds,
                                       bkb(P, 3, tile.cb), bke(P, 3, tile.cb));
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
-    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
-        const int rho = e / BN, cc = e % BN;
-        if (rho < nrows && cc < ncols) {
-            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
-            const float cv = P.cov[(size_t)(row0 + rho) * P.N + ((col0 + cc) >> 1)];
-            const float xp = P.xm[o] + cv * lds[rho * C::LDC + cc];
-            P.xmap[o] = xp;
-            lds[rho * C::LDC + cc] = xp;
+    float* sit = lds + C::CTILE_FLOATS + 2048;   // past the partial-store scratch
+    {
+        // the loads of this thread's elements before the xmap stores (which may alias them as far
+        // as the compiler knows)
+        constexpr int IT = GBM * BN / AMP_WG;
+        static_assert(C::CTILE_FLOATS + 2048 + GBM * (BN / 2) <= C::A_FLOATS, "1 / tau tile");
+        float xv[IT], cvv[IT];
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
+            const bool ok = rho < nrows && cc < ncols;
+            xv[u] = ok ? P.xm[(size_t)(row0 + rho) * twoN + col0 + cc] : 0.f;
+            cvv[u] = ok ? P.cov[(size_t)(row0 + rho) * P.N + ((col0 + cc) >> 1)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
+            if (rho < nrows && cc < ncols) {
+                const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+                const float xp = xv[u] + cvv[u] * lds[rho * C::LDC + cc];
+                P.xmap[o] = xp;
+                lds[rho * C::LDC + cc] = xp;
+                // the denoiser's 1 / tau of this position, read from LDS there instead of a global
+                // load per position inside its loop (the same float32 operations)
+                if ((cc & 1) == 0) sit[rho * (BN / 2) + (cc >> 1)] = 1.0f / (cvv[u] * 0.5f);
+            }
         }
     }
     __syncthreads();
     BampDenoisePolicy pol;
-    pol.tile = lds; pol.cov = P.cov; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.L = P.L;
+    pol.tile = lds; pol.itile = sit; pol.ldi = BN / 2; pol.ldc = C::LDC; pol.M = P.M; pol.N = P.N; pol.L = P.L;
     pol.spr = (ncols / 2) / P.M; pol.row0 = row0; pol.colc0 = col0 / 2;
     pol.xm = P.xm; pol.var_new = bvar(P, t); pol.var_prev = bvar(P, t + 1); pol.secmax = P.secmax; pol.secabs = P.secabs;
     PartAcc pa;

@@ -200,20 +200,13 @@ __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast
 // accumulator that is then added to the running one (one f32 rounding per group at the result's
 // magnitude instead of twelve; DESIGN.md §4 item 5: the accumulation error, not the product split,
 // is what moves the allclose exit at the rounding-decided golden points).
-// TGR (R = 1, NT > 1): the ring is refilled tile by tile — tile t's six next-group pieces are
-// issued right after tile t's 24 MFMAs, so they have the other tiles' MFMAs (and the partner
-// wave's) to land, where the group-wise refill left each group's loads only the partner's.
 #ifndef AMP_X3_GACC
 #define AMP_X3_GACC 0
 #endif
-#ifndef AMP_X3_TGR
-#define AMP_X3_TGR 0
-#endif
-template <int NT, int G, int R = 1, bool PIN = false, bool GACC = AMP_X3_GACC, bool TGR = AMP_X3_TGR>
+template <int NT, int G, int R = 1, bool PIN = false, bool GACC = AMP_X3_GACC>
 __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
                                         f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
     constexpr int RR = G < R ? G : R;
-    constexpr bool TILE_REFILL = TGR && RR == 1 && NT > 1;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int t = 0; t < NT; ++t) { cr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; ci[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -282,17 +275,9 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
 #undef AMP_MF
             if (GACC && g > 0) { cr[t] += gr; ci[t] += gi; }
             else { cr[t] = gr; ci[t] = gi; }
-            if constexpr (TILE_REFILL) {
-                if (g + 1 < G) {
-#pragma unroll
-                    for (int f = 0; f < 6; ++f)
-                        ring[0][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + 1) * 6 + f) * 1024, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
         }
         if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
-        if (!TILE_REFILL && g + RR < G) {
+        if (g + RR < G) {
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll

@@ -57,21 +57,43 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
         }
         __syncthreads();
     }
-    for (int e = threadIdx.x; e < GBM * 64; e += AMP_WG) {
+    // Every global load of this thread's elements is issued before any store: the stores to z / s
+    // may alias the next element's loads as far as the compiler knows, and a load-compute-store loop
+    // waited a full memory latency per element (each element reads and writes only its own z).
+    constexpr int IT = GBM * 64 / AMP_WG;
+    float2 yv[IT], zv[IT];
+    float po[IT];
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
+        const int rho = e >> 6, cp = e & 63;
+        const int row = row0 + rho, i = (col0 >> 1) + cp;
+        yv[u] = zv[u] = make_float2(0.f, 0.f);
+        po[u] = 1.f;
+        if (row < P.B && i < P.n) {
+            const size_t oc = (size_t)row * twon + 2 * i;
+            yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
+            zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
+            po[u] = phi_old[(size_t)row * P.Lout + i / P.Nr];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
         const int rho = e >> 6, cp = e & 63;
         const int row = row0 + rho, i = (col0 >> 1) + cp;
         if (row < P.B && i < P.n) {
             const int lo = i / P.Nr;
             const float gma = per_block ? sg[rho * nlo + lo - lo0] : scamp_gamma(P, psi + (size_t)row * P.Lin, lo);
-            const float b = gma / phi_old[(size_t)row * P.Lout + lo];
+            const float b = gma / po[u];
             const size_t oc = (size_t)row * twon + 2 * i;
             const float ar = lds[rho * C::LDC + 2 * cp], ai = lds[rho * C::LDC + 2 * cp + 1];
-            const float zr = (P.y[oc] - ar) + b * P.z[oc];
-            const float zi = (P.y[oc + 1] - ai) + b * P.z[oc + 1];
+            const float zr = (yv[u].x - ar) + b * zv[u].x;
+            const float zi = (yv[u].y - ai) + b * zv[u].y;
             const float ph = P.sigma2 + gma;
             const float iph = 1.0f / ph;
-            P.z[oc] = zr; P.z[oc + 1] = zi;
-            P.s[oc] = zr * iph; P.s[oc + 1] = zi * iph;
+            *reinterpret_cast<float2*>(P.z + oc) = make_float2(zr, zi);
+            *reinterpret_cast<float2*>(P.s + oc) = make_float2(zr * iph, zi * iph);
             if (i % P.Nr == 0) phi_new[(size_t)row * P.Lout + lo] = ph;
         }
     }
@@ -153,14 +175,26 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
         tau_t[e] = tv;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
-        const int rho = e / BN, cc = e % BN;
-        if (rho < nrows && cc < ncols) {
-            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
-            const float tv = tau_t[rho * ntc + ((col0 + cc) >> 1) / P.Nt - lc0];
-            const float xp = P.xm[o] + tv * lds[rho * C::LDC + cc];
-            P.xmap[o] = xp;
-            lds[rho * C::LDC + cc] = xp;
+    {
+        // xmmse of every element of this thread first (the xmap stores may alias them as far as
+        // the compiler knows: one load latency per element otherwise)
+        constexpr int IT = GBM * BN / AMP_WG;
+        float xv[IT];
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
+            xv[u] = (rho < nrows && cc < ncols) ? P.xm[(size_t)(row0 + rho) * twoN + col0 + cc] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
+            if (rho < nrows && cc < ncols) {
+                const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+                const float tv = tau_t[rho * ntc + ((col0 + cc) >> 1) / P.Nt - lc0];
+                const float xp = xv[u] + tv * lds[rho * C::LDC + cc];
+                P.xmap[o] = xp;
+                lds[rho * C::LDC + cc] = xp;
+            }
         }
     }
     __syncthreads();
