@@ -125,7 +125,10 @@ typedef struct amp_vamp_args {
  *        its row's / column's maximum (>= 24 bits down to 2^-7 of it), dropped terms < 2^-30 of
  *        (row max . column max); on the cfg4 GEMM 23x closer to a float64 sum than an f32 sum
  *        (amp_persist.h gemm_i8); a non-finite A row gives a NaN result row; same shape
- *        constraints as X3, one workgroup per CU;
+ *        constraints as X3, one workgroup per CU.  Its different rounding moves the allclose
+ *        early exit (vamp.py:185) where that exit is decided by rounding: at three cfg4-QPSK
+ *        1 dB golden points it stops at 18 / 16 / 14 iterations where the reference runs to 20
+ *        (VER / SER within 1e-3; tests/test_gpu_vamp.py T_DIVERGENCE);
  *  AUTO  X3 where the planes fit, else F32 (environment AMP_VAMP_GEMM=f32 keeps F32,
  *        AMP_VAMP_GEMM=h2 picks H2). */
 #define AMP_GEMM_AUTO 0
