@@ -61,7 +61,7 @@ class AmpVamp2Args(C.Structure):
 
 class AmpVampDecideArgs(C.Structure):
     _fields_ = [('x', C.c_void_p), ('sym', C.c_void_p), ('idx', C.c_void_p), ('ibits_trunc', C.c_int32),
-                ('pad', C.c_int32), ('counts', C.c_void_p)]
+                ('pad', C.c_int32), ('counts', C.c_void_p), ('host_record', C.c_void_p)]
 
 
 class AmpVampShard(C.Structure):
@@ -245,6 +245,13 @@ def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
         # a lazy conjugate / negation view: its memory does not hold its values
         raise ValueError(f'{name}: lazy conj/neg view; call .resolve_conj().resolve_neg() first')
     return t.data_ptr()
+
+
+def fold_launch() -> bool:
+    """AMP_FOLD_LAUNCH=1 (A/B runs): the persistent engines leave the counter fold to a launch of
+    its own and do not write the host record (amp_host.h fold_in_kernel); read per call, as there.
+    AMP_HOST_RECORD=0 (A/B runs): the record is copied back as for the other engines."""
+    return os.environ.get('AMP_FOLD_LAUNCH') == '1' or os.environ.get('AMP_HOST_RECORD') == '0'
 
 
 _CU_STREAMS = {}

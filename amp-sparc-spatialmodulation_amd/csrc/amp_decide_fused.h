@@ -6,6 +6,7 @@
 #pragma once
 
 #include "amp_decide.h"
+#include "amp_persist.h"
 
 namespace amp {
 
@@ -18,9 +19,14 @@ namespace amp {
 // scr: >= 16 * sizeof(DecWG) bytes.
 // row0: first row of the concatenated [E * B] tensors; lrow0: the same trial within its epoch
 // (the flat indices and channel uses the counters compare are per batch, loss.py:105-179).
-template <int PWG, int KK, class PK>
+// PUB with a nonzero pub_tag (the persistent engines, which fold the records themselves:
+// dec_fold_gather): the record is published as 13 tagged 16-byte granules of 8 bytes each (sc1
+// write-through stores, like the per-iteration partials, amp_persist.h part_publish) at
+// P.dwg + 256 blockIdx.x bytes; else stored plainly for vamp_decide_fold.
+template <int PWG, int KK, bool PUB = false, class PK>
 __device__ __forceinline__ void decide_epilogue(const PK& P, const DecConst& dc, const float* sR, const float* sX, int ldr, int row0,
-                                int lrow0, int nrows, float* sT, void* lab_lds, int lab_cap, void* scr) {
+                                int lrow0, int nrows, float* sT, void* lab_lds, int lab_cap, void* scr,
+                                unsigned pub_tag = 0) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int M = P.M, L = P.L, N = P.N;
     const int S = nrows * L;
@@ -130,8 +136,116 @@ __device__ __forceinline__ void decide_epilogue(const PK& P, const DecConst& dc,
             decpart_add(o.p, sw[v].p);
             o.ver += sw[v].ver; o.verf += sw[v].verf; o.verm += sw[v].verm; o.verL += sw[v].verL; o.fer += sw[v].fer;
         }
-        P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
-                                 // an agent-scope release writes back the L2 and cost ~90 us)
+        if (PUB && pub_tag != 0u) {
+            const unsigned long long v[13] = {
+                (unsigned long long)o.p.ier, (unsigned long long)o.p.ser, (unsigned long long)o.p.iber,
+                (unsigned long long)o.p.sber, (unsigned long long)__double_as_longlong(o.p.mse),
+                (unsigned long long)__double_as_longlong(o.p.msef), (unsigned long long)__double_as_longlong(o.p.msem),
+                (unsigned long long)__double_as_longlong(o.p.mseL), (unsigned long long)o.ver,
+                (unsigned long long)o.verf, (unsigned long long)o.verm, (unsigned long long)o.verL,
+                (unsigned long long)o.fer};
+            const __amdgpu_buffer_rsrc_t rs = gran_rsrc(P.dwg, (unsigned)(gridDim.x * 256u));
+#pragma unroll
+            for (int j = 0; j < 13; ++j) {
+                const u32x4 g = {(unsigned)v[j], (unsigned)(v[j] >> 32), (unsigned)j, pub_tag};
+                __builtin_amdgcn_raw_buffer_store_b128(g, rs, (int)(blockIdx.x * 256u + 16u * j), 0, 16);   // sc1
+            }
+        } else {
+            P.dwg[blockIdx.x] = o;   // folded by vamp_decide_fold after this launch (no cross-XCD fence here:
+                                     // an agent-scope release writes back the L2 and cost ~90 us)
+        }
+    }
+}
+
+// The fold of the n published records of workgroups [base, base + n) of this launch (one epoch),
+// by waves 0-3 of the calling workgroup, in vamp_decide_fold's order (thread i < 256 holds record i,
+// a 64-lane sum per wave, thread 0 adds the four wave sums in order: the same bits).  Each thread
+// polls its record's granules until all 13 carry `tag` (a workgroup that has not yet reached its
+// epilogue); a bounded spin (2 s).  Thread 0 writes *out.  Returns false (every thread) on a timeout.
+template <class PK>
+__device__ bool dec_fold_gather(const PK& P, int base, int n, unsigned tag, amp_counts* out, void* lds, int* s_flag) {
+    const int tid = threadIdx.x;
+    DecWG a;
+    a.p = decpart_zero();
+    a.ver = a.verf = a.verm = a.verL = a.fer = 0;
+    if (tid == 0) *s_flag = 1;
+    __syncthreads();
+    if (tid < 256) {
+        if (tid < n) {
+            const __amdgpu_buffer_rsrc_t rs = gran_rsrc(P.dwg, (unsigned)((base + n) * 256));
+            const int off = (base + tid) * 256;
+            u32x4 g[13];
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                bool all = true;
+#pragma unroll
+                for (int j = 0; j < 13; ++j) {
+                    g[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * j, 0, 16);
+                    all &= g[j].w == tag;
+                }
+                if (all) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {   // 2 s at 100 MHz
+                    *s_flag = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            auto u64 = [&](int j) { return ((unsigned long long)g[j].y << 32) | g[j].x; };
+            DecWG q;
+            q.p.ier = (long long)u64(0); q.p.ser = (long long)u64(1); q.p.iber = (long long)u64(2);
+            q.p.sber = (long long)u64(3);
+            q.p.mse = __longlong_as_double((long long)u64(4)); q.p.msef = __longlong_as_double((long long)u64(5));
+            q.p.msem = __longlong_as_double((long long)u64(6)); q.p.mseL = __longlong_as_double((long long)u64(7));
+            q.ver = (long long)u64(8); q.verf = (long long)u64(9); q.verm = (long long)u64(10);
+            q.verL = (long long)u64(11); q.fer = (long long)u64(12);
+            decpart_add(a.p, q.p);
+            a.ver += q.ver; a.verf += q.verf; a.verm += q.verm; a.verL += q.verL; a.fer += q.fer;
+        }
+        a.p.ier = group_sum(a.p.ier, 64); a.p.ser = group_sum(a.p.ser, 64);
+        a.p.iber = group_sum(a.p.iber, 64); a.p.sber = group_sum(a.p.sber, 64);
+        a.p.mse = group_sum(a.p.mse, 64); a.p.msef = group_sum(a.p.msef, 64);
+        a.p.msem = group_sum(a.p.msem, 64); a.p.mseL = group_sum(a.p.mseL, 64);
+        a.ver = group_sum(a.ver, 64); a.verf = group_sum(a.verf, 64); a.verm = group_sum(a.verm, 64);
+        a.verL = group_sum(a.verL, 64); a.fer = group_sum(a.fer, 64);
+    }
+    DecWG* sw = reinterpret_cast<DecWG*>(lds);
+    __syncthreads();
+    if (tid < 256 && (tid & 63) == 0) sw[tid >> 6] = a;
+    __syncthreads();
+    if (tid == 0) {
+        amp_counts c;
+        c.ier = c.ser = c.iber = c.sber = 0;
+        c.ver = c.verf = c.verm = c.verL = c.fer = 0;
+        c.mse = c.msef = c.msem = c.mseL = 0.0;
+        for (int v = 0; v < 4; ++v) {
+            const DecWG& q = sw[v];
+            c.ier += q.p.ier; c.ser += q.p.ser; c.iber += q.p.iber; c.sber += q.p.sber;
+            c.mse += q.p.mse; c.msef += q.p.msef; c.msem += q.p.msem; c.mseL += q.p.mseL;
+            c.ver += q.ver; c.verf += q.verf; c.verm += q.verm; c.verL += q.verL; c.fer += q.fer;
+        }
+        *out = c;
+    }
+    __syncthreads();
+    const bool ok = *s_flag != 0;
+    __syncthreads();
+    return ok;
+}
+
+// A record (status, counters) written to page-locked host memory (the caller's
+// amp_vamp_decide_args.host_record): status at byte 0, counters at byte 64, as nine 16-byte
+// non-temporal stores by thread 0 (the buffer is host memory the device maps uncached; the
+// stream's completion signal follows the kernel's stores).
+__device__ __forceinline__ void host_record_write(unsigned char* rec, const amp_status& s, const amp_counts& c) {
+    u32x4 w[11];
+    static_assert(sizeof(amp_status) == 32 && sizeof(amp_counts) == 104, "record layout");
+    __builtin_memcpy(&w[0], &s, 32);
+    w[2] = w[3] = u32x4{0u, 0u, 0u, 0u};
+    w[10] = u32x4{0u, 0u, 0u, 0u};
+    __builtin_memcpy(&w[4], &c, 104);
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+        if (i == 2 || i == 3) continue;
+        __builtin_nontemporal_store(w[i], reinterpret_cast<u32x4*>(rec) + i);
     }
 }
 

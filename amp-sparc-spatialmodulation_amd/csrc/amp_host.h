@@ -217,6 +217,15 @@ struct CWeightJob {
 // Up to CW_MAX_JOBS jobs in ONE launch (blockIdx.y = job; the side-by-side epochs with a channel
 // each build three per epoch); the same launch zeroes `nzero` words at `zero` (or none).
 constexpr int CW_MAX_JOBS = 24;
+
+// The persistent engines fold the fused decision's per-workgroup counter records inside their own
+// launch and write the host record themselves (amp_decide_fused.h); AMP_FOLD_LAUNCH=1 keeps the
+// separate vamp_decide_fold launch and leaves the host record alone (A/B runs; the Python layer
+// then copies the record back, vamp.py LazyResult).  Read per call.
+inline bool fold_in_kernel() {
+    const char* e = getenv("AMP_FOLD_LAUNCH");
+    return !(e && e[0] == '1');
+}
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);
 int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* wt, int kap, int ncp,
                       hipStream_t st);

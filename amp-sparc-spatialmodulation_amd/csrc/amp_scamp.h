@@ -75,8 +75,11 @@ struct ScampK {
     const float2* xtrue;   // [B][N] transmitted x
     const long long* sym;  // [B*L] gray labels
     const long long* idx;  // [B*L] flat nonzero indices
-    DecWG* dwg;            // [nwg] per-workgroup records
+    DecWG* dwg;            // per-workgroup records: [nwg] x 256 B of tagged granules (folded in the
+                           // persistent kernel, amp_decide_fused.h dec_fold_gather)
     amp_counts* counts;    // out
+    unsigned char* host_rec;   // optional page-locked host record (amp_vamp_decide_args.host_record)
+    int fold_in;               // the persistent kernel folds the records itself (else vamp_decide_fold)
     unsigned long long* trace;   // diagnostic phase stamps (amp_scamp_persist_trace), else null
     // launch engine: rcnt[1] is scamp_fix_psi_fin's arrival counter (zeroed by scamp_init_kernel)
     unsigned* rcnt;
@@ -142,7 +145,7 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.bandA = cv.take<int>((size_t)2 * (P.ncpA / 128));
     w.bandB = cv.take<int>((size_t)2 * (P.ncpB / P.bn));
     w.xs = cv.take<XState>(1);
-    w.dwg = cv.take<DecWG>((size_t)nwg);
+    w.dwg = cv.take<DecWG>((size_t)2 * nwg);   // 256 B of granules per workgroup
     w.bytes = cv.off;
     return w;
 }

@@ -716,6 +716,8 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.Wq1 = w.Wq1; P.Wq2 = w.Wq2; P.pparts = w.pparts; P.pxch = w.pxch; P.pbar = w.pbar;
     P.Wx1 = w.Wx1; P.Wx2 = w.Wx2;
     P.dec_on = 0; P.ibits = 0; P.xtrue = nullptr; P.sym = nullptr; P.idx = nullptr; P.counts = nullptr;
+    P.host_rec = nullptr;
+    P.fold_in = fold_in_kernel() ? 1 : 0;
     P.dwg = w.dwg;
     P.trace = nullptr;
     P.rcnt = w.pbar + 8;
@@ -917,10 +919,12 @@ int amp_scamp_detect_count(const amp_dims* d, const amp_constellation* c, const 
     P.sym = (const long long*)dec->sym;
     P.idx = (const long long*)dec->idx;
     P.counts = (amp_counts*)dec->counts;
+    P.host_rec = P.fold_in ? (unsigned char*)dec->host_record : nullptr;
     DecConst dc = to_decconst(c);
     static_cast<Const64&>(dc) = c64;
-    if ((rc = scamp_persist_launch(P, dc, st))) return rc;
-    hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);
+    if ((rc = scamp_persist_launch(P, dc, st))) return rc;   // the counter records folded inside it ...
+    if (P.fold_in) return AMP_OK;
+    hipLaunchKernelGGL(vamp_decide_fold, dim3(1), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg, P.counts);   // ... or here
     AMP_LAUNCH_CHECK("vamp_decide_fold (scamp)");
     return AMP_OK;
 }

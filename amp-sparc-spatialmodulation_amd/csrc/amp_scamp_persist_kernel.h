@@ -539,20 +539,31 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
         P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldx + col];
     }
     for (int e = tid; e < nrows * Lin; e += PWG) P.psi0[(size_t)row0 * Lin + e] = psi_last[e];
-    if (wg == 0 && tid == 0) {
-        amp_status s;
-        s.T = stopped ? T : P.max_iter;
-        s.nan_state = aborted ? -1 : (fixed != 0 ? 1 : 0);
-        s.stopped = stopped;
-        s.pad = 0;
-        s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
-        *P.status = s;
-    }
+    amp_status s;
+    s.T = stopped ? T : P.max_iter;
+    s.nan_state = aborted ? -1 : (fixed != 0 ? 1 : 0);
+    s.stopped = stopped;
+    s.pad = 0;
+    s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
+    if (wg == 0 && tid == 0) *P.status = s;
     if (P.dec_on) {
         // fused MAP decision + counters on xmap (scamp.py:107 -> loss.py:67-179): the s / plane region
-        // holds the truth rows (n >= N: rows of ldx floats fit), the z region the labels
+        // holds the truth rows (n >= N: rows of ldx floats fit), the z region the labels; workgroup 0
+        // folds every workgroup's record from its tagged granules (no fold launch)
         __syncthreads();
-        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldx, row0, row0, nrows, sS, sZ, 4 * SPB * Y.ldz, scr);
+        const unsigned dtag = P.fold_in ? P.gen * (unsigned)(P.max_iter + 1) + (unsigned)P.max_iter + 1u : 0u;
+        decide_epilogue<PWG, KK, true>(P, dc, sR, sX, ldx, row0, row0, nrows, sS, sZ, 4 * SPB * Y.ldz, scr, dtag);
+        if (P.fold_in && wg == 0) {
+            __syncthreads();
+            const bool ok = dec_fold_gather(P, 0, nwg, dtag, P.counts, scr, &s_flag);
+            if (tid == 0) {
+                if (!ok) {   // a workgroup never published: results invalid
+                    s.nan_state = -1;
+                    *P.status = s;
+                }
+                if (P.host_rec) host_record_write(P.host_rec, s, *P.counts);
+            }
+        }
     }
 }
 

@@ -55,7 +55,10 @@ struct VampK {
     const float2* xtrue;        // [B][N] transmitted x
     const long long* sym;       // [B*L] gray labels
     const long long* idx;       // [B*L] flat nonzero indices
-    DecWG* dwg;                 // [nwg] per-workgroup records
+    DecWG* dwg;                 // per-workgroup records: [nwg] x 256 B of tagged granules (the
+                                // persistent engine folds them itself, amp_decide_fused.h)
+    unsigned char* host_rec;    // optional page-locked host record (amp_vamp_decide_args.host_record)
+    int fold_in;                // the persistent kernel folds the records itself (else vamp_decide_fold)
     amp_counts* counts;         // out
     unsigned long long* trace;   // diagnostic phase stamps (amp_vamp_persist_trace), else null
     int x3;                      // persistent engine GEMMs: 0 f32 MFMA, 1 bf16x3, 2 fp16x2 (Wx1 / Wx2)
@@ -127,7 +130,7 @@ static VampWs vamp_carve(const amp_dims* d, int k, int max_iter, void* base, int
     w.pxch = cv.take<double>((size_t)max_iter * nwg * 4);
     w.pbar = cv.take<unsigned>(PBAR_WORDS);                  // barrier words (zeroed per launch); the
     w.pparts = cv.take<Partial>((size_t)max_iter * nwg);     // granules carry generation tags
-    w.dwg = cv.take<DecWG>((size_t)nwg);
+    w.dwg = cv.take<DecWG>((size_t)2 * nwg);              // 256 B of granules per workgroup
     w.xs = cv.take<XState>(1);
     w.bytes = cv.off;
     return w;

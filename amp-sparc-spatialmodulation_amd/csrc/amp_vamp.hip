@@ -474,6 +474,8 @@ static int vamp_setup(const amp_dims* d, const amp_constellation* c, const amp_v
     P.gen = 0;
     P.ytil_in_kernel = 0;
     P.dec_on = 0; P.ibits = 0; P.xtrue = nullptr; P.sym = nullptr; P.idx = nullptr; P.counts = nullptr;
+    P.host_rec = nullptr;
+    P.fold_in = fold_in_kernel() ? 1 : 0;
     P.dwg = w.dwg;
     P.y = (const float*)a->y;
     P.trace = nullptr;
@@ -841,6 +843,7 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
     P.sym = (const long long*)dec->sym;
     P.idx = (const long long*)dec->idx;
     P.counts = (amp_counts*)dec->counts;
+    P.host_rec = P.fold_in ? (unsigned char*)dec->host_record : nullptr;
     return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 
@@ -877,6 +880,7 @@ int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32
     out[1] = (uint64_t)((char*)w.pxch - base);
     out[2] = (uint64_t)((char*)w.pbar - base);
     out[3] = (uint64_t)((char*)w.dwg - base);
+    out[4] = (uint64_t)((char*)w.ytil - base);
     return AMP_OK;
 }
 
@@ -927,6 +931,7 @@ static int detect_count_epochs_impl(const amp_dims* d, const amp_constellation* 
     P.sym = (const long long*)dec->sym;
     P.idx = (const long long*)dec->idx;
     P.counts = (amp_counts*)dec->counts;
+    P.host_rec = P.fold_in ? (unsigned char*)dec->host_record : nullptr;
     return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 
@@ -1018,6 +1023,7 @@ int amp_vamp_detect_count_shard(const amp_dims* d, const amp_constellation* c, c
     P.sym = (const long long*)dec->sym;
     P.idx = (const long long*)dec->idx;
     P.counts = (amp_counts*)dec->counts;
+    P.host_rec = P.fold_in ? (unsigned char*)dec->host_record : nullptr;
     return vamp_persist_launch(P, c64, to_decconst(c), st, ncu);
 }
 

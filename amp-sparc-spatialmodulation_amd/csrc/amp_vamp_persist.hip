@@ -120,9 +120,10 @@ int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, 
     (void)ncu;
     DecConst d2 = dc;
     static_cast<Const64&>(d2) = c64;
-    int rc = persist_dispatch(P, d2, st);
-    if (rc || !P.dec_on) return rc;
-    // one block per epoch folds this launch's workgroup records (a shard: its own workgroups)
+    // the decision's counter records are folded inside the launch (amp_decide_fused.h
+    // dec_fold_gather; a shard folds its own workgroups), else by one block per epoch here
+    const int rc = persist_dispatch(P, d2, st);
+    if (rc || !P.dec_on || P.fold_in) return rc;
     hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg / P.E, P.counts);
     AMP_LAUNCH_CHECK("vamp_decide_fold");
     return AMP_OK;

@@ -717,15 +717,28 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         P.xm[(size_t)(row0 + row) * twoN + col] = sX[row * ldr + col];
     }
     for (int e = tid; e < nrows * N; e += PWG) P.var0[(size_t)row0 * N + e] = vlast[e];
-    if (wl == P.wg_off && tid == 0) {   // this launch's first workgroup of the epoch
-        amp_status s = vamp_make_status(P, cur, nx, fixed);
-        if (aborted) s.nan_state = -1;
-        P.status[ep] = s;
-    }
+    amp_status st_rec = vamp_make_status(P, cur, nx, fixed);
+    if (aborted) st_rec.nan_state = -1;
+    if (wl == P.wg_off && tid == 0) P.status[ep] = st_rec;   // this launch's first workgroup of the epoch
     if (P.dec_on) {
         __syncthreads();   // the V0/V1 region (vlast) becomes the label / mismatch scratch
-        decide_epilogue<PWG, KK>(P, dc, sR, sX, ldr, row0, lrow0, nrows, sA, lds + Y.offV0, 4 * (Y.offScr - Y.offV0),
-                                 scr);
+        // the records are folded here, by the epoch's first workgroup of this launch, from the
+        // tagged granules every workgroup publishes (no fold launch; tag unique per launch)
+        const unsigned dtag = P.fold_in ? P.gen * (unsigned)(P.max_iter + 1) + (unsigned)P.max_iter + 1u : 0u;
+        decide_epilogue<PWG, KK, true>(P, dc, sR, sX, ldr, row0, lrow0, nrows, sA, lds + Y.offV0,
+                                       4 * (Y.offScr - Y.offV0), scr, dtag);
+        const int nloc = nwg / P.E;                    // this launch's workgroups of one epoch
+        if (P.fold_in && wg % nloc == 0) {             // wl == P.wg_off: the status writer above
+            __syncthreads();
+            const bool ok = dec_fold_gather(P, wg, nloc, dtag, P.counts + ep, scr, &s_flag);
+            if (tid == 0) {
+                if (!ok) {                             // a workgroup never published: results invalid
+                    st_rec.nan_state = -1;
+                    P.status[ep] = st_rec;
+                }
+                if (P.host_rec && P.E == 1) host_record_write(P.host_rec, st_rec, P.counts[ep]);
+            }
+        }
     }
 }
 

@@ -78,6 +78,162 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
     }
 }
 
+// The k = 256 form (cfg4: n = 512): a workgroup takes 32 trials (two 16-row A tiles) and half the
+// outputs (eight 16-column tiles, one per wave), so each operator group a wave streams feeds 48
+// MFMAs of two row tiles — half the operator bytes per CU of the 16-trial form (1.5 MB, the per-CU
+// L2 rate was its wall).  The 32 rows' planes of all n = 512 columns would take 196 KB of LDS, so
+// the reduction runs in NH stages of KS columns (96 KB of planes each), in order: every output
+// sums the same products in the same order as gemm_x3 (bit-identical y~).
+// D: operator groups in flight (the kernel has registers to spare: 94 VGPRs at D = 1).  hook():
+// called once after the first group's MFMAs (the next stage's y loads go there, behind this
+// stage's first operator loads in the in-order vmcnt).
+template <int GH, int D, class Hook>
+__device__ __forceinline__ void x3_rows2(const unsigned short* sP0, const unsigned short* sP1, int ldx,
+                                         __amdgpu_buffer_rsrc_t wr, int gbase, f32x4 (&cr)[2], f32x4 (&ci)[2],
+                                         Hook&& hook) {
+    const int lane = threadIdx.x & 63;
+    const int vo = lane * 16;
+    u32x4 ring[D][6];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int f = 0; f < 6; ++f) ring[d][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((gbase + d) * 6 + f) * 1024, 0);
+    const int ln = pl_opaque(lane);
+    const int sw = (ln & 15) & pl_mask(ldx);
+    const int aoff = (ln & 15) * ldx + 8 * ((ln >> 4) ^ (sw & 3));
+    const int s32 = 32 * (sw >> 2);
+    const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+#pragma unroll
+    for (int g = 0; g < GH; ++g) {
+        const u32x4* w = ring[g % D];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const unsigned short* ap = (rt ? sP1 : sP0) + aoff + ((32 * g) ^ s32);
+            u32x4 a[6], na[3];
+#pragma unroll
+            for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+#pragma unroll
+            for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
+            f32x4 gr = cr[rt], gi = ci[rt];
+#define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
+            // gemm_x3's product order (smallest terms first)
+            AMP_MF(gr, a[0], w[2]);  AMP_MF(gi, a[0], w[5]);
+            AMP_MF(gr, a[1], w[1]);  AMP_MF(gi, a[1], w[4]);
+            AMP_MF(gr, a[2], w[0]);  AMP_MF(gi, a[2], w[3]);
+            AMP_MF(gr, na[0], w[5]); AMP_MF(gi, a[3], w[2]);
+            AMP_MF(gr, na[1], w[4]); AMP_MF(gi, a[4], w[1]);
+            AMP_MF(gr, na[2], w[3]); AMP_MF(gi, a[5], w[0]);
+            AMP_MF(gr, a[0], w[1]);  AMP_MF(gi, a[0], w[4]);
+            AMP_MF(gr, a[1], w[0]);  AMP_MF(gi, a[1], w[3]);
+            AMP_MF(gr, na[0], w[4]); AMP_MF(gi, a[3], w[1]);
+            AMP_MF(gr, na[1], w[3]); AMP_MF(gi, a[4], w[0]);
+            AMP_MF(gr, a[0], w[0]);  AMP_MF(gi, a[0], w[3]);
+            AMP_MF(gr, na[0], w[3]); AMP_MF(gi, a[3], w[0]);
+#undef AMP_MF
+            cr[rt] = gr; ci[rt] = gi;
+        }
+        if (g + D < GH) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f)
+                ring[g % D][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((gbase + g + D) * 6 + f) * 1024, 0);
+        }
+        if (g == 0) hook();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+#ifndef AMP_YTIL_RING
+#define AMP_YTIL_RING 3
+#endif
+template <int GH, int NH>
+__global__ __launch_bounds__(512, 1) void ytil_x3_r2_kernel(const float* __restrict__ y, int rows, const void* wq,
+                                                             float* __restrict__ ytil, int k, int rows_per_op,
+                                                             long long wq_stride) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    unsigned short* sP0 = reinterpret_cast<unsigned short*>(lds);
+    constexpr int KS = 32 * GH, n = KS * NH, G = GH * NH;
+    const int ldx = pl_ldx(KS);
+    unsigned short* sP1 = sP0 + 6 * 16 * ldx;
+    const int row0 = blockIdx.x * 32;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ct = blockIdx.y * 8 + wave;   // this wave's 16-column output tile
+    const int ctu = __builtin_amdgcn_readfirstlane(ct);
+    const char* wop = (const char*)wq + (long long)(row0 / rows_per_op) * wq_stride;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(wop) + (size_t)ctu * G * 6 * 1024, (short)0, 0x7ffffff0, 0x00020000);
+    f32x4 cr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 ci[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    // stage h's KS columns of the 32 rows: 8 complex values per item, rows fastest; the next
+    // stage's loads are in flight while this stage's GEMM runs
+    constexpr int ITEMS = 32 * (KS >> 3), PER = ITEMS / 512;
+    float4 v[PER][4];
+    auto load_stage = [&](int h) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = tid + i * 512, row = e % 32, j0 = 8 * (e / 32);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[i][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (row0 + row < rows)
+                    v[i][q] = *reinterpret_cast<const float4*>(y + (size_t)(row0 + row) * 2 * n + 2 * (h * KS + j0) + 4 * q);
+            }
+        }
+    };
+    load_stage(0);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        if (h > 0) __syncthreads();   // every wave is done with the previous stage's planes
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = tid + i * 512, row = e % 32, j0 = 8 * (e / 32);
+            float re[8], im[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                re[2 * q] = v[i][q].x; im[2 * q] = v[i][q].y; re[2 * q + 1] = v[i][q].z; im[2 * q + 1] = v[i][q].w;
+            }
+            x3_store8(row < 16 ? sP0 : sP1, ldx, row & 15, j0, re, im);
+        }
+        __syncthreads();
+        x3_rows2<GH, AMP_YTIL_RING>(sP0, sP1, ldx, wr, h * GH, cr, ci, [&] {
+            if (h + 1 < NH) load_stage(h + 1);
+        });
+    }
+    const int o = 16 * ct + (lane & 15);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = row0 + 16 * rt + 4 * (lane >> 4) + r;
+            if (row < rows) *reinterpret_cast<float2*>(ytil + (size_t)row * 2 * k + 2 * o) = make_float2(cr[rt][r], ci[rt][r]);
+        }
+}
+
+static int ytil_x3_r2_launch(const float* y, int rows, const void* wq, float* ytil, int k, int rows_per_op,
+                             long long wq_stride, hipStream_t st) {
+    const void* fn = (const void*)ytil_x3_r2_kernel<8, 2>;
+    const size_t lds = (size_t)2 * 6 * 16 * pl_ldx(256) * 2;
+    static int attr = -1;
+    if (attr < 0) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) {
+            set_error("ytil_x3_r2: hipFuncSetAttribute: %s", hipGetErrorString(e));
+            return AMP_E_LAUNCH;
+        }
+        attr = 1;
+    }
+    hipLaunchKernelGGL((ytil_x3_r2_kernel<8, 2>), dim3(cdiv(rows, 32), 2), dim3(512), lds, st, y, rows, wq, ytil, k,
+                       rows_per_op, wq_stride);
+    AMP_LAUNCH_CHECK("ytil_x3_r2");
+    return AMP_OK;
+}
+
+// AMP_YTIL_R2=0 keeps the 16-trial form at k = 256 (A/B runs; read per launch, so a test can
+// compare both forms in one process)
+static bool ytil_r2_env() {
+    const char* e = getenv("AMP_YTIL_R2");
+    return !(e && e[0] == '0');
+}
+
 template <int NC, int G, int NWV = 4>
 static int ytil_x3_launch_t(const float* y, int rows, const void* wq, float* ytil, int k, int rows_per_op,
                             long long wq_stride, hipStream_t st) {
@@ -108,7 +264,10 @@ int ytil_x3_launch(const float* y, int n, int rows, const void* wq, float* ytil,
     switch (k) {
     case 64: return ytil_x3_launch_t<1, 4>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
     case 128: return ytil_x3_launch_t<2, 8>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
-    case 256:   // eight waves (two per SIMD) hide the operator stream better, as in the engine
+    case 256:   // 32 trials x half the outputs per workgroup (every operator group feeds two row
+                // tiles); else eight waves of 16 trials, as in the engine
+        if (ytil_r2_env() && (rows_per_op % 32 == 0 || rows_per_op >= rows))
+            return ytil_x3_r2_launch(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
         return ytil_x3_launch_t<2, 16, 8>(y, rows, wq, ytil, k, rows_per_op, wq_stride, st);
     default: break;
     }

@@ -174,13 +174,16 @@ class SCAMP(LazyResult, nn.Module):
             if persistent and _FUSED_DECIDE and self.L.decision_mode == 'sparc':
                 # forward + decision on T.xmap (scamp.py:107) + counters in one launch sequence
                 dec = self.L.decide_args(x, symbol, index, out=res[64:])
+                dec.host_record = None if nat.fold_launch() else host.data_ptr()   # status + counters written there
                 T._call('amp_scamp_detect_count', C.byref(dec))
+                written = not nat.fold_launch()
             else:
                 T._call('amp_scamp_run')
                 # decision on T.xmap (scamp.py:107); counters next to the status record
                 self.L.device_counts(T.buf.xmap, T.buf.xmmse, x, symbol, index, out=res[64:])
+                written = False
             rescue = (lambda: self._rescue_forward(W, A, y, SNR, x, symbol, index)) if persistent else None
-            self._arm(self.L, res, host, 'amp_scamp_run', rescue)          # + L.dump(), scamp.py:99
+            self._arm(self.L, res, host, 'amp_scamp_run', rescue, written=written)   # + L.dump(), scamp.py:99
         self._keep = T
         self.last = T
         return self.L

@@ -181,7 +181,8 @@ class LazyResult:
         self._slot ^= 1
         return self._ring[self._slot]
 
-    def _arm(self, L: Loss, res: torch.Tensor, host: torch.Tensor, what: str, rescue=None) -> None:
+    def _arm(self, L: Loss, res: torch.Tensor, host: torch.Tensor, what: str, rescue=None,
+             written: bool = False) -> None:
         """Queue the copy of `res` to `host` on the device's current stream and make L resolve it
         lazily; the previous forward's record is resolved first.
 
@@ -192,8 +193,11 @@ class LazyResult:
         rescue (or if it fails too) the resolve raises.  The rescue re-reads the forward's input
         tensors when the Loss resolves (at the latest inside the next forward call), so they must
         not be overwritten in place before then — the reference's own contract for the returned
-        Loss (read it before the next call, vamp_model.py:61-62)."""
-        host.copy_(res, non_blocking=True)
+        Loss (read it before the next call, vamp_model.py:61-62).
+        written: the forward's last kernel wrote the record into `host` itself
+        (amp_vamp_decide_args.host_record), so no copy is queued."""
+        if not written:
+            host.copy_(res, non_blocking=True)
         done = torch.cuda.Event()
         done.record(torch.cuda.current_stream(res.device))   # the stream the launches and the copy ran on
         L.resolve()                 # the previous forward's counters (it has finished by now)
@@ -287,6 +291,7 @@ class VAMP(LazyResult, nn.Module):
         if fused:
             # forward + decision on T.r (vamp.py:187) + counters in one launch sequence
             dec = self.L.decide_args(x, symbols, indices, out=res[64:])
+            dec.host_record = None if nat.fold_launch() else host.data_ptr()   # status + counters written there
             nat.check(lib.amp_vamp_detect_count(C.byref(T.dims), C.byref(T.const), C.byref(T.args), C.byref(dec),
                                                  T.stream), 'amp_vamp_detect_count')
         else:
@@ -295,7 +300,7 @@ class VAMP(LazyResult, nn.Module):
             self.L.device_counts(T.buf.r, T.buf.xmmse, x, symbols, indices, out=res[64:])
         persistent = lib.amp_vamp_select_engine(C.byref(T.dims), T.k, self.engine) == nat.ENGINE_PERSISTENT
         rescue = (lambda: self._rescue_forward(U, s, Vh, y, SNR, x, symbols, indices)) if persistent else None
-        self._arm(self.L, res, host, 'amp_vamp_run', rescue)              # + L.dump(), vamp.py:180
+        self._arm(self.L, res, host, 'amp_vamp_run', rescue, written=fused and not nat.fold_launch())   # + L.dump()
         self.last = T
         return self.L
 

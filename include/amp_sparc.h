@@ -172,6 +172,13 @@ typedef struct amp_vamp_decide_args {
     int32_t ibits_trunc;  /* ceil(log2(Lin*B*Na)) (loss.py:20) */
     int32_t pad;
     void* counts;         /* out amp_counts (device) */
+    void* host_record;    /* optional (NULL: none): a 256-byte page-locked host buffer mapped for the
+                           * device (hipHostMalloc / torch pin_memory).  amp_vamp_detect_count on the
+                           * persistent engine then also writes the forward's amp_status at byte 0
+                           * and its amp_counts at byte 64 there (system-scope stores from the last
+                           * kernel of the forward), so the caller needs no device-to-host copy: the
+                           * record is valid once the stream has passed the forward.  Ignored by
+                           * the other entry points. */
 } amp_vamp_decide_args;
 int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                           const amp_vamp_decide_args* dec, void* stream);
@@ -237,7 +244,8 @@ size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max
 /* Diagnostic: byte offsets inside the epochs workspace of the persistent engine's exchange
  * records: out[0] the per-iteration granule pairs ([max_iter][epochs * ceil(B/16)] x 32 B:
  * {sum var f64, not-close u32, tag u32}, {max|xi| f32, min section max f32, 0, tag}), out[1] the
- * rare-path float64 words, out[2] the barrier words, out[3] the per-workgroup counter records. */
+ * rare-path float64 words, out[2] the barrier words, out[3] the per-workgroup counter records,
+ * out[4] y~ ([epochs * B][2k] floats; also the single-forward workspace's, epochs = 1). */
 int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs, uint64_t* out);
 /* Diagnostic: every later persistent VAMP launch of this process writes its per-iteration state
  * to buf (device, float32: [max_iter][nwg][5][16][2N]: w after GEMM1's epilogue, r after GEMM2's,

@@ -295,6 +295,32 @@ def test_vamp_engines_agree(device, ebn0):
     assert torch.allclose(rs[0], rs[1], rtol=0, atol=2e-6 * scale), float((rs[0] - rs[1]).abs().max())
 
 
+@pytest.mark.parametrize('B', [4096, 1008])
+def test_ytil_row_pair_form_bit_identical(device, B, monkeypatch):
+    """y~ = (s Uh) y at k = 256 (vamp.py:22): the 32-trial / half-output workgroups of
+    ytil_x3_r2_kernel (two row tiles per operator group, the reduction in two 256-column stages)
+    give the same bits as the 16-trial gemm_x3 form (AMP_YTIL_R2=0, read per launch), and so do
+    the whole forward's r / xmmse / var; B = 1008 ends off a multiple of 32."""
+    import ctypes as C
+    import amp_native as nat
+    from vamp import VAMP
+    ent = CURVES['cfg4_vamp_16qam']
+    cfg = _config(ent['Nt'], ent['Na'], ent['Nr'], B, ent['alphabet'], iterations=3)
+    inp = _regen_inputs(cfg, 2, 8.0)
+    k = ent['Nt']
+    off = (C.c_uint64 * 5)()
+    nat.check(nat.lib().amp_vamp_debug_offsets(C.byref(cfg.dims()), k, 3, 1, off), 'amp_vamp_debug_offsets')
+    outs = []
+    for r2 in ('0', '1'):
+        monkeypatch.setenv('AMP_YTIL_R2', r2)
+        T = VAMP(cfg, engine=2).detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
+        torch.cuda.synchronize()
+        yt = T.buf.ws[off[4]:off[4] + B * 2 * k * 4].clone()
+        outs.append([yt, T.buf.r.clone(), T.buf.xmmse.clone(), T.buf.var.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+
+
 @pytest.mark.parametrize('name', ['cfg4_vamp_16qam', 'cfg2_vamp_qpsk'])
 @pytest.mark.parametrize('iters', [1, 3])
 def test_vamp_x3_gemm_matches_f32(device, name, iters):

@@ -42,6 +42,11 @@ def test_struct_layouts_match_header():
     assert C.sizeof(nat.AmpStatus) == 32
     assert C.sizeof(nat.AmpCounts) == 13 * 8
     assert nat.AmpVampArgs.noise_var.offset == 48 and C.sizeof(nat.AmpVampArgs) == 112
+    # amp_vamp_decide_args: x, sym, idx, (ibits_trunc, pad), counts, host_record
+    assert nat.AmpVampDecideArgs.counts.offset == 32 and nat.AmpVampDecideArgs.host_record.offset == 40
+    assert C.sizeof(nat.AmpVampDecideArgs) == 48
+    # amp_status at byte 0 and amp_counts at byte 64 of a 256-byte result record (vamp.py LazyResult)
+    assert C.sizeof(nat.AmpStatus) <= 64 and 64 + C.sizeof(nat.AmpCounts) <= 256
 
 
 def test_workspace_sizes():

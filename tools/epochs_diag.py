@@ -24,7 +24,7 @@ from vamp import VAMP  # noqa: E402
 
 
 def granules(ws: torch.Tensor, d, k, iters, epochs):
-    off = (C.c_uint64 * 4)()
+    off = (C.c_uint64 * 5)()
     nat.check(nat.lib().amp_vamp_debug_offsets(C.byref(d), k, iters, epochs, off), 'amp_vamp_debug_offsets')
     nwg = epochs * ((d.B + 15) // 16)
     n = iters * nwg * 32

@@ -112,6 +112,12 @@ for s in ${STEPS:-bench}; do
         run ab_${DIAG:-tgr} 300 env AMP_LIB_PATH=$D python3 bench.py --no-cpu-baseline &&
         run ab_def2 300 python3 bench.py --no-cpu-baseline &&
         run ab_${DIAG:-tgr}_2 300 env AMP_LIB_PATH=$D python3 bench.py --no-cpu-baseline ;;
+    # A/B of an environment switch (ENVAB="NAME=value") against the default on one box
+    ab_env) run abe_def 300 python3 bench.py --no-cpu-baseline &&
+            run abe_env 300 env $ENVAB python3 bench.py --no-cpu-baseline &&
+            run abe_def2 300 python3 bench.py --no-cpu-baseline &&
+            run abe_env2 300 env $ENVAB python3 bench.py --no-cpu-baseline ;;
+    tests_ytil) run tests_ytil 300 $PYT tests/test_gpu_vamp.py -m gpu -k "ytil or engines_agree or n256 or x3_gemm" ;;
     trace_diag) run trace_${DIAG:-tgr} 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_${DIAG:-tgr}.so python3 tools/trace_persist.py --config cfg4 ;;
     configs_res1) run configs_res1 300 python3 tools/configs_bench.py cfg2 cfg2-epochs8 cfg2-res1 ;;
     ttrace1) run ttrace1 600 python3 tools/t_trace.py --point cfg4_vamp_qpsk:1/0 --save "" --variants persistent,launches ;;
