@@ -24,6 +24,9 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #ifndef AMP_X3_W8_PIN
 #define AMP_X3_W8_PIN 0
 #endif
+#ifndef AMP_X3_W8_RING
+#define AMP_X3_W8_RING 1                // eight-wave bf16x3 GEMM ring depth (A/B builds try 2 with AMP_X3_W8_PIN)
+#endif
 #ifndef AMP_X3_W8_PKGRID
 #define AMP_X3_W8_PKGRID 1              // the eight-wave bf16x3 form keeps 16-QAM's packed grid denoiser
 #endif
@@ -94,7 +97,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     constexpr int PWG = 64 * NWV;
     constexpr int NC = X3 ? NT / 2 : 1;        // complex column tiles per wave (X3)
     constexpr int G3 = NT * NWV / 4;           // 32-wide complex reduction groups: N / 32
-    constexpr int X3R = 1;                     // weight groups in flight (gemm_x3)
+    constexpr int X3R = (NWV == 8) ? AMP_X3_W8_RING : 1;   // weight groups in flight (gemm_x3)
     // eight waves: no A-fragment prefetch in gemm_x3 (the partner wave covers the LDS reads;
     // 24 registers fewer) when AMP_X3_W8_PIN (A/B builds)
     constexpr bool X3PIN = NWV == 8 && AMP_X3_W8_PIN;

@@ -103,15 +103,24 @@ __device__ __forceinline__ void x3_rows2(const unsigned short* sP0, const unsign
     const int aoff = (ln & 15) * ldx + 8 * ((ln >> 4) ^ (sw & 3));
     const int s32 = 32 * (sw >> 2);
     const u32x4 sgn = {0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};
+    // A fragments one row tile ahead (read from LDS while the previous tile's MFMAs run)
+    auto lda = [&](int g, int rt, u32x4 (&a)[6]) {
+        const unsigned short* ap = (rt ? sP1 : sP0) + aoff + ((32 * g) ^ s32);
+#pragma unroll
+        for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+    };
+    u32x4 acur[6];
+    lda(0, 0, acur);
 #pragma unroll
     for (int g = 0; g < GH; ++g) {
         const u32x4* w = ring[g % D];
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-            const unsigned short* ap = (rt ? sP1 : sP0) + aoff + ((32 * g) ^ s32);
-            u32x4 a[6], na[3];
+            u32x4 a[6], anx[6], na[3];
 #pragma unroll
-            for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const u32x4*>(ap + f * 16 * ldx);
+            for (int f = 0; f < 6; ++f) a[f] = acur[f];
+            if (rt == 0) lda(g, 1, anx);
+            else if (g + 1 < GH) lda(g + 1, 0, anx);
 #pragma unroll
             for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
             f32x4 gr = cr[rt], gi = ci[rt];
@@ -131,6 +140,10 @@ __device__ __forceinline__ void x3_rows2(const unsigned short* sP0, const unsign
             AMP_MF(gr, na[0], w[3]); AMP_MF(gi, a[3], w[0]);
 #undef AMP_MF
             cr[rt] = gr; ci[rt] = gi;
+            if (rt == 0 || g + 1 < GH) {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) acur[f] = anx[f];
+            }
         }
         if (g + D < GH) {
 #pragma unroll
