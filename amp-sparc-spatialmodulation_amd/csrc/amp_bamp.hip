@@ -14,6 +14,7 @@
 #include "amp_denoise.h"
 #include "amp_gemm.h"
 #include "amp_gemm_h2.h"
+#include "amp_gemm_x3.h"
 #include <vector>
 #include <cstdio>
 #include "amp_host.h"
@@ -65,8 +66,11 @@ struct BampK {
     float P0, Ps;
     // fp16x2 GEMMs (amp_gemm_h2.h): the four operators h2-packed into the weight buffers above
     // (real |H|^2 two planes, complex H / H^H four), each GEMM's A rows split into `ap` first
-    int h2, rows_pad;
-    unsigned short* ap;    // [4 planes][rows_pad][max(N, n)] fp16
+    // bf16x3 GEMMs (amp_gemm_x3.h, x3 = 1): the same scheme with three bf16 pieces per value (real
+    // |H|^2 three planes, complex H / H^H six; no exponents)
+    int h2, x3, rows_pad;
+    int tile_rows;         // row-block-major tile order (xcd_tile_rows: the fp16x2 tiles), else xcd_tile
+    unsigned short* ap;    // [4 planes][rows_pad][max(N, n)] fp16, or [6 planes][...] bf16
     int* rexp;             // [rows_pad] row exponents
     // launch engine: rcnt[1] is bamp_fixall's arrival counter (zeroed by bamp_init_kernel)
     unsigned* rcnt;
@@ -147,9 +151,12 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     bamp_geometry(d, P);
     Carve cv(base);
     BampWs w;
-    w.Wabs2 = cv.take<float>((size_t)P.ncpA1 * P.kapA1);
+    // the split forms' shapes also hold the bf16x3 real operators: three 16-bit planes, 1.5x the
+    // f32 weight, over the padded outputs the last column tile streams
+    const bool x3 = bamp_h2_shape(d);
+    w.Wabs2 = cv.take<float>((size_t)P.ncpA1 * P.kapA1 * (x3 ? 3 : 2) / 2);
     w.WH = cv.take<float>((size_t)P.ncpA2 * P.kapA2);
-    w.Wabs2T = cv.take<float>((size_t)P.ncpB1 * P.kapB1);
+    w.Wabs2T = cv.take<float>((size_t)P.ncpB1 * P.kapB1 * (x3 ? 3 : 2) / 2);
     w.WHH = cv.take<float>((size_t)P.ncpB2 * P.kapB2);
     w.v = cv.take<float>((size_t)d->B * d->n);
     w.z = cv.take<float>((size_t)d->B * 2 * d->n);
@@ -170,8 +177,9 @@ static BampWs bamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.ap = nullptr;
     w.rexp = nullptr;
     if (bamp_h2_shape(d)) {
+        // the A planes of either split form (fp16x2: four, bf16x3: six)
         const size_t rp = (size_t)round_up(d->B, GBM);
-        w.ap = cv.take<unsigned short>(4 * rp * std::max(d->N, d->n));
+        w.ap = cv.take<unsigned short>(6 * rp * std::max(d->N, d->n));
         w.rexp = cv.take<int>(rp);
     }
     w.bytes = cv.off;
@@ -192,9 +200,11 @@ template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (KC == GKC && P.h2)
+    if (KC == GKC && P.x3)
+        gemm_tile_x3<128, false>(P.ap, P.rows_pad, P.N, P.Wabs2, row0, col0, lds, bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
+    else if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds, bkb(P, 0, tile.cb),
                                        bke(P, 0, tile.cb));
     else
@@ -213,10 +223,12 @@ template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (KC == GKC && P.h2)
+    if (KC == GKC && P.x3)
+        gemm_tile_x3<128, true>(P.ap, P.rows_pad, P.N, P.WH, row0, col0, lds, bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
+    else if (KC == GKC && P.h2)
         gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds, bkb(P, 1, tile.cb),
                                        bke(P, 1, tile.cb));
     else
@@ -231,18 +243,16 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     float vv[IT], iuo[IT];
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
+        // unconditional loads at a clamped index (a lane-divergent branch around them serialises
+        // their latencies, amp_gemm.h ALoadPlain); out-of-range elements are never stored
         const int e = threadIdx.x + u * AMP_WG;
         const int rho = e >> 6, cp = e & 63;           // complex column pair
-        const int row = row0 + rho, i = (col0 >> 1) + cp;
-        yv[u] = zv[u] = make_float2(0.f, 0.f);
-        vv[u] = iuo[u] = 0.f;
-        if (row < P.B && i < P.n) {
-            const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
-            yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
-            zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
-            vv[u] = P.v[o];
-            iuo[u] = P.invu[o];
-        }
+        const int row = min(row0 + rho, P.B - 1), i = min((col0 >> 1) + cp, P.n - 1);
+        const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
+        yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
+        zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
+        vv[u] = P.v[o];
+        iuo[u] = P.invu[o];
     }
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
@@ -270,9 +280,11 @@ template <int KC = GKC>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
-    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (KC == GKC && P.h2)
+    if (KC == GKC && P.x3)
+        gemm_tile_x3<128, false>(P.ap, P.rows_pad, P.n, P.Wabs2T, row0, col0, lds, bkb(P, 2, tile.cb), bke(P, 2, tile.cb));
+    else if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds, bkb(P, 2, tile.cb),
                                        bke(P, 2, tile.cb));
     else
@@ -324,10 +336,12 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     using C = GemmCfg<BN, KC>;
-    const GemmTile tile = (KC == GKC && P.h2) ? xcd_tile_rows() : xcd_tile();
+    const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (KC == GKC && P.h2)
+    if (KC == GKC && P.x3)
+        gemm_tile_x3<BN, true>(P.ap, P.rows_pad, P.n, P.WHH, row0, col0, lds, bkb(P, 3, tile.cb), bke(P, 3, tile.cb));
+    else if (KC == GKC && P.h2)
         gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds, bkb(P, 3, tile.cb),
                                bke(P, 3, tile.cb));
     else
@@ -343,10 +357,10 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
         float xv[IT], cvv[IT];
 #pragma unroll
         for (int u = 0; u < IT; ++u) {
-            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
-            const bool ok = rho < nrows && cc < ncols;
-            xv[u] = ok ? P.xm[(size_t)(row0 + rho) * twoN + col0 + cc] : 0.f;
-            cvv[u] = ok ? P.cov[(size_t)(row0 + rho) * P.N + ((col0 + cc) >> 1)] : 0.f;
+            // unconditional loads at a clamped index (see bamp_ka2); out-of-range elements unused
+            const int e = threadIdx.x + u * AMP_WG, rho = min(e / BN, nrows - 1), cc = min(e % BN, ncols - 1);
+            xv[u] = P.xm[(size_t)(row0 + rho) * twoN + col0 + cc];
+            cvv[u] = P.cov[(size_t)(row0 + rho) * P.N + ((col0 + cc) >> 1)];
         }
 #pragma unroll
         for (int u = 0; u < IT; ++u) {
@@ -697,10 +711,17 @@ __global__ void bamp_output_kernel(BampK P) {
         P.var0[e] = P.var1[e];
 }
 
-// dynamic LDS of every BAMP GEMM launch: the f32 tile's A block or the fp16x2 tile's four staged
-// planes, whichever is larger (either arithmetic runs from the same instantiation)
-constexpr size_t BLDS = h2_tile_lds<256, true>() > GemmCfg<256>::LDS_BYTES ? h2_tile_lds<256, true>()
-                                                                             : GemmCfg<256>::LDS_BYTES;
+// dynamic LDS of every BAMP GEMM launch: the f32 tile's A block or the split tiles' staged planes,
+// whichever is larger (every arithmetic runs from the same instantiation)
+constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
+constexpr size_t BLDS = cmax(h2_tile_lds<256, true>(), GemmCfg<256>::LDS_BYTES);
+// the bf16x3 launches' LDS: the staged planes or the C tile + the epilogue's scratch past it (the
+// partial-store scratch; bamp_kb2: + the 1 / tau tile): 48 KB for the complex tiles, three per CU
+constexpr size_t XLDS_R = x3_tile_lds<128, false>(2048);
+constexpr size_t XLDS_C = x3_tile_lds<128, true>(2048);
+template <int BN>
+constexpr size_t xlds_kb2() { return x3_tile_lds<BN, true>(2048 + GBM * (BN / 2)); }
+static_assert(xlds_kb2<256>() <= BLDS && XLDS_C <= BLDS, "bf16x3 tiles within the attribute");
 static_assert(BLDS <= 80 * 1024, "two BAMP GEMM workgroups per CU");
 static int bamp_lds_attr(const void* fn) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BLDS);
@@ -725,7 +746,7 @@ static bool bamp_short_chunks(const BampK& P) {
         const char* e = getenv("AMP_BAMP_KC");
         return e && atoi(e) == 512;
     }();
-    return !P.h2 && !off;
+    return !P.h2 && !P.x3 && !off;
 }
 
 template <int KK>
@@ -735,11 +756,11 @@ static void launch_kb2_kk(const BampK& P, const Const64& c64, int gr, int t, hip
         return;
     }
     if (P.bn == 128)
-        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BLDS, st, P,
-                           c64, t);
+        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG),
+                           P.x3 ? xlds_kb2<128>() : BLDS, st, P, c64, t);
     else
-        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), BLDS, st, P,
-                           c64, t);
+        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG),
+                           P.x3 ? xlds_kb2<256>() : BLDS, st, P, c64, t);
 }
 
 static void launch_kb2(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
@@ -818,19 +839,29 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.elementwise = a->denoiser;
     P.P0 = a->P0;
     P.Ps = a->Ps;
-    // GEMM arithmetic: f32 MFMA (AUTO: the reference's c64 operand precision, bamp.py:59-64) or,
-    // only when asked for (AMP_GEMM_H2, or AUTO with AMP_BAMP_GEMM=h2), the fp16x2 tile (22-bit
-    // operands: narrower than the reference)
-    AMP_REQUIRE(a->gemm == AMP_GEMM_AUTO || a->gemm == AMP_GEMM_F32 || a->gemm == AMP_GEMM_H2,
-                "amp_bamp_run: gemm %d (AUTO, F32 or H2)", a->gemm);
+    // GEMM arithmetic, all at the reference's c64 operand precision (bamp.py:59-64) unless fp16x2 is
+    // asked for: AMP_GEMM_F32 (f32 MFMA), AMP_GEMM_X3 (bf16x3 tiles, 24-bit operands) or, only when
+    // asked for (AMP_GEMM_H2, or AUTO with AMP_BAMP_GEMM=h2), the fp16x2 tile (22-bit operands:
+    // narrower than the reference).  AUTO: f32 MFMA (AMP_BAMP_GEMM=x3: bf16x3 where the shape tiles).
+    AMP_REQUIRE(a->gemm == AMP_GEMM_AUTO || a->gemm == AMP_GEMM_F32 || a->gemm == AMP_GEMM_H2 || a->gemm == AMP_GEMM_X3,
+                "amp_bamp_run: gemm %d (AUTO, F32, X3 or H2)", a->gemm);
     const bool h2ok = bamp_h2_shape(d);
-    AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || h2ok, "amp_bamp_run: the fp16x2 GEMMs need N %% 64 == 0 and n %% 64 == 0 "
-                "(N = %d, n = %d)", d->N, d->n);
-    static const bool h2_env = [] {
+    AMP_REQUIRE((a->gemm != AMP_GEMM_H2 && a->gemm != AMP_GEMM_X3) || h2ok,
+                "amp_bamp_run: the split-precision GEMMs need N %% 64 == 0 and n %% 64 == 0 (N = %d, n = %d)", d->N, d->n);
+    static const char gemm_env = [] {
         const char* e = getenv("AMP_BAMP_GEMM");
-        return e && e[0] == 'h';
+        return e ? e[0] : '\0';
     }();
-    P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && h2_env)) ? 1 : 0;
+    P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && gemm_env == 'h')) ? 1 : 0;
+    P.x3 = (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && h2ok && gemm_env == 'x')) ? 1 : 0;
+    // tile order: the fp16x2 tiles walk row blocks (each XCD serves the whole 4 MB operator from its
+    // L2); the bf16x3 operator (6 MB at cfg5) does not fit, so its tiles walk column blocks (each
+    // XCD keeps its share of the operator resident).  AMP_BAMP_X3_ROWS=1: row-major (A/B runs).
+    static const bool x3_rows = [] {
+        const char* e = getenv("AMP_BAMP_X3_ROWS");
+        return e && e[0] == '1';
+    }();
+    P.tile_rows = P.h2 || (P.x3 && x3_rows) ? 1 : 0;
     P.rows_pad = round_up(d->B, GBM);
     P.ap = w.ap;
     P.rexp = w.rexp;
@@ -842,7 +873,16 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
 static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t st) {
     int rc;
     const float2* H = (const float2*)a->H;
-    if (P.h2) {
+    if (P.x3) {
+        // the four operators as bf16x3 planes in ONE launch: |H|^2 (O = n, J = N), H (O = n, J = N),
+        // |H|^2^T (O = N, J = n), H^H (O = N, J = n)
+        CWeightJob j[4];
+        j[0] = CWeightJob{H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.Wabs2, P.N, P.n, WPACKX3_ABS2, 0};
+        j[1] = CWeightJob{H, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WH, P.N, P.n, WPACKX3, 0};
+        j[2] = CWeightJob{H, 1, P.N, 0, nullptr, P.N, P.n, (float*)P.Wabs2T, P.n, P.N, WPACKX3_ABS2, 0};
+        j[3] = CWeightJob{H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.n, P.N, WPACKX3, 0};
+        if ((rc = build_cweights(j, 4, nullptr, 0, st))) return rc;
+    } else if (P.h2) {
         // the four operators as fp16x2 planes (exponent BH2_EX) in ONE launch: |H|^2 (O = n, J = N),
         // H (O = n, J = N), |H|^2^T (O = N, J = n), H^H (O = N, J = n)
         CWeightJob j[4];
@@ -858,12 +898,14 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
     if ((rc = build_abs2_weight(H, 1, P.N, P.N, P.n, (float*)P.Wabs2T, P.kapB1, P.ncpB1, st))) return rc;
     if ((rc = build_cweight(H, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WHH, P.kapB2, P.ncpB2, st))) return rc;
     }
-    if (P.band[0] && P.h2) {
-        // per column tile: real |H|^2 (two planes, 8 16-tiles per 128 outputs), complex H (four, 4)
-        if ((rc = h2_kband(P.Wabs2, 2, P.N / 32, 8, P.ncpA1 / 128, P.n / 16, const_cast<int*>(P.band[0]), st))) return rc;
-        if ((rc = h2_kband(P.WH, 4, P.N / 32, 4, P.ncpA2 / 128, P.n / 16, const_cast<int*>(P.band[1]), st))) return rc;
-        if ((rc = h2_kband(P.Wabs2T, 2, P.n / 32, 8, P.ncpB1 / 128, P.N / 16, const_cast<int*>(P.band[2]), st))) return rc;
-        if ((rc = h2_kband(P.WHH, 4, P.n / 32, P.bn / 32, P.ncpB2 / P.bn, P.N / 16, const_cast<int*>(P.band[3]), st))) return rc;
+    if (P.band[0] && (P.h2 || P.x3)) {
+        // per column tile: real |H|^2 (fp16x2 two planes, bf16x3 three; 8 16-tiles per 128
+        // outputs), complex H (four / six planes, 4)
+        const int pr = P.x3 ? 3 : 2, pc = P.x3 ? 6 : 4;
+        if ((rc = h2_kband(P.Wabs2, pr, P.N / 32, 8, P.ncpA1 / 128, P.n / 16, const_cast<int*>(P.band[0]), st))) return rc;
+        if ((rc = h2_kband(P.WH, pc, P.N / 32, 4, P.ncpA2 / 128, P.n / 16, const_cast<int*>(P.band[1]), st))) return rc;
+        if ((rc = h2_kband(P.Wabs2T, pr, P.n / 32, 8, P.ncpB1 / 128, P.N / 16, const_cast<int*>(P.band[2]), st))) return rc;
+        if ((rc = h2_kband(P.WHH, pc, P.n / 32, P.bn / 32, P.ncpB2 / P.bn, P.N / 16, const_cast<int*>(P.band[3]), st))) return rc;
         if (getenv("AMP_DEBUG_BAND")) {   // diagnostic: the ranges as formed (synchronises the stream)
             const int nt[4] = {P.ncpA1 / 128, P.ncpA2 / 128, P.ncpB1 / 128, P.ncpB2 / P.bn};
             for (int i = 0; i < 4; ++i) {
@@ -896,6 +938,15 @@ static void bamp_split(const BampK& P, const float* a, int lda, int K, bool cpx,
     // a workgroup per row when four rows per workgroup would leave CUs idle on long rows
     const int wpr = (P.rows_pad / 4 < 2 * device_cu_count() && K >= 1024) ? 4 : 1;
     const dim3 grid(P.rows_pad * wpr / 4);
+    if (P.x3) {
+        if (cpx)
+            hipLaunchKernelGGL(x3_split_rows_kernel<true>, grid, dim3(256), 0, st, a, lda, P.B, P.rows_pad, K, P.ap,
+                               stop, wpr);
+        else
+            hipLaunchKernelGGL(x3_split_rows_kernel<false>, grid, dim3(256), 0, st, a, lda, P.B, P.rows_pad, K, P.ap,
+                               stop, wpr);
+        return;
+    }
     if (cpx)
         hipLaunchKernelGGL(h2_split_rows_kernel<true>, grid, dim3(256), 0, st, a, lda, P.B, P.rows_pad, K, P.ap,
                            P.rexp, stop, wpr);
@@ -907,17 +958,17 @@ static void bamp_split(const BampK& P, const float* a, int lda, int K, bool cpx,
 static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st) {
     const int gr = cdiv(P.B, GBM);
     // the host reads bvar(P, t + 1) as the device does: (t + 1) & 1 picks var1, else var0
-    if (P.h2) bamp_split(P, ((t + 1) & 1) ? P.var1 : P.var0, P.N, P.N, false, t, st);
+    if (P.h2 || P.x3) bamp_split(P, ((t + 1) & 1) ? P.var1 : P.var0, P.N, P.N, false, t, st);
     const bool skc = bamp_short_chunks(P);
     if (skc) hipLaunchKernelGGL((bamp_ka1<256>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_ka1<>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BLDS, st, P, t);
-    if (P.h2) bamp_split(P, P.xm, 2 * P.N, P.N, true, t, st);
+    else hipLaunchKernelGGL((bamp_ka1<>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), P.x3 ? XLDS_R : BLDS, st, P, t);
+    if (P.h2 || P.x3) bamp_split(P, P.xm, 2 * P.N, P.N, true, t, st);
     if (skc) hipLaunchKernelGGL((bamp_ka2<256>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_ka2<>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BLDS, st, P, t);
-    if (P.h2) bamp_split(P, P.invu, P.n, P.n, false, t, st);
+    else hipLaunchKernelGGL((bamp_ka2<>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), P.x3 ? XLDS_C : BLDS, st, P, t);
+    if (P.h2 || P.x3) bamp_split(P, P.invu, P.n, P.n, false, t, st);
     if (skc) hipLaunchKernelGGL((bamp_kb1<256>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_kb1<>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BLDS, st, P, t);
-    if (P.h2) bamp_split(P, P.s, 2 * P.n, P.n, true, t, st);
+    else hipLaunchKernelGGL((bamp_kb1<>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), P.x3 ? XLDS_R : BLDS, st, P, t);
+    if (P.h2 || P.x3) bamp_split(P, P.s, 2 * P.n, P.n, true, t, st);
     launch_kb2(P, c64, gr, t, st);
 }
 

@@ -79,6 +79,14 @@ __host__ __device__ __forceinline__ size_t x3_index(int o, int j, int f, int J) 
     return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 6 + f) * 64 + lane) * 8 + (kk & 7);
 }
 
+// The same for a real operator in the bf16x3 launch tile (amp_gemm_x3.h): three planes per
+// (tile, group), f = 0-2: x0 x1 x2.
+__host__ __device__ __forceinline__ size_t x3r_index(int o, int j, int f, int J) {
+    const int kk = j & 31;
+    const int lane = (o & 15) + 16 * (kk >> 3);
+    return ((((size_t)(o >> 4) * (J >> 5) + (j >> 5)) * 3 + f) * 64 + lane) * 8 + (kk & 7);
+}
+
 // The same for the fp16x2 form (gemm_h2): four planes per (tile, group), f = 0-1: Re h0 h1,
 // 2-3: Im h0 h1.
 __host__ __device__ __forceinline__ size_t h2_index(int o, int j, int f, int J) {
@@ -131,13 +139,21 @@ __device__ __forceinline__ GemmTile xcd_tile_rows() {
     return GemmTile{pos / nc, pos % nc};
 }
 
-// Plain A operand: rows of `lda` floats, `ka` valid columns (zero beyond, and for rows >= rows).
+// Plain A operand: rows of `lda` floats, `ka` valid columns (zero beyond, and for rows >= rows;
+// ka % 4 == 0, ka >= 4, rows >= 1).  The tile stages its A chunks in two steps: raw() issues the
+// load at a clamped, always valid address (no branch: a lane-divergent `if` around a load makes
+// the other lanes' zero write wait for it, i.e. every load of a chunk waited out its full latency
+// in turn), fin() zeroes the out-of-range elements once the value is needed (at the LDS store).
 struct ALoadPlain {
     const float* __restrict__ a;
     int lda, rows, ka;
-    __device__ __forceinline__ float4 operator()(int row, int k) const {
-        if (row >= rows || k >= ka) return make_float4(0.f, 0.f, 0.f, 0.f);
-        return *reinterpret_cast<const float4*>(a + (size_t)row * lda + k);
+    using Raw = float4;
+    __device__ __forceinline__ Raw raw(int row, int k) const {
+        return *reinterpret_cast<const float4*>(a + (size_t)min(row, rows - 1) * lda + min(k, ka - 4));
+    }
+    __device__ __forceinline__ float4 fin(const Raw& v, int row, int k) const {
+        const bool ok = row < rows && k < ka;
+        return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 };
 
@@ -179,26 +195,28 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)((kb >> 3) + d) * 64];
     // A chunk staging: all loads of a batch in flight before its LDS stores.  Short chunks
     // (KC <= 256: 8 float4 per thread) load the NEXT chunk into registers while this one's MFMAs
-    // run; 512-wide chunks stage in two half-batches between the chunks.
+    // run; 512-wide chunks stage in two half-batches between the chunks.  Every chunk is staged
+    // with the full chunk's compile-time geometry (AL::raw / fin): a tail chunk's columns past ke
+    // are not loaded (a masked load with no else-write: nothing waits on it) and land in LDS as
+    // whatever the registers held, but no group reads them.
     constexpr int PER = GBM * (KC / 4) / AMP_WG;    // float4 per thread for a full chunk
     constexpr bool PF = PER <= 8;
-    float4 nxt[PF ? PER : 1];
-    auto load_chunk = [&](int c0, float4* t4, int h, int cnt) {
-        const int q4 = min(KC, ke - c0) >> 2, nq = GBM * q4;
+    using Raw = typename AL::Raw;
+    Raw nxt[PF ? PER : 1];
+    auto load_chunk = [&](int c0, Raw* t4, int h, int cnt) {
 #pragma unroll
         for (int i = 0; i < cnt; ++i) {
             const int e = tid + (h + i) * AMP_WG;
-            const int row = e / q4, k4 = e - row * q4;
-            t4[i] = (e < nq) ? al(row0 + row, c0 + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int row = e / (KC / 4), k4 = e % (KC / 4);
+            if (c0 + 4 * k4 < ke) t4[i] = al.raw(row0 + row, c0 + 4 * k4);
         }
     };
-    auto store_chunk = [&](int c0, const float4* t4, int h, int cnt) {
-        const int q4 = min(KC, ke - c0) >> 2, nq = GBM * q4;
+    auto store_chunk = [&](int c0, const Raw* t4, int h, int cnt) {
 #pragma unroll
         for (int i = 0; i < cnt; ++i) {
             const int e = tid + (h + i) * AMP_WG;
-            const int row = e / q4, k4 = e - row * q4;
-            if (e < nq) *reinterpret_cast<float4*>(lds + row * LDA + 4 * k4) = t4[i];
+            const int row = e / (KC / 4), k4 = e % (KC / 4);
+            *reinterpret_cast<float4*>(lds + row * LDA + 4 * k4) = al.fin(t4[i], row0 + row, c0 + 4 * k4);
         }
     };
     if constexpr (PF) {
@@ -215,7 +233,7 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
             if (kc0 > kb) __syncthreads();   // every wave is done with the previous chunk
 #pragma unroll
             for (int h = 0; h < PER; h += PER / 2) {
-                float4 t4[PER / 2];
+                Raw t4[PER / 2];
                 load_chunk(kc0, t4, h, PER / 2);
                 store_chunk(kc0, t4, h, PER / 2);
             }

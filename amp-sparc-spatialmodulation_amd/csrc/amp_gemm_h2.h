@@ -189,27 +189,25 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
     for (int kc0 = kb; kc0 < ke; kc0 += H2KC) {
         const int kc = min(H2KC, ke - kc0);
         if (kc0 > kb) __syncthreads();                  // every wave done with the previous chunk
-        // stage PL planes x 32 rows x kc elements (16-byte loads, all in flight before the stores)
+        // stage PL planes x 32 rows x the chunk (16-byte loads, all in flight before the stores),
+        // with the full chunk's compile-time geometry (amp_gemm_x3.h): a tail chunk's columns past
+        // ke are not loaded (a masked load with no else-write) and never read
         {
-            const int q8 = kc >> 3;                     // 16-byte units per plane row
-            const int tot = PL * GBM * q8;
-            constexpr int CH = PL * GBM * (H2KC / 8) / AMP_WG;
+            constexpr int Q8 = H2KC / 8;                // 16-byte units per plane row
+            constexpr int CH = PL * GBM * Q8 / AMP_WG;
+            static_assert(CH * AMP_WG == PL * GBM * Q8, "whole chunk per workgroup");
             u32x4 v[CH];
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
                 const int e = tid + i * AMP_WG;
-                if (e < tot) {
-                    const int f = e / (GBM * q8), rem = e - f * GBM * q8, r = rem / q8, c8 = rem - r * q8;
-                    v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + kc0 + 8 * c8);
-                }
+                const int f = e / (GBM * Q8), rem = e % (GBM * Q8), r = rem / Q8, c8 = rem % Q8;
+                if (kc0 + 8 * c8 < ke) v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + kc0 + 8 * c8);
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) {
                 const int e = tid + i * AMP_WG;
-                if (e < tot) {
-                    const int f = e / (GBM * q8), rem = e - f * GBM * q8, r = rem / q8, c8 = rem - r * q8;
-                    *reinterpret_cast<u32x4*>(sP + (f * GBM + r) * H2LDK + pl_col(r, 8 * c8, H2SWM)) = v[i];
-                }
+                const int f = e / (GBM * Q8), rem = e % (GBM * Q8), r = rem / Q8, c8 = rem % Q8;
+                *reinterpret_cast<u32x4*>(sP + (f * GBM + r) * H2LDK + pl_col(r, 8 * c8, H2SWM)) = v[i];
             }
         }
         __syncthreads();

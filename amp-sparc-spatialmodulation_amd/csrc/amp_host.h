@@ -196,7 +196,7 @@ inline bool section_bn_wide_env() {
 inline int section_bn(const amp_dims* d) { return (2 * d->M <= 128 && !section_bn_wide_env()) ? 128 : 256; }
 
 // Expanded-weight builders (amp_weights.hip)
-enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2, WPACKX3 = 3, WPACKH2 = 4, WPACKH2_ABS2 = 5, WPACKI8 = 6 };
+enum { WPACK_NONE = 0, WPACK32 = 1, WPACK16 = 2, WPACKX3 = 3, WPACKH2 = 4, WPACKH2_ABS2 = 5, WPACKI8 = 6, WPACKX3_ABS2 = 7 };
 // X3 / H2: bf16x3 / fp16x2 planes of X, H2_ABS2: fp16x2 planes of the real |X|^2 (h2r_index),
 // I8: int8x4 digit planes of X with per-column exponents (i8_index); kap = J, ncp = O
 int build_cweight(const float2* src, long so, long sj, int conj, const float* rowscale, int O, int J,

@@ -69,6 +69,10 @@ struct ScampK {
     // tile of WA (128 wide) / WAH (bn wide) the reduction range holding its nonzero blocks
     const int* bandA;
     const int* bandB;
+    // launch engine, bf16x3 tiles (amp_gemm_x3.h, lx3 = 1): WA / WAH hold the x3-packed operators
+    // (x3_index), each GEMM's A rows split first into `lap` (six bf16 planes)
+    int lx3, rows_pad;
+    unsigned short* lap;
     XState* xs;            // trial-sharded exchange words (amp_scamp_run_sharded)
     // fused decision (amp_scamp_detect_count: decide_epilogue at the end of scamp_persist)
     int dec_on, ibits;
@@ -97,10 +101,14 @@ struct ScampWs {
     Partial* pparts;
     double* pxch;
     int *bandA, *bandB;
+    unsigned short* lap;
     XState* xs;
     DecWG* dwg;
     size_t bytes;
 };
+
+// the launch engine's bf16x3 tiles need whole 64-wide reduction groups and output tiles
+inline bool scamp_lx3_shape(const amp_dims* d) { return d->N % 64 == 0 && d->n % 64 == 0; }
 
 // 128 columns whenever a section fits (2M <= 128): twice the workgroups of a whole-coupling-
 // block tile (cfg3: 256 instead of 128).  A tile that does not hold whole coupling blocks
@@ -146,6 +154,8 @@ inline ScampWs scamp_carve(const amp_dims* d, int max_iter, void* base) {
     w.bandB = cv.take<int>((size_t)2 * (P.ncpB / P.bn));
     w.xs = cv.take<XState>(1);
     w.dwg = cv.take<DecWG>((size_t)2 * nwg);   // 256 B of granules per workgroup
+    w.lap = scamp_lx3_shape(d) ? cv.take<unsigned short>((size_t)6 * round_up(d->B, GBM) * std::max(d->N, d->n))
+                               : nullptr;
     w.bytes = cv.off;
     return w;
 }

@@ -13,6 +13,7 @@
 #include <atomic>
 #include <mutex>
 
+#include "amp_gemm_x3.h"
 #include "amp_scamp.h"
 
 namespace amp {
@@ -26,7 +27,10 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandA ? P.bandA[2 * tile.cb] : 0, ke = P.bandA ? P.bandA[2 * tile.cb + 1] : -1;
-    gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
+    if (KC != GKC && P.lx3)
+        gemm_tile_x3<128, true>(P.lap, P.rows_pad, P.N, P.WA, row0, col0, lds, kb, ke);
+    else
+        gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
     using C = GemmCfg<128, KC>;
     const float* psi = spsi(P, t + 1);               // psi of iteration t-1 (ones at t = 0)
     const float* phi_old = sphi(P, t + 1);           // +inf at t = 0 (scamp.py:19)
@@ -65,17 +69,15 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     float po[IT];
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
+        // unconditional loads at a clamped index (a lane-divergent branch around them serialises
+        // their latencies, amp_gemm.h ALoadPlain); out-of-range elements are never stored
         const int e = threadIdx.x + u * AMP_WG;
         const int rho = e >> 6, cp = e & 63;
-        const int row = row0 + rho, i = (col0 >> 1) + cp;
-        yv[u] = zv[u] = make_float2(0.f, 0.f);
-        po[u] = 1.f;
-        if (row < P.B && i < P.n) {
-            const size_t oc = (size_t)row * twon + 2 * i;
-            yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
-            zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
-            po[u] = phi_old[(size_t)row * P.Lout + i / P.Nr];
-        }
+        const int row = min(row0 + rho, P.B - 1), i = min((col0 >> 1) + cp, P.n - 1);
+        const size_t oc = (size_t)row * twon + 2 * i;
+        yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
+        zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
+        po[u] = phi_old[(size_t)row * P.Lout + i / P.Nr];
     }
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
@@ -136,7 +138,10 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandB ? P.bandB[2 * tile.cb] : 0, ke = P.bandB ? P.bandB[2 * tile.cb + 1] : -1;
-    gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
+    if ((BN == 256 || KC != GKC) && P.lx3)
+        gemm_tile_x3<BN, true>(P.lap, P.rows_pad, P.n, P.WAH, row0, col0, lds, kb, ke);
+    else
+        gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
     const int lc0 = (col0 / 2) / P.Nt, nlc = max(1, (ncols / 2) / P.Nt);   // coupling blocks in this tile
     // tau of the blocks this tile covers only (blocks lc0 .. lc0 + ntc - 1): each is written to
@@ -182,8 +187,9 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
         float xv[IT];
 #pragma unroll
         for (int u = 0; u < IT; ++u) {
-            const int e = threadIdx.x + u * AMP_WG, rho = e / BN, cc = e % BN;
-            xv[u] = (rho < nrows && cc < ncols) ? P.xm[(size_t)(row0 + rho) * twoN + col0 + cc] : 0.f;
+            // unconditional loads at a clamped index (see scamp_ka); out-of-range elements unused
+            const int e = threadIdx.x + u * AMP_WG, rho = min(e / BN, nrows - 1), cc = min(e % BN, ncols - 1);
+            xv[u] = P.xm[(size_t)(row0 + rho) * twoN + col0 + cc];
         }
 #pragma unroll
         for (int u = 0; u < IT; ++u) {
@@ -597,9 +603,23 @@ static bool scamp_short_chunks(const ScampK& P) {
     return P.bandA != nullptr && !off;
 }
 
+// the bf16x3 tiles run in the 128-wide short-chunk instantiations (their epilogues' LDS budget is
+// the 256-chunk A block) with the staged planes' 48 KB, the 256-wide kb in its GKC instantiation
+constexpr size_t SX3_LDS = x3_tile_lds<128, true>(GemmCfg<128, 256>::A_FLOATS - GemmCfg<128, 256>::CTILE_FLOATS);
+static_assert(x3_tile_lds<256, true>(0) <= GemmCfg<256>::LDS_BYTES, "bf16x3 planes within the 256-wide tile's LDS");
+
+// A rows -> six bf16 planes for the next bf16x3 GEMM (no-op launch once the loop has stopped)
+static void scamp_split(const ScampK& P, const float* a, int lda, int K, int t, hipStream_t st) {
+    const int wpr = (P.rows_pad / 4 < 2 * device_cu_count() && K >= 1024) ? 4 : 1;
+    hipLaunchKernelGGL(x3_split_rows_kernel<true>, dim3(P.rows_pad * wpr / 4), dim3(256), 0, st, a, lda, P.B,
+                       P.rows_pad, K, P.lap, &P.iters[t].stopped, wpr);
+}
+
 template <int KK>
 static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
-    if (P.bn == 128 && scamp_short_chunks(P))
+    if (P.bn == 128 && P.lx3)
+        hipLaunchKernelGGL((scamp_kb<128, KK, 256>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
+    else if (P.bn == 128 && scamp_short_chunks(P))
         hipLaunchKernelGGL((scamp_kb<128, KK, 256>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SKC_LDS,
                            st, P, t);
     else if (P.bn == 128)
@@ -609,13 +629,17 @@ static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_
 }
 
 static void launch_ka(const ScampK& P, int gr, int t, hipStream_t st) {
-    if (scamp_short_chunks(P))
+    if (P.lx3) {
+        scamp_split(P, P.xm, 2 * P.N, P.N, t, st);
+        hipLaunchKernelGGL(scamp_ka<256>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
+    } else if (scamp_short_chunks(P))
         hipLaunchKernelGGL(scamp_ka<256>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), SKC_LDS, st, P, t);
     else
         hipLaunchKernelGGL(scamp_ka<GKC>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), GemmCfg<128>::LDS_BYTES, st, P, t);
 }
 
 static void launch_kb(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
+    if (P.lx3) scamp_split(P, P.s, 2 * P.n, P.n, t, st);
     switch (P.c.K) {
     case 1: launch_kb_kk<1>(P, gr, ldsB, t, st); break;
     case 2: launch_kb_kk<2>(P, gr, ldsB, t, st); break;
@@ -724,14 +748,25 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     P.c = to_const(c);
     c64 = to_const64(c);
     AMP_REQUIRE(a->gemm >= AMP_GEMM_AUTO && a->gemm <= AMP_GEMM_H2, "amp_scamp: gemm %d", a->gemm);
-    const bool fits = scamp_persist_x3_fits(d);
-    AMP_REQUIRE((a->gemm != AMP_GEMM_X3 && a->gemm != AMP_GEMM_H2) || fits,
-                "amp_scamp: the split-precision engine's LDS carve exceeds 160 KB");
+    const bool fits = scamp_persist_x3_fits(d), lx3ok = scamp_lx3_shape(d);
+    AMP_REQUIRE(a->gemm != AMP_GEMM_H2 || fits, "amp_scamp: the split-precision engine's LDS carve exceeds 160 KB");
+    AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || fits || lx3ok,
+                "amp_scamp: bf16x3 needs the persistent engine's LDS carve within 160 KB or, on the launch engine, "
+                "N %% 64 == 0 and n %% 64 == 0 (N = %d, n = %d)", d->N, d->n);
+    // launch engine: bf16x3 tiles when asked for (AMP_GEMM_X3) or, under AUTO, with
+    // AMP_SCAMP_LAUNCH_GEMM=x3; f32 MFMA tiles otherwise
+    static const bool lx3_env = [] {
+        const char* e = getenv("AMP_SCAMP_LAUNCH_GEMM");
+        return e && e[0] == 'x';
+    }();
+    P.lx3 = lx3ok && (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && lx3_env)) ? 1 : 0;
+    P.rows_pad = round_up(d->B, GBM);
+    P.lap = w.lap;
     // 0 f32 MFMA, 1 bf16x3, 2 fp16x2.  AUTO keeps bf16x3 for SCAMP: with fp16x2 one cfg3 golden
     // (QPSK, 7 dB, seed 1) never meets the psi allclose exit (T 20 vs the reference's 6, VER / SER
     // equal): at nMSE 1e-9 psi is ~1e-9 and torch.allclose's atol 1e-8 decides, which the
     // fp16x2 products' 2^-22 terms move.  AMP_SCAMP_GEMM=f32 / h2 for A/B runs.
-    P.x3 = a->gemm == AMP_GEMM_H2 ? 2 : a->gemm == AMP_GEMM_X3 ? 1 : a->gemm == AMP_GEMM_F32 || !fits ? 0
+    P.x3 = a->gemm == AMP_GEMM_H2 ? 2 : a->gemm == AMP_GEMM_X3 ? (fits ? 1 : 0) : a->gemm == AMP_GEMM_F32 || !fits ? 0
          : scamp_gemm_f32_requested() ? 0 : scamp_gemm_h2_requested() ? 2 : 1;
     return AMP_OK;
 }
@@ -761,9 +796,23 @@ static int scamp_persist_prepare(ScampK& P, const amp_scamp_args* a, hipStream_t
 static int scamp_prepare_impl(const ScampK& P, const amp_scamp_args* a, hipStream_t st) {
     int rc;
     const float2* A = (const float2*)a->A;
+    if (P.lx3) {
+        // bf16x3 planes (x3_index) in the f32 weights' buffers (12 of their 16 bytes per entry):
+        // A x (O = n, J = N), A^H s (O = N, J = n)
+        CWeightJob j[2];
+        j[0] = CWeightJob{A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.N, P.n, WPACKX3, 0};
+        j[1] = CWeightJob{A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WAH, P.n, P.N, WPACKX3, 0};
+        if ((rc = build_cweights(j, 2, nullptr, 0, st))) return rc;
+        if (P.bandA) {
+            if ((rc = h2_kband(P.WA, 6, P.N / 32, 4, P.ncpA / 128, P.n / 16, const_cast<int*>(P.bandA), st))) return rc;
+            if ((rc = h2_kband(P.WAH, 6, P.n / 32, P.bn / 32, P.ncpB / P.bn, P.N / 16, const_cast<int*>(P.bandB), st)))
+                return rc;
+        }
+    } else {
     if ((rc = build_cweight(A, P.N, 1, 0, nullptr, P.n, P.N, (float*)P.WA, P.kapA, P.ncpA, st))) return rc;
     if ((rc = build_cweight(A, 1, P.N, 1, nullptr, P.N, P.n, (float*)P.WAH, P.kapB, P.ncpB, st))) return rc;
-    if (P.bandA) {
+    }
+    if (P.bandA && !P.lx3) {
         if ((rc = weight_kband(P.WA, P.kapA, P.ncpA, 128, const_cast<int*>(P.bandA), st))) return rc;
         if ((rc = weight_kband(P.WAH, P.kapB, P.ncpB, P.bn, const_cast<int*>(P.bandB), st))) return rc;
     }
@@ -871,6 +920,8 @@ int amp_scamp_run(const amp_dims* d, const amp_constellation* c, const amp_scamp
                 "amp_scamp_run: persistent engine needs (2N, 2n) in {(128, 256), (256, 512), (256, 256)}, M <= 64 "
                 "and ceil(B/16) = %d <= %d CUs", cdiv(d->B, 16), device_cu_count());
     if (a->engine == AMP_ENGINE_PERSISTENT || (a->engine == AMP_ENGINE_AUTO && elig)) {
+        AMP_REQUIRE(a->gemm != AMP_GEMM_X3 || scamp_persist_x3_fits(d),
+                    "amp_scamp_run: the persistent bf16x3 engine's LDS carve exceeds 160 KB");
         if ((rc = scamp_persist_prepare(P, a, st))) return rc;
         DecConst dc;
         static_cast<Const64&>(dc) = c64;   // no decision in this launch: only the float64 table is read

@@ -35,18 +35,26 @@ __global__ __launch_bounds__(RWG) void vamp_init_scalars(VampK P) {
 }
 
 // r~ = (xmmse - dxdr * r) * normScalar (vamp.py:91), formed while loading GEMM1's A tile.
+// Staged in two steps like ALoadPlain (amp_gemm.h): both loads at a clamped address, the formula
+// and the zeroing of out-of-range elements at the LDS store.
 struct ALoadRt {
     const float* __restrict__ xm;
     const float* __restrict__ r;
     int lda, rows, ka;
     float dxdr, ns;
-    __device__ __forceinline__ float4 operator()(int row, int k) const {
-        if (row >= rows || k >= ka) return make_float4(0.f, 0.f, 0.f, 0.f);
-        const size_t o = (size_t)row * lda + k;
-        const float4 x = *reinterpret_cast<const float4*>(xm + o);
-        const float4 q = *reinterpret_cast<const float4*>(r + o);
-        return make_float4((x.x - dxdr * q.x) * ns, (x.y - dxdr * q.y) * ns, (x.z - dxdr * q.z) * ns,
-                           (x.w - dxdr * q.w) * ns);
+    struct Raw {
+        float4 x, q;
+    };
+    __device__ __forceinline__ Raw raw(int row, int k) const {
+        const size_t o = (size_t)min(row, rows - 1) * lda + min(k, ka - 4);
+        return Raw{*reinterpret_cast<const float4*>(xm + o), *reinterpret_cast<const float4*>(r + o)};
+    }
+    __device__ __forceinline__ float4 fin(const Raw& v, int row, int k) const {
+        const bool ok = row < rows && k < ka;
+        const float4 x = v.x, q = v.q;
+        const float4 f = make_float4((x.x - dxdr * q.x) * ns, (x.y - dxdr * q.y) * ns, (x.z - dxdr * q.z) * ns,
+                                     (x.w - dxdr * q.w) * ns);
+        return ok ? f : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 };
 

@@ -245,6 +245,26 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
         }
         return;
     }
+    if (J.packed == WPACKX3_ABS2) {
+        // bf16x3 planes of the real |X|^2 (torch's complex abs, the correctly rounded hypot, then an
+        // f32 square: bamp.py:18 `H.abs()**2`) for gemm_tile_x3 (amp_gemm_x3.h)
+        unsigned short* w3 = reinterpret_cast<unsigned short*>(J.wt);
+        const long tot = (long)J.ncp * J.kap;
+        for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+            const int o = (int)(e / J.kap), j = (int)(e % J.kap);
+            float v = 0.f;
+            if (o < J.O && j < J.J) {
+                const float2 z = J.src[o * J.so + j * J.sj];
+                const float a = (float)sqrt((double)z.x * z.x + (double)z.y * z.y);
+                v = a * a;
+            }
+            unsigned p[3];
+            split3(v, p[0], p[1], p[2]);
+#pragma unroll
+            for (int f = 0; f < 3; ++f) w3[x3r_index(o, j, f, J.kap)] = (unsigned short)p[f];
+        }
+        return;
+    }
     const long total = (long)(J.ncp / 2) * (J.kap / 2);
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const int o = (int)(e / (J.kap / 2)), j = (int)(e % (J.kap / 2));
@@ -273,7 +293,7 @@ int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero,
     for (int i = 0; i < njobs; ++i) {
         const CWeightJob& J = jobs[i];
         const bool planar = J.packed == WPACKX3 || J.packed == WPACKH2 || J.packed == WPACKH2_ABS2 ||
-                            J.packed == WPACKI8;
+                            J.packed == WPACKI8 || J.packed == WPACKX3_ABS2;
         AMP_REQUIRE((planar ? J.J <= J.kap && J.O <= J.ncp : 2 * J.J <= J.kap && 2 * J.O <= J.ncp) &&
                         (J.packed == WPACK_NONE || (J.packed == WPACK32 && J.kap % GBK == 0 && J.ncp % 128 == 0) ||
                          (J.packed == WPACK16 && J.kap % 16 == 0 && J.ncp % 16 == 0) ||
@@ -396,14 +416,20 @@ __global__ __launch_bounds__(256) void h2_kband_fin(int* __restrict__ band, int 
     band[2 * t + 1] = hi < 0 ? 0 : 32 * ((hi | 1) + 1);
 }
 
-// h2_kband_kernel over an h2-packed operator (PL planes, G 32-groups per 16-output tile, tpt
-// 16-output tiles per GEMM column tile, ntiles column tiles, n16 packed 16-output tiles): [kb, ke)
-// per column tile.
+// h2_kband_kernel over a plane-packed operator (PL 16-bit planes: fp16x2 2 / 4, bf16x3 3 / 6; G
+// 32-groups per 16-output tile, tpt 16-output tiles per GEMM column tile, ntiles column tiles, n16
+// packed 16-output tiles): [kb, ke) per column tile.
 int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* band, hipStream_t st) {
-    AMP_REQUIRE(G % 2 == 0 && (PL == 2 || PL == 4), "h2_kband: G %d / PL %d", G, PL);
+    AMP_REQUIRE(G % 2 == 0 && (PL == 2 || PL == 3 || PL == 4 || PL == 6), "h2_kband: G %d / PL %d", G, PL);
     const int gps = 64;
     hipLaunchKernelGGL(weight_kband_init, dim3(cdiv(ntiles, 256)), dim3(256), 0, st, band, ntiles, G);
-    if (PL == 4)
+    if (PL == 6)
+        hipLaunchKernelGGL(h2_kband_kernel<6>, dim3(ntiles, cdiv(G, gps)), dim3(256), 0, st, (const u32x4*)wq, G, tpt,
+                           gps, n16, band);
+    else if (PL == 3)
+        hipLaunchKernelGGL(h2_kband_kernel<3>, dim3(ntiles, cdiv(G, gps)), dim3(256), 0, st, (const u32x4*)wq, G, tpt,
+                           gps, n16, band);
+    else if (PL == 4)
         hipLaunchKernelGGL(h2_kband_kernel<4>, dim3(ntiles, cdiv(G, gps)), dim3(256), 0, st, (const u32x4*)wq, G, tpt,
                            gps, n16, band);
     else

@@ -150,6 +150,75 @@ def test_scamp_x3_matches_f32(device, alph, ebn0, split):
         assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
 
 
+@pytest.mark.parametrize('ebn0', [0.0, 8.0])
+@pytest.mark.parametrize('alph', ['QPSK', '16QAM'])
+@pytest.mark.parametrize('split', ['x3', 'h2'])
+def test_bamp_split_matches_f32(device, alph, ebn0, split):
+    """BAMP's split-precision launch tiles (bf16x3 amp_gemm_x3.h, fp16x2 amp_gemm_h2.h) against
+    its f32-MFMA tiles (N = 1024, n = 256, B = 1024): after one and three iterations xmap agrees
+    to float32 GEMM summation-order noise, the full detection to T within one and the counting
+    metrics within 1e-3."""
+    import torch
+    import amp_native as nat
+    from bamp import BAMP
+    sg = nat.GEMM_X3 if split == 'x3' else nat.GEMM_H2
+    inp = None
+    for iters in (1, 3):
+        cfg = _config(128, 8, 256, 1024, alph, iterations=iters)
+        if inp is None:
+            inp = _regen_inputs(cfg, 0, ebn0, svd=False)
+        xs = []
+        for gemm in (nat.GEMM_F32, sg):
+            T = BAMP(cfg, gemm=gemm).detect(inp['A'], inp['y'], inp['SNR'])
+            xs.append(T.xmap.clone())
+        scale = float(torch.nan_to_num(xs[0]).abs().max())
+        assert torch.allclose(xs[0], xs[1], rtol=0, atol=4e-6 * scale, equal_nan=True), \
+            (iters, float((xs[0] - xs[1]).abs().nan_to_num().max()), scale)
+    cfg = _config(128, 8, 256, 1024, alph, iterations=20)
+    outs = []
+    for gemm in (nat.GEMM_F32, sg):
+        L = BAMP(cfg, gemm=gemm)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        outs.append({k: float(np.asarray(v)) for k, v in L.loss.items()})
+    a, b = outs
+    assert abs(a['T'] - b['T']) <= 1, (a['T'], b['T'])
+    for k in ('ver', 'ser', 'fer', 'ier'):
+        assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
+
+
+@pytest.mark.parametrize('ebn0', [0.0, 8.0])
+@pytest.mark.parametrize('alph', ['QPSK', '16QAM'])
+def test_scamp_launch_x3_matches_f32(device, alph, ebn0):
+    """SCAMP's launch engine on bf16x3 tiles (amp_gemm_x3.h) against its f32-MFMA tiles at cfg3
+    (N = 1024, n = 256): after one and three iterations xmap agrees to float32 GEMM summation-order
+    noise, the full detection to T within one and the counting metrics within 1e-3."""
+    import torch
+    import amp_native as nat
+    from scamp import SCAMP
+    inp = None
+    for iters in (1, 3):
+        cfg = _config(128, 8, 256, 4096, alph, iterations=iters)
+        if inp is None:
+            inp = _regen_inputs(cfg, 0, ebn0, svd=False)
+        xs = []
+        for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+            det = SCAMP(cfg, engine=nat.ENGINE_LAUNCHES, gemm=gemm)
+            det.detect(inp['W'], inp['A'], inp['y'], inp['SNR'])
+            xs.append(det.xmap.clone())
+        scale = float(torch.nan_to_num(xs[0]).abs().max())
+        assert torch.allclose(xs[0], xs[1], rtol=0, atol=4e-6 * scale, equal_nan=True), \
+            (iters, float((xs[0] - xs[1]).abs().nan_to_num().max()), scale)
+    cfg = _config(128, 8, 256, 4096, alph, iterations=20)
+    outs = []
+    for gemm in (nat.GEMM_F32, nat.GEMM_X3):
+        L = SCAMP(cfg, engine=nat.ENGINE_LAUNCHES, gemm=gemm)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'],
+                                                              inp['sym'], inp['idx'])
+        outs.append({k: float(np.asarray(v)) for k, v in L.loss.items()})
+    a, b = outs
+    assert abs(a['T'] - b['T']) <= 1, (a['T'], b['T'])
+    for k in ('ver', 'ser', 'fer', 'ier'):
+        assert abs(a[k] - b[k]) <= 1e-3, (k, a[k], b[k])
+
+
 @pytest.mark.parametrize('ebn0', [0.0, 4.0, 8.0, 20.0])
 @pytest.mark.parametrize('alph', ['QPSK', '16QAM'])
 def test_scamp_engines_agree(device, alph, ebn0):

@@ -13,12 +13,15 @@ from test_gpu_vamp import _check_T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('gemm', ['auto', 'h2'])
+GEMMS = {'auto': 0, 'h2': 3, 'x3': 2}   # amp_native GEMM_AUTO / GEMM_H2 / GEMM_X3
+
+
+@pytest.mark.parametrize('gemm', sorted(GEMMS))
 @pytest.mark.parametrize('name,key', g6_points())
 def test_cfg5_correlated_curve_point(device, name, key, gemm):
-    """Both GEMM arithmetics of BAMP's launch engine: 'auto' is the exact-f32 MFMA GEMM (the
-    reference's operand precision), 'h2' the opt-in fp16x2 tile GEMM (amp_gemm_h2.h, 22-bit
-    operands)."""
+    """Every GEMM arithmetic of BAMP's launch engine: 'auto' is the f32 MFMA GEMM (the reference's
+    operand precision), 'x3' the bf16x3 tile GEMM (amp_gemm_x3.h, 24-bit operands), 'h2' the opt-in
+    fp16x2 tile GEMM (amp_gemm_h2.h, 22-bit operands)."""
     import amp_native as nat
     from bamp import BAMP
     ent = g6_curves()[name]
@@ -29,8 +32,8 @@ def test_cfg5_correlated_curve_point(device, name, key, gemm):
     if 'SNR' in ref:
         assert inp['SNR'] == pytest.approx(ref['SNR'], rel=1e-12)
     mv = lambda t: t.to(device)  # noqa: E731
-    L = BAMP(cfg, gemm=nat.GEMM_AUTO if gemm == 'auto' else nat.GEMM_H2)(mv(inp['A']), mv(inp['y']), inp['SNR'],
-                                                                        mv(inp['x']), inp['sym'], inp['idx'])
+    assert (nat.GEMM_AUTO, nat.GEMM_H2, nat.GEMM_X3) == (GEMMS['auto'], GEMMS['h2'], GEMMS['x3'])
+    L = BAMP(cfg, gemm=GEMMS[gemm])(mv(inp['A']), mv(inp['y']), inp['SNR'], mv(inp['x']), inp['sym'], inp['idx'])
     got = L.loss
     assert abs(float(got['ver']) - ref['ver']) <= 1e-3, (float(got['ver']), ref['ver'])
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])

@@ -18,8 +18,16 @@ from test_gpu_vamp import _check_T
 
 pytestmark = pytest.mark.gpu
 
-ISI_CASES = [(n, k, e) for (n, k) in g11_points()
-             for e in ((1, 2) if g11()[n]['algo'] == 'vamp' else (0,))]
+def _engines(ent):
+    """VAMP: both engines; BAMP and SCAMP: the default GEMM and, where the shape tiles
+    (N % 64 == 0 and n % 64 == 0), the bf16x3 launch tiles on the block-banded operator ('x3')."""
+    if ent['algo'] == 'vamp':
+        return (1, 2)
+    N, n = ent['Nt'] * ent['Lin'], ent['Nr'] * (ent['Lin'] + ent['Lh'] - 1)
+    return (0, 'x3') if N % 64 == 0 and n % 64 == 0 else (0,)
+
+
+ISI_CASES = [(n, k, e) for (n, k) in g11_points() for e in _engines(g11()[n])]
 
 
 @pytest.mark.parametrize('name,key,engine', ISI_CASES)
@@ -37,9 +45,13 @@ def test_isi_curve_point(device, name, key, engine):
         L = VAMP(cfg, engine=engine)(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'],
                                      inp['idx'])
     elif ent['algo'] == 'bamp':
-        L = BAMP(cfg)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        import amp_native as nat
+        gemm = nat.GEMM_X3 if engine == 'x3' else nat.GEMM_AUTO
+        L = BAMP(cfg, gemm=gemm)(inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
     else:
-        L = SCAMP(cfg)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+        import amp_native as nat
+        gemm = nat.GEMM_X3 if engine == 'x3' else nat.GEMM_AUTO
+        L = SCAMP(cfg, gemm=gemm)(inp['W'], inp['A'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
     got = L.loss
     for k in ('ver', 'ser'):                       # the north-star bar
         assert abs(float(got[k]) - ref[k]) <= 1e-3, (k, float(got[k]), ref[k])
