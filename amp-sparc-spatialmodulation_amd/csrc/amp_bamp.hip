@@ -196,13 +196,13 @@ __device__ __forceinline__ int bke(const BampK& P, int w, int cb) { return P.ban
 // need no longer chunks: 33 KB of LDS, four tiles per CU instead of two; the fp16x2 tile only in
 // the GKC instantiations).  The chunking does not change the MFMA order: the same bits.
 // v = |H|^2 var (bamp.py:59)
-template <int KC = GKC>
+template <int KC = GKC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (KC == GKC && P.x3)
+    if constexpr (X3)
         gemm_tile_x3<128, false>(P.ap, P.rows_pad, P.N, P.Wabs2, row0, col0, lds, bkb(P, 0, tile.cb), bke(P, 0, tile.cb));
     else if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.N, P.Wabs2, BH2_EX, row0, col0, lds, bkb(P, 0, tile.cb),
@@ -219,14 +219,14 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka1(BampK P, int t) {
 }
 
 // z = H xmmse - v (y - z) / u ; u = v + sigma2 ; s = (y - z) / u   (bamp.py:60-63)
-template <int KC = GKC>
+template <int KC = GKC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (KC == GKC && P.x3)
+    if constexpr (X3)
         gemm_tile_x3<128, true>(P.ap, P.rows_pad, P.N, P.WH, row0, col0, lds, bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     else if (KC == GKC && P.h2)
         gemm_tile_h2<128, true>(P.ap, P.rows_pad, P.rexp, P.N, P.WH, BH2_EX, row0, col0, lds, bkb(P, 1, tile.cb),
@@ -276,13 +276,13 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
 }
 
 // cov = 1 / (|H|^2^T (1/u))   (bamp.py:62)
-template <int KC = GKC>
+template <int KC = GKC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb1(BampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
     const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
-    if (KC == GKC && P.x3)
+    if constexpr (X3)
         gemm_tile_x3<128, false>(P.ap, P.rows_pad, P.n, P.Wabs2T, row0, col0, lds, bkb(P, 2, tile.cb), bke(P, 2, tile.cb));
     else if (KC == GKC && P.h2)
         gemm_tile_h2<128, false>(P.ap, P.rows_pad, P.rexp, P.n, P.Wabs2T, BH2_EX, row0, col0, lds, bkb(P, 2, tile.cb),
@@ -331,7 +331,7 @@ struct BampDenoisePolicy {
 };
 
 // xmap = xmmse + cov (H^H s) ; xmmse, var = denoiser(xmap, cov/2)   (bamp.py:63-64)
-template <int BN, int KK, int KC = GKC>
+template <int BN, int KK, int KC = GKC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_kb2(BampK P, Const64 c64, int t) 
     const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
-    if (KC == GKC && P.x3)
+    if constexpr (X3)
         gemm_tile_x3<BN, true>(P.ap, P.rows_pad, P.n, P.WHH, row0, col0, lds, bkb(P, 3, tile.cb), bke(P, 3, tile.cb));
     else if (KC == GKC && P.h2)
         gemm_tile_h2<BN, true>(P.ap, P.rows_pad, P.rexp, P.n, P.WHH, BH2_EX, row0, col0, lds, bkb(P, 3, tile.cb),
@@ -734,6 +734,7 @@ static int bamp_lds_attr(const void* fn) {
 template <int KK>
 static int bamp_kb2_attrs() {
     int rc = bamp_lds_attr((const void*)bamp_kb2<128, KK>);
+    if (!rc) rc = bamp_lds_attr((const void*)bamp_kb2<256, KK, GKC, true>);
     return rc ? rc : bamp_lds_attr((const void*)bamp_kb2<256, KK>);   // the KC = 256 forms fit the default 64 KB
 }
 
@@ -755,12 +756,19 @@ static void launch_kb2_kk(const BampK& P, const Const64& c64, int gr, int t, hip
         hipLaunchKernelGGL((bamp_kb2<128, KK, 256>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BSKC_LDS, st, P, c64, t);
         return;
     }
-    if (P.bn == 128)
-        hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG),
-                           P.x3 ? xlds_kb2<128>() : BLDS, st, P, c64, t);
-    else
-        hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG),
-                           P.x3 ? xlds_kb2<256>() : BLDS, st, P, c64, t);
+    if (P.bn == 128) {
+        if (P.x3)
+            hipLaunchKernelGGL((bamp_kb2<128, KK, GKC, true>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), xlds_kb2<128>(), st,
+                               P, c64, t);
+        else
+            hipLaunchKernelGGL((bamp_kb2<128, KK>), dim3(gr, P.ncpB2 / 128), dim3(AMP_WG), BLDS, st, P, c64, t);
+    } else {
+        if (P.x3)
+            hipLaunchKernelGGL((bamp_kb2<256, KK, GKC, true>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), xlds_kb2<256>(), st,
+                               P, c64, t);
+        else
+            hipLaunchKernelGGL((bamp_kb2<256, KK>), dim3(gr, P.ncpB2 / 256), dim3(AMP_WG), BLDS, st, P, c64, t);
+    }
 }
 
 static void launch_kb2(const BampK& P, const Const64& c64, int gr, int t, hipStream_t st) {
@@ -961,13 +969,16 @@ static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st
     if (P.h2 || P.x3) bamp_split(P, ((t + 1) & 1) ? P.var1 : P.var0, P.N, P.N, false, t, st);
     const bool skc = bamp_short_chunks(P);
     if (skc) hipLaunchKernelGGL((bamp_ka1<256>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_ka1<>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), P.x3 ? XLDS_R : BLDS, st, P, t);
+    else if (P.x3) hipLaunchKernelGGL((bamp_ka1<GKC, true>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), XLDS_R, st, P, t);
+    else hipLaunchKernelGGL((bamp_ka1<>), dim3(gr, P.ncpA1 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2 || P.x3) bamp_split(P, P.xm, 2 * P.N, P.N, true, t, st);
     if (skc) hipLaunchKernelGGL((bamp_ka2<256>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_ka2<>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), P.x3 ? XLDS_C : BLDS, st, P, t);
+    else if (P.x3) hipLaunchKernelGGL((bamp_ka2<GKC, true>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), XLDS_C, st, P, t);
+    else hipLaunchKernelGGL((bamp_ka2<>), dim3(gr, P.ncpA2 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2 || P.x3) bamp_split(P, P.invu, P.n, P.n, false, t, st);
     if (skc) hipLaunchKernelGGL((bamp_kb1<256>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BSKC_LDS, st, P, t);
-    else hipLaunchKernelGGL((bamp_kb1<>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), P.x3 ? XLDS_R : BLDS, st, P, t);
+    else if (P.x3) hipLaunchKernelGGL((bamp_kb1<GKC, true>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), XLDS_R, st, P, t);
+    else hipLaunchKernelGGL((bamp_kb1<>), dim3(gr, P.ncpB1 / 128), dim3(AMP_WG), BLDS, st, P, t);
     if (P.h2 || P.x3) bamp_split(P, P.s, 2 * P.n, P.n, true, t, st);
     launch_kb2(P, c64, gr, t, st);
 }
@@ -978,7 +989,7 @@ static void bamp_gemms(const BampK& P, const Const64& c64, int t, hipStream_t st
 static int bamp_iterate_impl(const BampK& P, const Const64& c64, int t, hipStream_t st) {
     bamp_gemms(P, c64, t, st);
     hipLaunchKernelGGL(bamp_r, dim3(1), dim3(BRWG), 0, st, P, c64, t);
-    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
+    const int nfix = fix_grid(P.nblk, P.B * P.L);
     hipLaunchKernelGGL(bamp_fixall, dim3(nfix), dim3(AMP_WG), 0, st, P, c64, t);
     AMP_LAUNCH_CHECK("bamp iteration");
     return AMP_OK;

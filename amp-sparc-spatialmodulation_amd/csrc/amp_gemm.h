@@ -196,9 +196,10 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
     // A chunk staging: all loads of a batch in flight before its LDS stores.  Short chunks
     // (KC <= 256: 8 float4 per thread) load the NEXT chunk into registers while this one's MFMAs
     // run; 512-wide chunks stage in two half-batches between the chunks.  Every chunk is staged
-    // with the full chunk's compile-time geometry (AL::raw / fin): a tail chunk's columns past ke
-    // are not loaded (a masked load with no else-write: nothing waits on it) and land in LDS as
-    // whatever the registers held, but no group reads them.
+    // with the full chunk's compile-time geometry and no branch (AL::raw / fin): a tail chunk's
+    // columns past ke are loaded at clamped addresses and land in LDS, but no group reads them.
+    // (Masking those loads instead put the staging back inside branches, where the compiler
+    // drains the weight ring before the stores: cfg5 BAMP 18.3 -> 20.5 ms, same box.)
     constexpr int PER = GBM * (KC / 4) / AMP_WG;    // float4 per thread for a full chunk
     constexpr bool PF = PER <= 8;
     using Raw = typename AL::Raw;
@@ -208,7 +209,7 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
         for (int i = 0; i < cnt; ++i) {
             const int e = tid + (h + i) * AMP_WG;
             const int row = e / (KC / 4), k4 = e % (KC / 4);
-            if (c0 + 4 * k4 < ke) t4[i] = al.raw(row0 + row, c0 + 4 * k4);
+            t4[i] = al.raw(row0 + row, c0 + 4 * k4);
         }
     };
     auto store_chunk = [&](int c0, const Raw* t4, int h, int cnt) {

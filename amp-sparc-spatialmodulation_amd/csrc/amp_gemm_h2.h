@@ -190,8 +190,8 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
         const int kc = min(H2KC, ke - kc0);
         if (kc0 > kb) __syncthreads();                  // every wave done with the previous chunk
         // stage PL planes x 32 rows x the chunk (16-byte loads, all in flight before the stores),
-        // with the full chunk's compile-time geometry (amp_gemm_x3.h): a tail chunk's columns past
-        // ke are not loaded (a masked load with no else-write) and never read
+        // with the full chunk's compile-time geometry and no branch (amp_gemm_x3.h): a tail chunk's
+        // columns past ke are loaded at clamped addresses and never read
         {
             constexpr int Q8 = H2KC / 8;                // 16-byte units per plane row
             constexpr int CH = PL * GBM * Q8 / AMP_WG;
@@ -201,7 +201,7 @@ __device__ __forceinline__ void gemm_tile_h2(const unsigned short* __restrict__ 
             for (int i = 0; i < CH; ++i) {
                 const int e = tid + i * AMP_WG;
                 const int f = e / (GBM * Q8), rem = e % (GBM * Q8), r = rem / Q8, c8 = rem % Q8;
-                if (kc0 + 8 * c8 < ke) v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + kc0 + 8 * c8);
+                v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + min(kc0 + 8 * c8, K - 8));
             }
 #pragma unroll
             for (int i = 0; i < CH; ++i) {

@@ -175,8 +175,8 @@ __device__ __forceinline__ void gemm_tile_x3(const unsigned short* __restrict__ 
     // while this chunk's MFMAs issue, and land in LDS after them (the f32 tile's short-chunk
     // scheme, amp_gemm.h).  Every chunk is staged with the full chunk's compile-time geometry (no
     // divisions, no per-element guards: straight-line code keeps every vmcnt wait counted, so the
-    // weight ring stays in flight across the stores); a tail chunk's columns past ke are not
-    // loaded (a masked load with no else-write: nothing waits on it) and never read.
+    // weight ring stays in flight across the stores); a tail chunk's columns past ke are loaded
+    // at clamped addresses and never read.
     constexpr int CH = PL * GBM * (X3KC / 8) / AMP_WG;   // 16-byte units per thread
     static_assert(CH * AMP_WG == PL * GBM * (X3KC / 8), "whole chunk per workgroup");
     u32x4 v[CH];
@@ -185,7 +185,7 @@ __device__ __forceinline__ void gemm_tile_x3(const unsigned short* __restrict__ 
         for (int i = 0; i < CH; ++i) {
             const int e = tid + i * AMP_WG;
             const int f = e / (GBM * (X3KC / 8)), rem = e % (GBM * (X3KC / 8)), r = rem / (X3KC / 8), c8 = rem % (X3KC / 8);
-            if (c0 + 8 * c8 < ke) v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + c0 + 8 * c8);
+            v[i] = *reinterpret_cast<const u32x4*>(planes + f * ps + (size_t)(row0 + r) * K + min(c0 + 8 * c8, K - 8));
         }
     };
     auto store_chunk = [&]() {

@@ -234,6 +234,12 @@ int build_abs2_weight(const float2* src, long so, long sj, int O, int J, float* 
 // the tile is all zero).  One pass over the weight (amp_weights.hip).
 int weight_kband(const float* wp, int kap, int ncp, int BN, int* band, hipStream_t st);
 int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* band, hipStream_t st);
+
+// Grid of the launch engines' rare-path fix-up launches (grid-stride over `work` sections, one
+// count slot per workgroup within the iteration's nblk partial slots): at most two workgroups per
+// CU, since the launch runs every iteration and is a no-op unless a fix-up is pending, when its
+// cost is the dispatch of its workgroups (4096 of them took 27 us at cfg5).
+int fix_grid(int nblk, int work);
 template <int BN>
 int set_lds_attr(const void* fn);
 int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,

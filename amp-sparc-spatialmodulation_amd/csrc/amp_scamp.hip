@@ -19,7 +19,9 @@
 namespace amp {
 
 // z = y - A xmmse + b z ; phi = sigma2 + gamma ; s = z / phi   (scamp.py:45-51, 57)
-template <int KC>
+// X3: the bf16x3 tile (amp_gemm_x3.h) in an instantiation of its own, so the f32 tiles keep their
+// register budget (one instantiation holding both ran the f32 ISI shape 25 % slower)
+template <int KC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -27,7 +29,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_ka(ScampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandA ? P.bandA[2 * tile.cb] : 0, ke = P.bandA ? P.bandA[2 * tile.cb + 1] : -1;
-    if (KC != GKC && P.lx3)
+    if constexpr (X3)
         gemm_tile_x3<128, true>(P.lap, P.rows_pad, P.N, P.WA, row0, col0, lds, kb, ke);
     else
         gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WA, P.kapA, row0, col0, lds, kb, ke);
@@ -129,7 +131,7 @@ struct ScampDenoisePolicy {
 };
 
 // tau = L / (W^T (1/phi)) / Mr ; xmap = xmmse + tau (A^H s) ; xmmse = denoiser ; psi   (scamp.py:53-59)
-template <int BN, int KK, int KC = GKC>
+template <int BN, int KK, int KC = GKC, bool X3 = false>
 __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     if (P.iters[t].stopped) return;
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(AMP_WG) void scamp_kb(ScampK P, int t) {
     const int row0 = tile.rb * GBM, col0 = tile.cb * BN;
     const int twoN = 2 * P.N, twon = 2 * P.n;
     const int kb = P.bandB ? P.bandB[2 * tile.cb] : 0, ke = P.bandB ? P.bandB[2 * tile.cb + 1] : -1;
-    if ((BN == 256 || KC != GKC) && P.lx3)
+    if constexpr (X3)
         gemm_tile_x3<BN, true>(P.lap, P.rows_pad, P.n, P.WAH, row0, col0, lds, kb, ke);
     else
         gemm_tile<BN, ALoadPlain, KC>(ALoadPlain{P.s, twon, P.B, twon}, P.WAH, P.kapB, row0, col0, lds, kb, ke);
@@ -587,6 +589,7 @@ static int g_scamp_rc = 0;
 template <int KK>
 static int scamp_kb_attrs() {
     int rc = set_lds_attr<128>((const void*)scamp_kb<128, KK>);
+    if (!rc) rc = set_lds_attr<256>((const void*)scamp_kb<256, KK, GKC, true>);
     return rc ? rc : set_lds_attr<256>((const void*)scamp_kb<256, KK>);
 }
 
@@ -618,7 +621,9 @@ static void scamp_split(const ScampK& P, const float* a, int lda, int K, int t, 
 template <int KK>
 static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_t st) {
     if (P.bn == 128 && P.lx3)
-        hipLaunchKernelGGL((scamp_kb<128, KK, 256>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
+        hipLaunchKernelGGL((scamp_kb<128, KK, 256, true>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
+    else if (P.lx3)
+        hipLaunchKernelGGL((scamp_kb<256, KK, GKC, true>), dim3(gr, P.ncpB / 256), dim3(AMP_WG), ldsB, st, P, t);
     else if (P.bn == 128 && scamp_short_chunks(P))
         hipLaunchKernelGGL((scamp_kb<128, KK, 256>), dim3(gr, P.ncpB / 128), dim3(AMP_WG), SKC_LDS,
                            st, P, t);
@@ -631,7 +636,7 @@ static void launch_kb_kk(const ScampK& P, int gr, size_t ldsB, int t, hipStream_
 static void launch_ka(const ScampK& P, int gr, int t, hipStream_t st) {
     if (P.lx3) {
         scamp_split(P, P.xm, 2 * P.N, P.N, t, st);
-        hipLaunchKernelGGL(scamp_ka<256>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
+        hipLaunchKernelGGL((scamp_ka<256, true>), dim3(gr, P.ncpA / 128), dim3(AMP_WG), SX3_LDS, st, P, t);
     } else if (scamp_short_chunks(P))
         hipLaunchKernelGGL(scamp_ka<256>, dim3(gr, P.ncpA / 128), dim3(AMP_WG), SKC_LDS, st, P, t);
     else
@@ -832,7 +837,7 @@ static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStr
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
     // fix-up grid: one slot per block in iteration t's partials (consumed by then)
-    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
+    const int nfix = fix_grid(P.nblk, P.B * P.L);
     launch_ka(P, gr, t, st);
     launch_kb(P, gr, ldsB, t, st);
     if (P.psi_split)
@@ -847,7 +852,7 @@ static int scamp_iterate_impl(const ScampK& P, const Const64& c64, int t, hipStr
 static int scamp_iterate_sharded(const ScampK& P, const Const64& c64, int t, hipStream_t st, bool& hook_failed) {
     const int gr = cdiv(P.B, GBM);
     const size_t ldsB = (P.bn == 128 ? GemmCfg<128>::LDS_BYTES : GemmCfg<256>::LDS_BYTES);
-    const int nfix = std::max(1, std::min(P.nblk, cdiv(P.B * P.L, AMP_WG)));
+    const int nfix = fix_grid(P.nblk, P.B * P.L);
     launch_ka(P, gr, t, st);
     launch_kb(P, gr, ldsB, t, st);
     if (P.psi_split) hipLaunchKernelGGL(scamp_psi, dim3(P.psi_nblk), dim3(AMP_WG), 0, st, P, t);

@@ -440,6 +440,15 @@ int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* b
     return AMP_OK;
 }
 
+int fix_grid(int nblk, int work) {
+    static const bool uncapped = [] {   // AMP_FIX_GRID=0: one workgroup per 256 sections (A/B runs)
+        const char* e = getenv("AMP_FIX_GRID");
+        return e && e[0] == '0';
+    }();
+    const int g = std::max(1, std::min(nblk, cdiv(work, AMP_WG)));
+    return uncapped ? g : std::min(g, 2 * device_cu_count());
+}
+
 int gemm_store(const float* a, int lda, int rows, int ka, const float* wt, int kap, int ncp, float* c, int ldc,
                int nc, hipStream_t st) {
     static bool attr = false;
