@@ -172,8 +172,10 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             const int j0 = 8 * (e / PBM);
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 2 * n + 2 * j0 + 4 * h);
+                // unconditional load at a clamped row, zeroed after it (a lane-divergent branch around
+                // the load serialises the loads' latencies: amp_gemm.h ALoadPlain)
+                float4 v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + max(min(row, nrows - 1), 0)) * 2 * n + 2 * j0 + 4 * h);
+                if (!(row < nrows)) v = make_float4(0.f, 0.f, 0.f, 0.f);
                 re[i][2 * h] = v.x; im[i][2 * h] = v.y; re[i][2 * h + 1] = v.z; im[i][2 * h + 1] = v.w;
             }
 #pragma unroll
@@ -221,8 +223,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             for (int r = 0; r < 4; ++r) {
                 const int row = 4 * (lane >> 4) + r;
                 const bool in = row < nrows;
-                yt[2 * t][r] = in ? P.ytil[(size_t)(row0 + row) * twok + 2 * o] : 0.f;
-                yt[2 * t + 1][r] = in ? P.ytil[(size_t)(row0 + row) * twok + 2 * o + 1] : 0.f;
+                // unconditional loads at a clamped row, zeroed after them (see the y load above)
+                const size_t yo = (size_t)(row0 + max(min(row, nrows - 1), 0)) * twok + 2 * o;
+                const float a = P.ytil[yo], b = P.ytil[yo + 1];
+                yt[2 * t][r] = in ? a : 0.f;
+                yt[2 * t + 1][r] = in ? b : 0.f;
             }
         }
       }
@@ -232,8 +237,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         const int ldy = 4 * N + 4;
         for (int e = tid; e < PBM * N; e += PWG) {          // float4 units: 4N floats per row
             const int row = e / N, c4 = 4 * (e - row * N);
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row < nrows) v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + row) * 4 * N + c4);
+            float4 v = *reinterpret_cast<const float4*>(P.y + (size_t)(row0 + max(min(row, nrows - 1), 0)) * 4 * N + c4);
+            if (!(row < nrows)) v = make_float4(0.f, 0.f, 0.f, 0.f);
             *reinterpret_cast<float4*>(lds + row * ldy + c4) = v;
         }
         __syncthreads();
@@ -251,7 +256,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = 4 * (lane >> 4) + r;
-                yt[t][r] = (row < nrows) ? P.ytil[(size_t)(row0 + row) * twok + col] : 0.f;
+                const float yv = P.ytil[(size_t)(row0 + max(min(row, nrows - 1), 0)) * twok + col];
+                yt[t][r] = (row < nrows) ? yv : 0.f;
             }
         }
     }
@@ -497,8 +503,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = 4 * (ln >> 4) + r;
-                        const float2 v = row < nrows ? *reinterpret_cast<const float2*>(P.ytil + (size_t)(row0 + row) * twok + 2 * oo)
-                                                     : make_float2(0.f, 0.f);
+                        const float2 u = *reinterpret_cast<const float2*>(P.ytil + (size_t)(row0 + max(min(row, nrows - 1), 0)) * twok + 2 * oo);
+                        const float2 v = row < nrows ? u : make_float2(0.f, 0.f);
                         ytr[r] = v.x; yti[r] = v.y;
                     }
                 } else {

@@ -57,8 +57,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
         float re[8], im[8];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (row0 + row < rows) v = *reinterpret_cast<const float4*>(y + (size_t)(row0 + row) * 2 * n + 2 * j0 + 4 * h);
+            // unconditional load at a clamped row (a lane-divergent branch around it serialises the
+            // loads' latencies, amp_gemm.h ALoadPlain); rows past `rows` are never stored
+            const float4 v = *reinterpret_cast<const float4*>(y + (size_t)min(row0 + row, rows - 1) * 2 * n + 2 * j0 + 4 * h);
             re[2 * h] = v.x; im[2 * h] = v.y; re[2 * h + 1] = v.z; im[2 * h + 1] = v.w;
         }
         x3_store8(sP, ldx, row, j0, re, im);
@@ -185,11 +186,8 @@ __global__ __launch_bounds__(512, 1) void ytil_x3_r2_kernel(const float* __restr
         for (int i = 0; i < PER; ++i) {
             const int e = tid + i * 512, row = e % 32, j0 = 8 * (e / 32);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                v[i][q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (row0 + row < rows)
-                    v[i][q] = *reinterpret_cast<const float4*>(y + (size_t)(row0 + row) * 2 * n + 2 * (h * KS + j0) + 4 * q);
-            }
+            for (int q = 0; q < 4; ++q)   // clamped row, no branch (see ytil_x3_kernel); rows past `rows` are never stored
+                v[i][q] = *reinterpret_cast<const float4*>(y + (size_t)min(row0 + row, rows - 1) * 2 * n + 2 * (h * KS + j0) + 4 * q);
         }
     };
     load_stage(0);

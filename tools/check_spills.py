@@ -39,8 +39,9 @@ ALLOWED = [
     (r'_ZN3amp12vamp_persistILi4ELi(1|2|4|8|16|64)ELi8ELi[124]ELb1ELi1ELb0ELb0E', 'eight-wave bf16x3 at N = 256'),
     # the four-wave bf16x3 form at N = 256 (AMP_VAMP_X3_WAVES=4, A/B runs only): the per-epoch
     # channel pointers, the force-inlined decision and the in-kernel counter fold cost BPSK / QPSK
-    # 12-24 loop-invariant values
-    (r'_ZN3amp12vamp_persistILi8ELi(1|2|4)ELi4ELi[124]ELb1ELi1ELb0ELb0E', 'four-wave bf16x3 at N = 256 (A/B form)'),
+    # 12-24 loop-invariant values (8-point alphabets 12 since the prologue's y~ loads became
+    # unconditional clamped loads)
+    (r'_ZN3amp12vamp_persistILi8ELi(1|2|4|8)ELi4ELi[124]ELb1ELi1ELb0ELb0E', 'four-wave bf16x3 at N = 256 (A/B form)'),
     # the eight-wave bf16x3 SCAMP form (cfg3's shape), the same kind of loop invariants
     (r'_ZN3amp13scamp_persistILi4ELi16ELi2ELi32ELi(1|2|4|8|16|64)ELb1ELb0ELi8E', 'eight-wave bf16x3 SCAMP'),
 ]
