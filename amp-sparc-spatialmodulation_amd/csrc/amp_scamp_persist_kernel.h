@@ -141,7 +141,10 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 4 * (lane >> 4) + r;
-            yt[t2][r] = (row < nrows) ? P.y[(size_t)(row0 + row) * twon + col] : 0.f;
+            // unconditional load at a clamped row, zeroed after it (a lane-divergent branch around
+            // the load serialises the loads' latencies: amp_gemm.h ALoadPlain)
+            const float yv = P.y[(size_t)(row0 + max(min(row, nrows - 1), 0)) * twon + col];
+            yt[t2][r] = (row < nrows) ? yv : 0.f;
         }
     }
     // Tracker (scamp.py:9-25): x = 0, z = y, psi = 1, phi = +inf
@@ -151,7 +154,8 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
     }
     for (int e = tid; e < SPB * twon; e += PWG) {
         const int row = e / twon, col = e - row * twon;
-        sZ[row * ldz + col] = (row < nrows) ? P.y[(size_t)(row0 + row) * twon + col] : 0.f;
+        const float yv = P.y[(size_t)(row0 + max(min(row, nrows - 1), 0)) * twon + col];
+        sZ[row * ldz + col] = (row < nrows) ? yv : 0.f;
     }
     for (int e = tid; e < SPB * Lin; e += PWG) lds[Y.offP0 + e] = lds[Y.offP1 + e] = 1.0f;
     for (int e = tid; e < SPB * Lout; e += PWG) sPhi[e] = INFINITY;
