@@ -120,7 +120,11 @@ __device__ __forceinline__ void gemm_tile_x3(const unsigned short* __restrict__ 
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int f = 0; f < PL; ++f)
+#ifdef AMP_X3T_NOWLOAD   // diagnostic builds only (wrong results): the tile without its operator stream
+                w[t][f] = u32x4{(unsigned)gg, (unsigned)f, (unsigned)t, 0x3f803f80u};
+#else
                 w[t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + gg) * PL + f) * 1024, 0);
+#endif
     };
     // one group's MFMAs: both row blocks of 16 trials against this wave's NT tiles (gl: the group
     // within the staged chunk)
@@ -137,7 +141,11 @@ __device__ __forceinline__ void gemm_tile_x3(const unsigned short* __restrict__ 
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const u32x4* x = w[t];
+#ifdef AMP_X3T_NOMMA   // diagnostic builds only (wrong results): the tile without its MFMAs
+#define AMP_MB(acc, p, q) acc[0] += __builtin_bit_cast(float, (p)[0] ^ (q)[0])
+#else
 #define AMP_MB(acc, p, q) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(p), as_bf16x8(q), acc, 0, 0, 0)
+#endif
                 if constexpr (CPX) {
                     // Cr = Ar.Xr - Ai.Xi, Ci = Ar.Xi + Ai.Xr, smallest terms first (gemm_x3's order)
                     u32x4 na[3];

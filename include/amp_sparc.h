@@ -294,9 +294,11 @@ typedef struct amp_bamp_args {
     size_t ws_bytes;
     float P0, Ps;       /* Config.P0 / Config.Ps as float32 (bamp.py:36), denoiser 1 only */
     int32_t gemm;       /* GEMM arithmetic: AMP_GEMM_AUTO (f32 MFMA, the reference's operand
-                           precision; environment AMP_BAMP_GEMM=h2 picks fp16x2 where N % 64 == 0 and
-                           n % 64 == 0, block-banded channels included), AMP_GEMM_F32, or AMP_GEMM_H2
-                           (OPT-IN, 22-bit operands, amp_gemm_h2.h: every GEMM's A rows split once into
+                           precision; environment AMP_BAMP_GEMM=x3 / h2 picks bf16x3 / fp16x2 where
+                           N % 64 == 0 and n % 64 == 0, block-banded channels included), AMP_GEMM_F32,
+                           AMP_GEMM_X3 (bf16x3 launch tiles, amp_gemm_x3.h: 24-bit operands, every
+                           GEMM's A rows split once into three bf16 pieces, no range limit), or
+                           AMP_GEMM_H2 (OPT-IN, 22-bit operands, amp_gemm_h2.h: every GEMM's A rows split once into
                            per-row scaled fp16 pieces; the operator pieces are scaled by 2^10, so |H|^2
                            must stay below 64, i.e. |H| < 8: beyond it a piece is inf and the detection
                            turns NaN, counted as errors, never silently wrong) */
@@ -332,7 +334,9 @@ typedef struct amp_scamp_args {
     const void* y;      /* c64 [B][n] */
     int32_t max_iter;
     int32_t engine;     /* amp_scamp_run only: AMP_ENGINE_AUTO / _LAUNCHES / _PERSISTENT (as for VAMP) */
-    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 / _H2 (as for VAMP) */
+    int32_t gemm;       /* persistent-engine GEMM arithmetic: AMP_GEMM_AUTO / _F32 / _X3 / _H2 (as for VAMP);
+                           on the launch engine AMP_GEMM_X3 runs bf16x3 launch tiles (N % 64 == 0,
+                           n % 64 == 0; under AUTO with AMP_SCAMP_LAUNCH_GEMM=x3), else f32 MFMA tiles */
     int32_t pad;
     double noise_var;   /* Na/Nr/SNR (scamp.py:98) */
     void* xmap;         /* out c64 [B][N] (scamp.py:107) */
