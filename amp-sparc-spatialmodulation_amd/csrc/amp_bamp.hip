@@ -23,6 +23,13 @@ namespace amp {
 
 constexpr int BRWG = 1024;
 
+// bamp_ka2's epilogue loads issued before the GEMM (A/B builds): measured slower, cfg5 64-QAM
+// 18.24 -> 18.52 ms, ISI BAMP 0.1330 -> 0.1345 ms per iteration (same box, gpurun_out r5pf; the
+// 48 registers they hold across the reduction cost more than the overlap gains)
+#ifndef AMP_KA2_PF
+#define AMP_KA2_PF 0
+#endif
+
 struct alignas(16) BampIter {
     int32_t stopped, T, fixed, fixed_all;
     // exact float64 fix-up of iteration T-1 pending (set by bamp_r, done and settled by
@@ -226,6 +233,31 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     const GemmTile tile = (KC == GKC && P.tile_rows) ? xcd_tile_rows() : xcd_tile();
     const int row0 = tile.rb * GBM, col0 = tile.cb * 128;
     const int twoN = 2 * P.N, twon = 2 * P.n;
+    // every global load of this thread's epilogue elements before any store (the z / invu / s
+    // stores may alias the next element's loads as far as the compiler knows: one memory latency
+    // per element otherwise); each element reads and writes only its own z and invu (so the loads
+    // may also go before the GEMM: AMP_KA2_PF, measured slower)
+    constexpr int IT = GBM * 64 / AMP_WG;
+    float2 yv[IT], zv[IT];
+    float vv[IT], iuo[IT];
+    auto epi_loads = [&] {
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            // unconditional loads at a clamped index (a lane-divergent branch around them
+            // serialises their latencies, amp_gemm.h ALoadPlain); out-of-range elements are never stored
+            const int e = threadIdx.x + u * AMP_WG;
+            const int rho = e >> 6, cp = e & 63;           // complex column pair
+            const int row = min(row0 + rho, P.B - 1), i = min((col0 >> 1) + cp, P.n - 1);
+            const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
+            yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
+            zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
+            vv[u] = P.v[o];
+            iuo[u] = P.invu[o];
+        }
+    };
+#if AMP_KA2_PF
+    epi_loads();
+#endif
     if constexpr (X3)
         gemm_tile_x3<128, true>(P.ap, P.rows_pad, P.N, P.WH, row0, col0, lds, bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     else if (KC == GKC && P.h2)
@@ -235,25 +267,9 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
         gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds,
                                        bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
-    // every global load of this thread's elements before any store (the z / invu / s stores may
-    // alias the next element's loads as far as the compiler knows: one memory latency per element
-    // otherwise); each element reads and writes only its own z and invu
-    constexpr int IT = GBM * 64 / AMP_WG;
-    float2 yv[IT], zv[IT];
-    float vv[IT], iuo[IT];
-#pragma unroll
-    for (int u = 0; u < IT; ++u) {
-        // unconditional loads at a clamped index (a lane-divergent branch around them serialises
-        // their latencies, amp_gemm.h ALoadPlain); out-of-range elements are never stored
-        const int e = threadIdx.x + u * AMP_WG;
-        const int rho = e >> 6, cp = e & 63;           // complex column pair
-        const int row = min(row0 + rho, P.B - 1), i = min((col0 >> 1) + cp, P.n - 1);
-        const size_t oc = (size_t)row * twon + 2 * i, o = (size_t)row * P.n + i;
-        yv[u] = *reinterpret_cast<const float2*>(P.y + oc);
-        zv[u] = *reinterpret_cast<const float2*>(P.z + oc);
-        vv[u] = P.v[o];
-        iuo[u] = P.invu[o];
-    }
+#if !AMP_KA2_PF
+    epi_loads();
+#endif
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
         const int e = threadIdx.x + u * AMP_WG;
