@@ -153,7 +153,8 @@ __device__ inline S2Lane s2_lane(const VampK& P, const float* s) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int i = lane + 64 * j;
-        a.v[j] = i < P.k ? s[i] * s[i] : 0.f;
+        const float x = s[min(i, P.k - 1)];   // unconditional load (no branch: amp_gemm.h ALoadPlain)
+        a.v[j] = i < P.k ? x * x : 0.f;
     }
     return a;
 }
