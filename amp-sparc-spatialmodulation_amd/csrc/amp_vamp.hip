@@ -67,15 +67,29 @@ __global__ __launch_bounds__(AMP_WG) void vamp_k1(VampK P, int t) {
     const int twoN = 2 * P.N, twok = 2 * P.k;
     gemm_tile<128>(ALoadRt{P.xm, P.r, twoN, P.B, twoN, it.dxdr_prev, it.ns_prev}, P.Wt1, P.kap1, row0, col0, lds);
     using C = GemmCfg<128>;
-    // w = scale * (y~ + vr * q) - q   (vamp.py:68-72; `x_tilde - q` is what V @ consumes)
-    for (int e = threadIdx.x; e < GBM * 128; e += AMP_WG) {
+    // w = scale * (y~ + vr * q) - q   (vamp.py:68-72; `x_tilde - q` is what V @ consumes).  Every
+    // load of this thread's elements first, unconditional at a clamped index (the w stores may
+    // alias them as far as the compiler knows, and a branch around a load serialises the loads'
+    // latencies: amp_gemm.h ALoadPlain); out-of-range elements are never stored
+    constexpr int IT = GBM * 128 / AMP_WG;
+    float yv[IT], s2v[IT];
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
+        const int row = min(row0 + (e >> 7), P.B - 1), col = min(col0 + (e & 127), twok - 1);
+        yv[u] = P.ytil[(size_t)row * twok + col];
+        s2v[u] = P.s2[col >> 1];
+    }
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+        const int e = threadIdx.x + u * AMP_WG;
         const int rho = e >> 7, cc = e & 127;
         const int row = row0 + rho, col = col0 + cc;
         if (row < P.B && col < twok) {
             const float q = lds[rho * C::LDC + cc];
-            const float sc = 1.0f / (P.s2[col >> 1] + it.vr);
+            const float sc = 1.0f / (s2v[u] + it.vr);
             const size_t o = (size_t)row * twok + col;
-            P.w[o] = sc * (P.ytil[o] + it.vr * q) - q;
+            P.w[o] = sc * (yv[u] + it.vr * q) - q;
         }
     }
 }
@@ -122,15 +136,29 @@ __global__ __launch_bounds__(AMP_WG) void vamp_k2(VampK P, int t) {
     gemm_tile<BN>(ALoadPlain{P.w, twok, P.B, twok}, P.Wt2, P.kap2, row0, col0, lds);
     // x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
     const int nrows = min(GBM, P.B - row0), ncols = min(BN, twoN - col0);
-    for (int e = threadIdx.x; e < GBM * BN; e += AMP_WG) {
-        const int rho = e / BN, cc = e % BN;
-        if (rho < nrows && cc < ncols) {
-            const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
-            const float rt = (P.xm[o] - it.dxdr_prev * P.r[o]) * it.ns_prev;
-            const float xt = lds[rho * C::LDC + cc] + rt;
-            const float rn = (xt - it.alpha * rt) * it.inv1ma;
-            P.r[o] = rn;
-            lds[rho * C::LDC + cc] = rn;
+    {
+        // every load of this thread's elements first, unconditional at a clamped index (see vamp_k1)
+        constexpr int IT = GBM * BN / AMP_WG;
+        float xv[IT], rv[IT];
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG;
+            const size_t o = (size_t)(row0 + min(e / BN, nrows - 1)) * twoN + col0 + min(e % BN, ncols - 1);
+            xv[u] = P.xm[o];
+            rv[u] = P.r[o];
+        }
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int e = threadIdx.x + u * AMP_WG;
+            const int rho = e / BN, cc = e % BN;
+            if (rho < nrows && cc < ncols) {
+                const size_t o = (size_t)(row0 + rho) * twoN + col0 + cc;
+                const float rt = (xv[u] - it.dxdr_prev * rv[u]) * it.ns_prev;
+                const float xt = lds[rho * C::LDC + cc] + rt;
+                const float rn = (xt - it.alpha * rt) * it.inv1ma;
+                P.r[o] = rn;
+                lds[rho * C::LDC + cc] = rn;
+            }
         }
     }
     __syncthreads();
