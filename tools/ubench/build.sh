@@ -12,3 +12,6 @@ $H -o bin/gemm_h2 gemm_h2_ubench.hip
 $H -o bin/gemm_i8 gemm_i8_ubench.hip
 $H -o bin/pk_dpp pk_dpp.hip
 $H -o bin/trans_pk trans_pk.hip
+$H -o bin/pair pair_ubench.hip
+$H -o bin/mfma_rd mfma_rd.hip
+$H -o bin/store_war store_war.hip
