@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 import subprocess
 
 import numpy as np
@@ -31,7 +32,7 @@ class AmpDims(C.Structure):
 
 
 class AmpStatus(C.Structure):
-    _fields_ = [('T', C.c_int32), ('nan_state', C.c_int32), ('stopped', C.c_int32), ('pad', C.c_int32),
+    _fields_ = [('T', C.c_int32), ('nan_state', C.c_int32), ('stopped', C.c_int32), ('gemm', C.c_int32),
                 ('last_scalar', C.c_float * 4)]
 
 
@@ -190,6 +191,13 @@ def build(verbose: bool = False) -> str:
     return LIB_PATH
 
 
+# Environment switches that only the diagnostic build reads (amp_host.h diag_env)
+DIAG_SWITCHES = ('AMP_BAMP_KC', 'AMP_BAND_GEMM', 'AMP_BAMP_GEMM', 'AMP_BAMP_X3_ROWS', 'AMP_SCAMP_KC', 'AMP_SCAMP_GEMM',
+                 'AMP_SCAMP_LAUNCH_GEMM', 'AMP_SCAMP_X3_WAVES', 'AMP_VAMP_GEMM', 'AMP_YTIL_IN_KERNEL', 'AMP_YTIL_X3',
+                 'AMP_PERSIST_WG2', 'AMP_VAMP_X3_WAVES', 'AMP_FIX_GRID', 'AMP_GRID_DENOISER', 'AMP_SECTION_BN',
+                 'AMP_FOLD_LAUNCH', 'AMP_HOST_RECORD')
+
+
 def lib():
     """The loaded library (raises if it has not been built)."""
     global _lib
@@ -198,6 +206,12 @@ def lib():
             raise RuntimeError(f'{LIB_PATH} not found: run __graft_entry__.build() (HIP extension missing; '
                                'there is no CPU fallback)')
         L = C.CDLL(LIB_PATH)
+        stray = sorted(k for k in os.environ if k in DIAG_SWITCHES)
+        if stray and not os.environ.get('AMP_LIB_PATH'):
+            warnings.warn(f'{", ".join(stray)}: A/B switches of the diagnostic build, ignored by the shipped '
+                          'library (make -C amp-sparc-spatialmodulation_amd/csrc DIAG=1, then '
+                          'AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_diag.so)',
+                          RuntimeWarning, stacklevel=2)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name, None)
             if f is None:
@@ -248,10 +262,16 @@ def dptr(t: torch.Tensor, dtype=None, name: str = 'tensor') -> int:
 
 
 def fold_launch() -> bool:
-    """AMP_FOLD_LAUNCH=1 (A/B runs): the persistent engines leave the counter fold to a launch of
-    its own and do not write the host record (amp_host.h fold_in_kernel); read per call, as there.
-    AMP_HOST_RECORD=0 (A/B runs): the record is copied back as for the other engines."""
-    return os.environ.get('AMP_FOLD_LAUNCH') == '1' or os.environ.get('AMP_HOST_RECORD') == '0'
+    """A diagnostic library (AMP_LIB_PATH, `make DIAG=1`) with AMP_FOLD_LAUNCH=1 or AMP_HOST_RECORD=0
+    (A/B runs): the persistent engines leave the counter fold to a launch of their own and the record
+    is copied back as for the other engines.  The shipped library always folds in-kernel and writes
+    the host record (amp_host.h fold_in_kernel)."""
+    return bool(os.environ.get('AMP_LIB_PATH')) and (os.environ.get('AMP_FOLD_LAUNCH') == '1' or
+                                                    os.environ.get('AMP_HOST_RECORD') == '0')
+
+
+# amp_status.gemm (include/amp_sparc.h AMP_ARITH_*): the GEMM arithmetic a forward ran
+ARITH_NAMES = {0: None, 1: 'f32', 2: 'bf16x3', 3: 'fp16x2', 4: 'int8x4'}
 
 
 _CU_STREAMS = {}

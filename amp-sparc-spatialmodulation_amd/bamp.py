@@ -142,9 +142,9 @@ class BAMPLayer(nn.Module):
 
 
 class BAMP(LazyResult, nn.Module):
-    """``gemm``: the GEMM arithmetic (amp_sparc.h amp_bamp_args.gemm): nat.GEMM_AUTO (f32 MFMA;
-    environment AMP_BAMP_GEMM=x3 / h2 picks a split form where the shape tiles), GEMM_F32, GEMM_X3
-    (bf16x3 tiles, 24-bit operands) or GEMM_H2 (fp16x2 tiles, 22-bit operands, opt-in)."""
+    """``gemm``: the GEMM arithmetic (amp_sparc.h amp_bamp_args.gemm): nat.GEMM_AUTO (f32 MFMA),
+    GEMM_F32, GEMM_X3 (bf16x3 tiles, 24-bit operands) or GEMM_H2 (fp16x2 tiles, 22-bit operands,
+    opt-in).  The arithmetic that ran is reported in ``self.L.arithmetic``."""
 
     def __init__(self, config: Config, gemm: int = nat.GEMM_AUTO) -> None:
         super().__init__()

@@ -26,9 +26,6 @@ constexpr int BRWG = 1024;
 // bamp_ka2's epilogue loads issued before the GEMM (A/B builds): measured slower, cfg5 64-QAM
 // 18.24 -> 18.52 ms, ISI BAMP 0.1330 -> 0.1345 ms per iteration (same box, gpurun_out r5pf; the
 // 48 registers they hold across the reduction cost more than the overlap gains)
-#ifndef AMP_KA2_PF
-#define AMP_KA2_PF 0
-#endif
 
 struct alignas(16) BampIter {
     int32_t stopped, T, fixed, fixed_all;
@@ -236,7 +233,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
     // every global load of this thread's epilogue elements before any store (the z / invu / s
     // stores may alias the next element's loads as far as the compiler knows: one memory latency
     // per element otherwise); each element reads and writes only its own z and invu (so the loads
-    // may also go before the GEMM: AMP_KA2_PF, measured slower)
+    // may also go before the GEMM: measured slower, round 5)
     constexpr int IT = GBM * 64 / AMP_WG;
     float2 yv[IT], zv[IT];
     float vv[IT], iuo[IT];
@@ -255,9 +252,6 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
             iuo[u] = P.invu[o];
         }
     };
-#if AMP_KA2_PF
-    epi_loads();
-#endif
     if constexpr (X3)
         gemm_tile_x3<128, true>(P.ap, P.rows_pad, P.N, P.WH, row0, col0, lds, bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     else if (KC == GKC && P.h2)
@@ -267,9 +261,7 @@ __global__ __launch_bounds__(AMP_WG) void bamp_ka2(BampK P, int t) {
         gemm_tile<128, ALoadPlain, KC>(ALoadPlain{P.xm, twoN, P.B, twoN}, P.WH, P.kapA2, row0, col0, lds,
                                        bkb(P, 1, tile.cb), bke(P, 1, tile.cb));
     using C = GemmCfg<128>;
-#if !AMP_KA2_PF
     epi_loads();
-#endif
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
         const int e = threadIdx.x + u * AMP_WG;
@@ -431,7 +423,8 @@ __device__ __forceinline__ void bamp_finish(const BampK& P, int t, uint32_t notc
     P.iters[t + 1] = nx;
     if (nx.stopped || t + 1 == P.max_iter) {
         amp_status s;
-        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped;
+        s.gemm = P.h2 ? AMP_ARITH_FP16X2 : P.x3 ? AMP_ARITH_BF16X3 : AMP_ARITH_F32;
         s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
         *P.status = s;
     }
@@ -567,7 +560,8 @@ __device__ inline void bamp_record(const BampK& P, int t, bool stop, int fixed) 
     P.iters[t + 1] = nx;
     if (nx.stopped || t + 1 == P.max_iter) {
         amp_status s;
-        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped;
+        s.gemm = P.h2 ? AMP_ARITH_FP16X2 : P.x3 ? AMP_ARITH_BF16X3 : AMP_ARITH_F32;
         s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
         *P.status = s;
     }
@@ -760,7 +754,7 @@ static int bamp_kb2_attrs() {
 constexpr size_t BSKC_LDS = GemmCfg<128, 256>::LDS_BYTES;
 static bool bamp_short_chunks(const BampK& P) {
     static const bool off = [] {
-        const char* e = getenv("AMP_BAMP_KC");
+        const char* e = diag_env("AMP_BAMP_KC");
         return e && atoi(e) == 512;
     }();
     return !P.h2 && !P.x3 && !off;
@@ -855,7 +849,7 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     P.rcnt = w.rcnt;
     {
         // block-banded H: the ranges are formed by the prepare launch sequence (AMP_BAND_GEMM=0: off)
-        const char* e = getenv("AMP_BAND_GEMM");
+        const char* e = diag_env("AMP_BAND_GEMM");
         const bool band = (d->Lin > 1 || d->Lout > 1) && !(e && e[0] == '0');
         for (int i = 0; i < 4; ++i) P.band[i] = band ? w.band[i] : nullptr;
     }
@@ -873,7 +867,7 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     AMP_REQUIRE((a->gemm != AMP_GEMM_H2 && a->gemm != AMP_GEMM_X3) || h2ok,
                 "amp_bamp_run: the split-precision GEMMs need N %% 64 == 0 and n %% 64 == 0 (N = %d, n = %d)", d->N, d->n);
     static const char gemm_env = [] {
-        const char* e = getenv("AMP_BAMP_GEMM");
+        const char* e = diag_env("AMP_BAMP_GEMM");
         return e ? e[0] : '\0';
     }();
     P.h2 = (a->gemm == AMP_GEMM_H2 || (a->gemm == AMP_GEMM_AUTO && h2ok && gemm_env == 'h')) ? 1 : 0;
@@ -882,7 +876,7 @@ static int bamp_setup(const amp_dims* d, const amp_constellation* c, const amp_b
     // L2); the bf16x3 operator (6 MB at cfg5) does not fit, so its tiles walk column blocks (each
     // XCD keeps its share of the operator resident).  AMP_BAMP_X3_ROWS=1: row-major (A/B runs).
     static const bool x3_rows = [] {
-        const char* e = getenv("AMP_BAMP_X3_ROWS");
+        const char* e = diag_env("AMP_BAMP_X3_ROWS");
         return e && e[0] == '1';
     }();
     P.tile_rows = P.h2 || (P.x3 && x3_rows) ? 1 : 0;
@@ -930,17 +924,6 @@ static int bamp_prepare_impl(const BampK& P, const amp_bamp_args* a, hipStream_t
         if ((rc = h2_kband(P.WH, pc, P.N / 32, 4, P.ncpA2 / 128, P.n / 16, const_cast<int*>(P.band[1]), st))) return rc;
         if ((rc = h2_kband(P.Wabs2T, pr, P.n / 32, 8, P.ncpB1 / 128, P.N / 16, const_cast<int*>(P.band[2]), st))) return rc;
         if ((rc = h2_kband(P.WHH, pc, P.n / 32, P.bn / 32, P.ncpB2 / P.bn, P.N / 16, const_cast<int*>(P.band[3]), st))) return rc;
-        if (getenv("AMP_DEBUG_BAND")) {   // diagnostic: the ranges as formed (synchronises the stream)
-            const int nt[4] = {P.ncpA1 / 128, P.ncpA2 / 128, P.ncpB1 / 128, P.ncpB2 / P.bn};
-            for (int i = 0; i < 4; ++i) {
-                std::vector<int> h(2 * nt[i]);
-                hipMemcpyAsync(h.data(), P.band[i], h.size() * 4, hipMemcpyDeviceToHost, st);
-                hipStreamSynchronize(st);
-                fprintf(stderr, "band[%d]:", i);
-                for (int k = 0; k < nt[i]; ++k) fprintf(stderr, " %d-%d", h[2 * k], h[2 * k + 1]);
-                fprintf(stderr, "\n");
-            }
-        }
     } else if (P.band[0]) {
         const float* wts[4] = {P.Wabs2, P.WH, P.Wabs2T, P.WHH};
         const int kaps[4] = {P.kapA1, P.kapA2, P.kapB1, P.kapB2}, ncps[4] = {P.ncpA1, P.ncpA2, P.ncpB1, P.ncpB2};

@@ -50,6 +50,28 @@ struct Carve {
     }
 };
 
+// Diagnostic switches of the A/B tools (tools/*.sh, tools/*_bench.py): read from the environment
+// only by a diagnostic build (`make DIAG=1` -> lib_diag/libampsparc_diag.so, loaded through
+// AMP_LIB_PATH).  The shipped library ignores them, so no environment variable changes what the
+// product computes (the GEMM arithmetic is an argument of the ABI and is reported back in
+// amp_status.gemm).
+inline const char* diag_env(const char* name) {
+#if defined(AMP_DIAG_ENV) && AMP_DIAG_ENV
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// An engine form that only the A/B tools select (four waves at N = 256, one workgroup per CU at
+// N = 64): instantiated in the diagnostic build only, so the shipped library does not carry it.
+#if defined(AMP_DIAG_ENV) && AMP_DIAG_ENV
+#define AMP_DIAG_ONLY(...) (__VA_ARGS__)
+#else
+#define AMP_DIAG_ONLY(...) (set_error("%s: an A/B form of the diagnostic build (make DIAG=1)", __func__), AMP_E_ARG)
+#endif
+
 // The product-grid form of the denoiser (amp_denoise.h) applies when the float32 points take
 // R distinct real and R distinct imaginary values with K = R^2 (R = 2, 4, 8), the grid's four
 // corners are in the table and the multiplicities follow a pattern the kernels know (every
@@ -58,7 +80,7 @@ struct Carve {
 // real alphabets keep the direct form.  AMP_GRID_DENOISER=0 disables it (A/B runs).
 inline bool grid_denoiser_enabled() {
     static const bool on = [] {
-        const char* e = getenv("AMP_GRID_DENOISER");
+        const char* e = diag_env("AMP_GRID_DENOISER");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -188,7 +210,7 @@ inline int persist_grid_launch(const char* what, const void* fn, int nwg, int th
 // AMP_SECTION_BN=256: the wide column tile also where sections fit the narrow one (A/B runs)
 inline bool section_bn_wide_env() {
     static const bool v = [] {
-        const char* e = getenv("AMP_SECTION_BN");
+        const char* e = diag_env("AMP_SECTION_BN");
         return e && atoi(e) == 256;
     }();
     return v;
@@ -219,11 +241,11 @@ struct CWeightJob {
 constexpr int CW_MAX_JOBS = 24;
 
 // The persistent engines fold the fused decision's per-workgroup counter records inside their own
-// launch and write the host record themselves (amp_decide_fused.h); AMP_FOLD_LAUNCH=1 keeps the
-// separate vamp_decide_fold launch and leaves the host record alone (A/B runs; the Python layer
-// then copies the record back, vamp.py LazyResult).  Read per call.
+// launch and write the host record themselves (amp_decide_fused.h); a diagnostic build with
+// AMP_FOLD_LAUNCH=1 keeps the separate vamp_decide_fold launch (A/B runs; round 5: ~2 us per step
+// slower).
 inline bool fold_in_kernel() {
-    const char* e = getenv("AMP_FOLD_LAUNCH");
+    const char* e = diag_env("AMP_FOLD_LAUNCH");
     return !(e && e[0] == '1');
 }
 int build_cweights(const CWeightJob* jobs, int njobs, unsigned* zero, int nzero, hipStream_t st);

@@ -196,14 +196,7 @@ __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast
 // PIN: keep each ring refill behind the group's MFMAs (a scheduling barrier): the compiler then
 // cannot hoist the next group's loads into fresh registers — the ring holds exactly R groups (the
 // two-waves-per-SIMD engines, which have 256 registers per wave, use R = 2 with it).
-// GACC: every 32-deep group's 12 products per accumulator are summed into a zeroed group
-// accumulator that is then added to the running one (one f32 rounding per group at the result's
-// magnitude instead of twelve; DESIGN.md §4 item 5: the accumulation error, not the product split,
-// is what moves the allclose exit at the rounding-decided golden points).
-#ifndef AMP_X3_GACC
-#define AMP_X3_GACC 0
-#endif
-template <int NT, int G, int R = 1, bool PIN = false, bool GACC = AMP_X3_GACC>
+template <int NT, int G, int R = 1, bool PIN = false>
 __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
                                         f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
     constexpr int RR = G < R ? G : R;
@@ -256,8 +249,7 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const u32x4* w = ring[d][t];
-            f32x4 gr = GACC && g > 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : cr[t];
-            f32x4 gi = GACC && g > 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ci[t];
+            f32x4 gr = cr[t], gi = ci[t];
 #define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
             // smallest terms first
             AMP_MF(gr, a[0], w[2]);  AMP_MF(gi, a[0], w[5]);
@@ -273,8 +265,7 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
             AMP_MF(gr, a[0], w[0]);  AMP_MF(gi, a[0], w[3]);
             AMP_MF(gr, na[0], w[3]); AMP_MF(gi, a[3], w[0]);
 #undef AMP_MF
-            if (GACC && g > 0) { cr[t] += gr; ci[t] += gi; }
-            else { cr[t] = gr; ci[t] = gi; }
+            cr[t] = gr; ci[t] = gi;
         }
         if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
         if (g + RR < G) {

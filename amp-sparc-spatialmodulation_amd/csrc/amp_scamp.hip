@@ -294,7 +294,8 @@ __device__ __forceinline__ void scamp_finish(const ScampK& P, int t, uint32_t no
     P.iters[t + 1] = nx;
     if (nx.stopped || t + 1 == P.max_iter) {
         amp_status s;
-        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped; s.pad = 0;
+        s.T = t + 1; s.nan_state = fixed != 0 ? 1 : 0; s.stopped = nx.stopped;
+        s.gemm = P.lx3 ? AMP_ARITH_BF16X3 : AMP_ARITH_F32;
         s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
         *P.status = s;
     }
@@ -600,7 +601,7 @@ constexpr size_t SKC_LDS = GemmCfg<128, 256>::LDS_BYTES;   // the short-chunk ti
 
 static bool scamp_short_chunks(const ScampK& P) {
     static const bool off = [] {
-        const char* e = getenv("AMP_SCAMP_KC");
+        const char* e = diag_env("AMP_SCAMP_KC");
         return e && atoi(e) == 512;
     }();
     return P.bandA != nullptr && !off;
@@ -686,7 +687,7 @@ namespace amp {
 // AMP_SCAMP_GEMM=f32: AMP_GEMM_AUTO keeps the f32-MFMA persistent GEMMs (A/B runs)
 static bool scamp_gemm_f32_requested() {
     static const bool v = [] {
-        const char* e = getenv("AMP_SCAMP_GEMM");
+        const char* e = diag_env("AMP_SCAMP_GEMM");
         return e && e[0] == 'f';
     }();
     return v;
@@ -695,7 +696,7 @@ static bool scamp_gemm_f32_requested() {
 // AMP_SCAMP_GEMM=h2: AMP_GEMM_AUTO picks the fp16x2 persistent GEMMs instead of bf16x3 (A/B runs)
 static bool scamp_gemm_h2_requested() {
     static const bool v = [] {
-        const char* e = getenv("AMP_SCAMP_GEMM");
+        const char* e = diag_env("AMP_SCAMP_GEMM");
         return e && e[0] == 'h';
     }();
     return v;
@@ -706,7 +707,7 @@ static bool scamp_gemm_h2_requested() {
 // AMP_BAND_GEMM=0 (A/B runs).
 static bool band_gemm_enabled() {
     static const bool on = [] {
-        const char* e = getenv("AMP_BAND_GEMM");
+        const char* e = diag_env("AMP_BAND_GEMM");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -761,7 +762,7 @@ static int scamp_setup(const amp_dims* d, const amp_constellation* c, const amp_
     // launch engine: bf16x3 tiles when asked for (AMP_GEMM_X3) or, under AUTO, with
     // AMP_SCAMP_LAUNCH_GEMM=x3; f32 MFMA tiles otherwise
     static const bool lx3_env = [] {
-        const char* e = getenv("AMP_SCAMP_LAUNCH_GEMM");
+        const char* e = diag_env("AMP_SCAMP_LAUNCH_GEMM");
         return e && e[0] == 'x';
     }();
     P.lx3 = lx3ok && (a->gemm == AMP_GEMM_X3 || (a->gemm == AMP_GEMM_AUTO && lx3_env)) ? 1 : 0;

@@ -547,7 +547,7 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
     s.T = stopped ? T : P.max_iter;
     s.nan_state = aborted ? -1 : (fixed != 0 ? 1 : 0);
     s.stopped = stopped;
-    s.pad = 0;
+    s.gemm = P.x3 + 1;   // x3: 0 f32, 1 bf16x3, 2 fp16x2
     s.last_scalar[0] = s.last_scalar[1] = s.last_scalar[2] = s.last_scalar[3] = 0.f;
     if (wg == 0 && tid == 0) *P.status = s;
     if (P.dec_on) {

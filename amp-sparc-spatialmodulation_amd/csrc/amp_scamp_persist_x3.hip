@@ -7,7 +7,7 @@ namespace amp {
 
 static bool scamp_waves8() {
     static const bool v = [] {
-        const char* e = getenv("AMP_SCAMP_X3_WAVES");
+        const char* e = diag_env("AMP_SCAMP_X3_WAVES");
         return !(e && atoi(e) == 4);
     }();
     return v;
@@ -19,7 +19,7 @@ int scamp_persist_launch_x3(const ScampK& P, const DecConst& c64, hipStream_t st
     // cfg3's shape: eight waves (two per SIMD) unless AMP_SCAMP_X3_WAVES=4 (A/B runs)
     if (twoN == 256 && twon == 512)
         return scamp_waves8() ? spersist_launch_s<4, 16, 2, 32, true, false, 8>(P, c64, st)
-                              : spersist_launch_s<8, 16, 4, 32, true>(P, c64, st);
+                              : AMP_DIAG_ONLY(spersist_launch_s<8, 16, 4, 32, true>(P, c64, st));
     if (twoN == 256 && twon == 256) return spersist_launch_s<4, 16, 4, 16, true>(P, c64, st);
     set_error("scamp_persist (bf16x3): (2N, 2n) = (%d, %d) not supported", twoN, twon);
     return AMP_E_ARG;

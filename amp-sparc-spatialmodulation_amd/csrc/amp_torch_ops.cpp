@@ -85,7 +85,7 @@ Tensor workspace(size_t bytes, const Tensor& like) {
     return at::empty({(int64_t)std::max<size_t>(bytes, 256)}, like.options().dtype(at::kByte));
 }
 
-// status record (amp_status) as int32 [4]: T, nan_state, stopped, pad
+// status record (amp_status) as int32 [4]: T, nan_state, stopped, gemm (AMP_ARITH_*)
 Tensor status_tensor(const Tensor& like) { return at::zeros({8}, like.options().dtype(at::kInt)); }
 
 // ---- amp::vamp_run — VAMP.forward (vamp.py:159-187) without the decision -------------------

@@ -239,7 +239,7 @@ __device__ inline amp_status vamp_make_status(const VampK& P, const VampIter& cu
     s.T = nx.stopped ? nx.T : P.max_iter;
     s.nan_state = fixed != 0 ? 1 : 0;
     s.stopped = nx.stopped;
-    s.pad = 0;
+    s.gemm = P.x3 + 1;   // x3: 0 f32, 1 bf16x3, 2 fp16x2, 3 int8x4 (the launch engine: 0)
     s.last_scalar[0] = cur.s2t; s.last_scalar[1] = cur.alpha; s.last_scalar[2] = cur.sigma2;
     s.last_scalar[3] = nx.stopped ? cur.dxdr_prev : nx.dxdr_prev;
     return s;
@@ -281,22 +281,6 @@ __device__ __forceinline__ void den_debug(const PDenoisePolicy& p, int sec, int 
         p.dbg[row * 2 * p.N + sj * p.M + m] = ze;
         p.dbg[row * 2 * p.N + p.N + sj * p.M + m] = vs;
     }
-}
-
-// PDenoisePolicy over half of every row's sections (the staggered eight-wave engine, DESIGN.md
-// §3.1): local section s is section off + (s & (2^lsh - 1)) of row s >> lsh.
-struct PHalfPolicy {
-    PDenoisePolicy p;
-    int lsh, off;
-    __device__ __forceinline__ int gsec(int s) const { return ((s >> lsh) << p.lspr) + off + (s & ((1 << lsh) - 1)); }
-    __device__ __forceinline__ void load(int sec, int m, float& rr, float& ri, float& it) const { p.load(gsec(sec), m, rr, ri, it); }
-    __device__ __forceinline__ void store(int sec, int m, float xr, float xi, float var, PartAcc& pa) const {
-        p.store(gsec(sec), m, xr, xi, var, pa);
-    }
-    __device__ __forceinline__ void section(int sec, float smax, float sabs) const { p.section(gsec(sec), smax, sabs); }
-};
-__device__ __forceinline__ void den_debug(const PHalfPolicy& h, int sec, int m, float ze, float vs) {
-    den_debug(h.p, h.gsec(sec), m, ze, vs);
 }
 
 constexpr int PBM = 16;   // trials per workgroup

@@ -436,7 +436,7 @@ __global__ void vamp_output_kernel(VampK P) {
 // AMP_VAMP_GEMM=f32: AMP_GEMM_AUTO keeps the f32-MFMA persistent GEMMs (measurement / A-B runs)
 bool gemm_f32_requested() {
     static const bool v = [] {
-        const char* e = getenv("AMP_VAMP_GEMM");
+        const char* e = diag_env("AMP_VAMP_GEMM");
         return e && e[0] == 'f';
     }();
     return v;
@@ -445,7 +445,7 @@ bool gemm_f32_requested() {
 // AMP_VAMP_GEMM=h2 makes AUTO pick the fp16x2 form (A/B runs only: 22-bit operands)
 static bool gemm_h2_requested() {
     static const bool v = [] {
-        const char* e = getenv("AMP_VAMP_GEMM");
+        const char* e = diag_env("AMP_VAMP_GEMM");
         return e && e[0] == 'h';
     }();
     return v;
@@ -461,7 +461,7 @@ static bool gemm_h2_requested() {
 // an f32 sum (amp_persist.h gemm_i8).
 static bool gemm_i8_requested() {   // AMP_VAMP_GEMM=i8: AUTO picks int8x4 (A/B runs)
     static const bool v = [] {
-        const char* e = getenv("AMP_VAMP_GEMM");
+        const char* e = diag_env("AMP_VAMP_GEMM");
         return e && e[0] == 'i';
     }();
     return v;
@@ -608,7 +608,7 @@ static int vamp_prepare_impl(const VampK& P, const amp_vamp_args* a, hipStream_t
 // 9 dB golden, T 4 vs the reference's 3).
 static int ytil_in_kernel_env() {
     static const int v = [] {
-        const char* e = getenv("AMP_YTIL_IN_KERNEL");
+        const char* e = diag_env("AMP_YTIL_IN_KERNEL");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
     return v;
@@ -618,7 +618,7 @@ static int ytil_in_kernel_env() {
 // amp_vamp_persist_x3.hip); AMP_YTIL_X3=0 keeps the f32 gemm_store launch (A/B runs)
 static bool ytil_x3_env() {
     static const bool v = [] {
-        const char* e = getenv("AMP_YTIL_X3");
+        const char* e = diag_env("AMP_YTIL_X3");
         return !(e && e[0] == '0');
     }();
     return v;

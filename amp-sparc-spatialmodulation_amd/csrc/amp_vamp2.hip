@@ -223,7 +223,7 @@ __global__ void v2_finish(V2K P) {
         st.T = S.T;
         st.nan_state = S.nan;
         st.stopped = S.stopped;
-        st.pad = 0;
+        st.gemm = AMP_ARITH_F32;
         st.last_scalar[0] = S.gamma; st.last_scalar[1] = S.alpha; st.last_scalar[2] = S.gamma_tilde;
         st.last_scalar[3] = S.dm;
         *P.status = st;

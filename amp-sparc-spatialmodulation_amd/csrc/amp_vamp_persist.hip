@@ -79,7 +79,7 @@ bool vamp_persist_x3_fits(int N, int k, int L) {
 // DESIGN.md §3.8).
 bool persist_wg2() {
     static const bool v = [] {
-        const char* e = getenv("AMP_PERSIST_WG2");
+        const char* e = diag_env("AMP_PERSIST_WG2");
         return !(e && e[0] == '0') && !gemm_f32_requested();
     }();
     return v;

@@ -10,7 +10,7 @@ int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.N) {
     case 64:   // as in the bf16x3 unit: the two-per-CU build for every N = 64 launch
         return persist_wg2() ? persist_launch_nt<2, 4, true, 2, true>(P, dc, st)
-                             : persist_launch_nt<2, 4, true, 1, true>(P, dc, st);
+                             : AMP_DIAG_ONLY(persist_launch_nt<2, 4, true, 1, true>(P, dc, st));
     case 128: return persist_launch_nt<4, 4, true, 1, true>(P, dc, st);
     case 256: return persist_launch_nt<8, 4, true, 1, true>(P, dc, st);
     default: break;

@@ -8,7 +8,7 @@ namespace amp {
 
 static bool i8_waves8() {
     static const bool v = [] {
-        const char* e = getenv("AMP_VAMP_X3_WAVES");
+        const char* e = diag_env("AMP_VAMP_X3_WAVES");
         return !(e && atoi(e) == 4);
     }();
     return v;
@@ -20,7 +20,7 @@ int persist_dispatch_i8(const VampK& P, const DecConst& dc, hipStream_t st) {
     case 128: return persist_launch_nt<4, 4, true, 1, false, true>(P, dc, st);
     case 256:   // eight waves (two per SIMD) unless AMP_VAMP_X3_WAVES=4, as the bf16x3 engine
         return i8_waves8() ? persist_launch_nt<4, 8, true, 1, false, true>(P, dc, st)
-                           : persist_launch_nt<8, 4, true, 1, false, true>(P, dc, st);
+                           : AMP_DIAG_ONLY(persist_launch_nt<8, 4, true, 1, false, true>(P, dc, st));
     default: break;
     }
     set_error("vamp_persist (int8x4): N = %d not supported", P.N);

@@ -30,12 +30,6 @@ constexpr int AMP_TRACE_STRIDE = 10;   // diagnostic stamps per (workgroup, iter
 #ifndef AMP_X3_W8_PKGRID
 #define AMP_X3_W8_PKGRID 1              // the eight-wave bf16x3 form keeps 16-QAM's packed grid denoiser
 #endif
-#ifndef AMP_X3_STAGGER
-#define AMP_X3_STAGGER 0                // 1: staggered GEMM2 / denoiser (A/B: slower)
-#endif
-#ifndef AMP_X3_STG_RING
-#define AMP_X3_STG_RING 1               // weight groups in flight of the staggered second-half GEMM2
-#endif
 #ifndef AMP_X3_DU
 #define AMP_X3_DU 2                     // 16-QAM sections in flight per lane group (bf16x3 engine; 4 measured: no gain)
 #endif
@@ -101,13 +95,6 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     // eight waves: no A-fragment prefetch in gemm_x3 (the partner wave covers the LDS reads;
     // 24 registers fewer) when AMP_X3_W8_PIN (A/B builds)
     constexpr bool X3PIN = NWV == 8 && AMP_X3_W8_PIN;
-    // Staggered GEMM2 / denoiser (eight-wave bf16x3 form, 2 NWV complex column tiles: N = 256).  Waves
-    // w and w + 4 share a SIMD.  (1) every wave forms r for ONE tile of the first half of the columns;
-    // (2) waves 0-3 denoise the first half's sections (VALU) while waves 4-7 form r for the second
-    // half (two tiles each: L2 stream + MFMA); (3) all eight waves denoise the second half.  One SIMD
-    // then runs one wave's denoiser beside its partner's GEMM instead of the two waves reaching the
-    // same phase together.
-    constexpr bool STG = X3 && !H2 && !I8 && NWV == 8 && NC == 2 && KK <= 16 && AMP_X3_STAGGER;
     const Const64& c64 = dc;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
@@ -641,14 +628,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
                     for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
             }
-            if constexpr (STG) {
-                f32x4 hr[1], hi[1];
-                gemm_x3<1, G3, X3R, X3PIN>(sP, ldx, Wx2, wave, hr, hi);   // (1) first half: tile `wave`
-                r_epi(wave, hr, hi);
-            } else {
-                if constexpr (!I8 && !H2) gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx2, cc0, cr, ci);
-                r_epi(cc0, cr, ci);
-            }
+            if constexpr (!I8 && !H2) gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx2, cc0, cr, ci);
+            r_epi(cc0, cr, ci);
         } else {
         gemm16<NT, NT * NWV>(sA, lda, P.Wq2, ct0, acc);
 #pragma unroll
@@ -668,30 +649,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         if (P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
         PartAcc pa;
-        if constexpr (STG) {
-            // sections per row half: spr / 2 (M divides N / 2 for every power-of-two M <= 64 at N = 256)
-            const int lsh = 31 - __builtin_clz(spr) - 1;
-            const int wvu = __builtin_amdgcn_readfirstlane(wave);   // wave-uniform branch (not exec-masked)
-            if (wvu < 4) {    // (2) the first half's sections on waves 0-3 ...
-                PHalfPolicy hp{pol, lsh, 0};
-                denoise_sections_u<true, KK, DU, PKDEN>(hp, nrows * (spr >> 1), M, P.c, pa, DenWaves{wvu, 4});
-            } else {          // ... beside the second half's GEMM2 on waves 4-7 (tiles NWV + 2 (wave - 4) ...)
-                // one GEMM wave per SIMD here: two weight groups in flight (the ring of both waves
-                // of the SIMD in the unstaggered form)
-                gemm_x3<NC, G3, AMP_X3_STG_RING, AMP_X3_STG_RING == 2>(sP, ldx, Wx2, NWV + 2 * (wvu - 4), cr, ci);
-                r_epi(NWV + 2 * (wvu - 4), cr, ci);
-            }
-            __syncthreads();
-            stamp(t, 4);
-            PHalfPolicy hp{pol, lsh, spr >> 1};   // (3) the second half's sections on all eight waves
-            denoise_sections_u<true, KK, DU, PKDEN>(hp, nrows * (spr >> 1), M, P.c, pa);
-        } else {
-            stamp(t, 4);
-            if constexpr (KK > 16)
-                denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
-            else
-                denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
-        }
+        stamp(t, 4);
+        if constexpr (KK > 16)
+            denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
+        else
+            denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
         part_publish(pa, grs, ((unsigned)t * nwx + wgx) * 32u, tag, scr);

@@ -11,7 +11,7 @@ namespace amp {
 // cfg4 iteration).  AMP_VAMP_X3_WAVES=4 keeps the four-wave form (A/B runs).
 static bool x3_waves8() {
     static const bool v = [] {
-        const char* e = getenv("AMP_VAMP_X3_WAVES");
+        const char* e = diag_env("AMP_VAMP_X3_WAVES");
         return !(e && atoi(e) == 4);
     }();
     return v;
@@ -21,10 +21,10 @@ int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st) {
     switch (P.N) {
     case 64:   // the two-per-CU build for every N = 64 launch, so that one epoch and side-by-side
                // epochs run the same arithmetic (bit-identical results, tests/test_gpu_epochs.py)
-        return persist_wg2() ? persist_launch_nt<2, 4, true, 2>(P, dc, st) : persist_launch_nt<2, 4, true>(P, dc, st);
+        return persist_wg2() ? persist_launch_nt<2, 4, true, 2>(P, dc, st) : AMP_DIAG_ONLY(persist_launch_nt<2, 4, true>(P, dc, st));
     case 128: return persist_launch_nt<4, 4, true>(P, dc, st);
     case 256:
-        return x3_waves8() ? persist_launch_nt<4, 8, true>(P, dc, st) : persist_launch_nt<8, 4, true>(P, dc, st);
+        return x3_waves8() ? persist_launch_nt<4, 8, true>(P, dc, st) : AMP_DIAG_ONLY(persist_launch_nt<8, 4, true>(P, dc, st));
     default: break;
     }
     set_error("vamp_persist (bf16x3): N = %d not supported", P.N);

@@ -442,7 +442,7 @@ int h2_kband(const void* wq, int PL, int G, int tpt, int ntiles, int n16, int* b
 
 int fix_grid(int nblk, int work) {
     static const bool uncapped = [] {   // AMP_FIX_GRID=0: one workgroup per 256 sections (A/B runs)
-        const char* e = getenv("AMP_FIX_GRID");
+        const char* e = diag_env("AMP_FIX_GRID");
         return e && e[0] == '0';
     }();
     const int g = std::max(1, std::min(nblk, cdiv(work, AMP_WG)));

@@ -101,6 +101,18 @@ class Loss:
     def loss(self, value: dict) -> None:
         self._loss = value
 
+    @property
+    def arithmetic(self):
+        """The GEMM arithmetic of the last forward recorded here, as the engine reported it
+        (amp_status.gemm: 'bf16x3', 'f32', 'fp16x2' or 'int8x4'; None before any forward)."""
+        if self._pending is not None:
+            self.resolve()
+        st = getattr(self, 'last_status', None)
+        if st is None:
+            return None
+        from amp_native import ARITH_NAMES
+        return ARITH_NAMES.get(int(st.gemm))
+
     def resolve(self) -> None:
         """Wait for and record the counters of the forward still in flight (if any)."""
         p, self._pending = self._pending, None

@@ -66,9 +66,15 @@ typedef struct amp_status {
     int32_t T;          /* executed iterations (t+1 at the early-exit break, vamp.py:185) */
     int32_t nan_state;  /* 1 when the last iteration produced NaN sections (float64 underflow rule) */
     int32_t stopped;    /* 1 when the allclose early exit fired */
-    int32_t pad;
+    int32_t gemm;       /* the GEMM arithmetic that ran: AMP_ARITH_* (0: not reported) */
     float last_scalar[4]; /* VAMP: sigma2_tilde, alpha, sigma2, dxdr of the last iteration */
 } amp_status;
+
+/* amp_status.gemm: the arithmetic of the engine's GEMMs in the forward that wrote the record */
+#define AMP_ARITH_F32 1      /* float32 operands and accumulation (f32 MFMA / tiles) */
+#define AMP_ARITH_BF16X3 2   /* three bf16 pieces per f32 operand (24 bits), six products, f32 accumulation */
+#define AMP_ARITH_FP16X2 3   /* two fp16 pieces per scaled operand (22 bits), three products (opt-in) */
+#define AMP_ARITH_INT8X4 4   /* four int8 digits per block-fixed-point operand (31 bits), exact int32 sums (opt-in) */
 
 /* Error counters of Loss.error_rate (loss.py:67-179), written by amp_map_decide_count. */
 typedef struct amp_counts {

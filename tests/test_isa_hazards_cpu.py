@@ -43,7 +43,8 @@ def test_scanner_store_data():
                  'global_store_dwordx2 v[0:1], v[4:5], off\nv_mov_b32_e32 v5, 0\n',
                  'ds_write_b128 v1, v[4:7]\nv_mov_b32_e32 v5, 0\n',
                  'scratch_store_dwordx4 off, v[26:29], off\nds_read_b128 v[26:29], v1 offset:144\n',
-                 'global_store_dwordx4 v[0:1], v[4:7], off\nv_mfma_f32_16x16x32_bf16 v[4:7], v[8:11], v[12:15], v[4:7]\n'):
+                 'global_store_dwordx4 v[0:1], v[4:7], off\nv_mfma_f32_16x16x32_bf16 v[4:7], v[8:11], v[12:15], v[4:7]\n',
+                 'global_store_dwordx4 v2, v[0:3], s[86:87] offset:160 nt\ns_endpgm\nv_cndmask_b32_e32 v0, s0, v0, vcc\n'):
         assert _scan(text) == [], text
 
 

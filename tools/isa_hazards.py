@@ -132,6 +132,8 @@ def scan(funcs):
                     if ws >= STORE_WAIT:
                         break
                     m2, o2 = ins[j]
+                    if m2 in ('s_endpgm', 's_branch', 's_setpc_b64'):   # the next listed instruction is not next in time
+                        break
                     if dst_regs(m2, o2) & data:
                         found.append(('store-data', name, ws, [f'{a} {b}' for a, b in ins[i:j + 1]]))
                         break
