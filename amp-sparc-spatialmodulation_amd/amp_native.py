@@ -113,6 +113,7 @@ SIGNATURES = {
     'amp_vamp_debug_dump': (C.c_int, [_P]),
     'amp_vamp_max_epochs': (C.c_int, [_D, _I]),
     'amp_vamp_max_epochs_gemm': (C.c_int, [_D, _I, _I]),
+    'amp_vamp_epochs_ch_eligible': (C.c_int, [_D, _I, _I]),
     'amp_set_allreduce_hook': (C.c_int, [_P, _P]),
     'amp_vamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
     'amp_bamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _I, _P]),
@@ -195,7 +196,7 @@ def build(verbose: bool = False) -> str:
 DIAG_SWITCHES = ('AMP_BAMP_KC', 'AMP_BAND_GEMM', 'AMP_BAMP_GEMM', 'AMP_BAMP_X3_ROWS', 'AMP_SCAMP_KC', 'AMP_SCAMP_GEMM',
                  'AMP_SCAMP_LAUNCH_GEMM', 'AMP_SCAMP_X3_WAVES', 'AMP_VAMP_GEMM', 'AMP_YTIL_IN_KERNEL', 'AMP_YTIL_X3',
                  'AMP_PERSIST_WG2', 'AMP_VAMP_X3_WAVES', 'AMP_FIX_GRID', 'AMP_GRID_DENOISER', 'AMP_SECTION_BN',
-                 'AMP_FOLD_LAUNCH', 'AMP_HOST_RECORD')
+                 'AMP_FOLD_LAUNCH', 'AMP_HOST_RECORD', 'AMP_SHARD_ANY_STREAM')
 
 
 def lib():

@@ -158,10 +158,10 @@ __device__ __forceinline__ void decide_epilogue(const PK& P, const DecConst& dc,
 }
 
 // The fold of the n published records of workgroups [base, base + n) of this launch (one epoch),
-// by waves 0-3 of the calling workgroup, in vamp_decide_fold's order (thread i < 256 holds record i,
-// a 64-lane sum per wave, thread 0 adds the four wave sums in order: the same bits).  Each thread
-// polls its record's granules until all 13 carry `tag` (a workgroup that has not yet reached its
-// epilogue); a bounded spin (2 s).  Thread 0 writes *out.  Returns false (every thread) on a timeout.
+// by waves 0-3 of the calling workgroup, in vamp_decide_fold's order (thread i < 256 folds records
+// i, i + 256, ..., a 64-lane sum per wave, thread 0 adds the four wave sums in order: the same
+// bits).  Each thread polls its records' granules until all 13 carry `tag` (a workgroup that has
+// not yet reached its epilogue); a bounded spin (2 s).  Thread 0 writes *out.  Returns false (every thread) on a timeout.
 template <class PK>
 __device__ bool dec_fold_gather(const PK& P, int base, int n, unsigned tag, amp_counts* out, void* lds, int* s_flag) {
     const int tid = threadIdx.x;
@@ -171,9 +171,10 @@ __device__ bool dec_fold_gather(const PK& P, int base, int n, unsigned tag, amp_
     if (tid == 0) *s_flag = 1;
     __syncthreads();
     if (tid < 256) {
-        if (tid < n) {
-            const __amdgpu_buffer_rsrc_t rs = gran_rsrc(P.dwg, (unsigned)((base + n) * 256));
-            const int off = (base + tid) * 256;
+        // thread i folds records i, i + 256, ... in order: vamp_decide_fold's order at 256 threads
+        const __amdgpu_buffer_rsrc_t rs = gran_rsrc(P.dwg, (unsigned)((base + n) * 256));
+        for (int i = tid; i < n; i += 256) {
+            const int off = (base + i) * 256;
             u32x4 g[13];
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {

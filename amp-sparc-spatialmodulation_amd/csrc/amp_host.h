@@ -173,6 +173,11 @@ int hook_failure(const char* what);   // sets the error text, returns AMP_E_LAUN
 
 int check_dims(const amp_dims* d, const amp_constellation* c, bool tiled = true);
 int device_cu_count();   // compute units of the current device (cached)
+// amp_stream_create_cu_range's registry (amp_weights.hip): the CU range of a stream it made, and the
+// claim of a range by one grid of a shard generation on an exchange buffer (false: the range
+// overlaps one already claimed for that buffer and generation)
+bool cu_range_of(hipStream_t st, int* cu0, int* cu1);
+bool shard_claim_range(const void* xbuf, unsigned gen, int cu0, int cu1);
 
 // Launch path of the persistent (grid-synchronising) engines: a plain launch after the
 // co-residency check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).

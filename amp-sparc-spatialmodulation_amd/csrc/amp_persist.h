@@ -196,13 +196,21 @@ __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast
 // PIN: keep each ring refill behind the group's MFMAs (a scheduling barrier): the compiler then
 // cannot hoist the next group's loads into fresh registers — the ring holds exactly R groups (the
 // two-waves-per-SIMD engines, which have 256 registers per wave, use R = 2 with it).
-template <int NT, int G, int R = 1, bool PIN = false>
+// HL: the two leading-piece products of each group (a0 b0 of Ar.Xr and of Ai.Xi, ~2^0 relative)
+// accumulate apart from the ten cross-piece products (<= 2^-8 relative), and the two sums are
+// added once at the end: the f32 rounding of the large running sum then happens 2 times per
+// group instead of 12 (the VAMP engine's GEMM error against float64: DESIGN.md §4 item 5).
+template <int NT, int G, int R = 1, bool PIN = false, bool HL = false>
 __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const void* __restrict__ wq, int ct0,
                                         f32x4 (&cr)[NT], f32x4 (&ci)[NT]) {
     constexpr int RR = G < R ? G : R;
+    constexpr int NL = HL ? NT : 1;
     const int lane = threadIdx.x & 63;
+    f32x4 lr[NL], li[NL];
 #pragma unroll
     for (int t = 0; t < NT; ++t) { cr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; ci[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+    for (int t = 0; t < NL; ++t) { lr[t] = f32x4{0.f, 0.f, 0.f, 0.f}; li[t] = f32x4{0.f, 0.f, 0.f, 0.f}; }
     const int ct0u = __builtin_amdgcn_readfirstlane(ct0);
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (char*)const_cast<void*>(wq) + (size_t)ct0u * G * 6 * 1024, (short)0, 0x7ffffff0, 0x00020000);
@@ -250,18 +258,24 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
         for (int t = 0; t < NT; ++t) {
             const u32x4* w = ring[d][t];
             f32x4 gr = cr[t], gi = ci[t];
+            f32x4 sr = HL ? lr[HL ? t : 0] : gr, si = HL ? li[HL ? t : 0] : gi;   // the cross-piece sums
 #define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
             // smallest terms first
-            AMP_MF(gr, a[0], w[2]);  AMP_MF(gi, a[0], w[5]);
-            AMP_MF(gr, a[1], w[1]);  AMP_MF(gi, a[1], w[4]);
-            AMP_MF(gr, a[2], w[0]);  AMP_MF(gi, a[2], w[3]);
-            AMP_MF(gr, na[0], w[5]); AMP_MF(gi, a[3], w[2]);
-            AMP_MF(gr, na[1], w[4]); AMP_MF(gi, a[4], w[1]);
-            AMP_MF(gr, na[2], w[3]); AMP_MF(gi, a[5], w[0]);
-            AMP_MF(gr, a[0], w[1]);  AMP_MF(gi, a[0], w[4]);
-            AMP_MF(gr, a[1], w[0]);  AMP_MF(gi, a[1], w[3]);
-            AMP_MF(gr, na[0], w[4]); AMP_MF(gi, a[3], w[1]);
-            AMP_MF(gr, na[1], w[3]); AMP_MF(gi, a[4], w[0]);
+            AMP_MF(sr, a[0], w[2]);  AMP_MF(si, a[0], w[5]);
+            AMP_MF(sr, a[1], w[1]);  AMP_MF(si, a[1], w[4]);
+            AMP_MF(sr, a[2], w[0]);  AMP_MF(si, a[2], w[3]);
+            AMP_MF(sr, na[0], w[5]); AMP_MF(si, a[3], w[2]);
+            AMP_MF(sr, na[1], w[4]); AMP_MF(si, a[4], w[1]);
+            AMP_MF(sr, na[2], w[3]); AMP_MF(si, a[5], w[0]);
+            AMP_MF(sr, a[0], w[1]);  AMP_MF(si, a[0], w[4]);
+            AMP_MF(sr, a[1], w[0]);  AMP_MF(si, a[1], w[3]);
+            AMP_MF(sr, na[0], w[4]); AMP_MF(si, a[3], w[1]);
+            AMP_MF(sr, na[1], w[3]); AMP_MF(si, a[4], w[0]);
+            if constexpr (HL) {
+                lr[HL ? t : 0] = sr; li[HL ? t : 0] = si;
+            } else {
+                gr = sr; gi = si;
+            }
             AMP_MF(gr, a[0], w[0]);  AMP_MF(gi, a[0], w[3]);
             AMP_MF(gr, na[0], w[3]); AMP_MF(gi, a[3], w[0]);
 #undef AMP_MF
@@ -276,6 +290,10 @@ __device__ __forceinline__ void gemm_x3(const unsigned short* sP, int ldx, const
                     ring[d][t][f] = __builtin_amdgcn_raw_buffer_load_b128(wr, vo, ((t * G + g + RR) * 6 + f) * 1024, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (HL) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) { cr[t] += lr[HL ? t : 0]; ci[t] += li[HL ? t : 0]; }
     }
 }
 

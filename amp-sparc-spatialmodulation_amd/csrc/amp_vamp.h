@@ -287,6 +287,7 @@ constexpr int PBM = 16;   // trials per workgroup
 
 bool vamp_persist_eligible(const amp_dims* d, int k, int ncu, int epochs = 1, int gemm = AMP_GEMM_AUTO);
 int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu, int gemm = AMP_GEMM_AUTO);
+int vamp_persist_wg_per_cu(const amp_dims* d, int k, int gemm);   // resident workgroups per CU of the launch
 int vamp_gemm_select(const amp_dims* d, int k, int gemm);   // 0 f32, 1 bf16x3, 2 fp16x2 (amp_vamp.hip)
 bool vamp_persist_x3_fits(int N, int k, int L);
 bool vamp_persist_ytil_in_kernel(const VampK& P);

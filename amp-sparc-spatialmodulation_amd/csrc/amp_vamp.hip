@@ -893,6 +893,13 @@ int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm) {
     return vamp_persist_max_epochs(d, k, device_cu_count(), gemm);
 }
 
+int amp_vamp_epochs_ch_eligible(const amp_dims* d, int32_t k, int32_t gemm) {
+    if (!d || k <= 0 || d->B <= 0 || gemm < AMP_GEMM_AUTO || gemm > AMP_GEMM_I8) return 0;
+    if (vamp_persist_max_epochs(d, k, device_cu_count(), gemm) < 1) return 0;
+    const int x3 = vamp_gemm_select(d, k, gemm);   // the check of amp_vamp_detect_count_epochs_ch
+    return ((x3 == 1 || x3 == 3) && ytil_x3_fits(d->n, k)) ? 1 : 0;
+}
+
 size_t amp_vamp_epochs_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter, int32_t epochs) {
     if (!d || k <= 0 || max_iter <= 0 || epochs < 1 || (long)d->B * epochs > (1L << 30)) return 0;
     amp_dims de = *d;
@@ -1018,7 +1025,24 @@ int amp_vamp_shard_reset(void* xbuf, void* stream) {
 
 int amp_vamp_detect_count_shard(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                 const amp_vamp_decide_args* dec, const amp_vamp_shard* sh, void* stream) {
-    AMP_REQUIRE(d && sh && sh->xbuf, "amp_vamp_detect_count_shard: null argument");
+    AMP_REQUIRE(d && sh && sh->xbuf && a, "amp_vamp_detect_count_shard: null argument");
+    // Co-residency by construction: every shard's grid spins on its partners' partials,
+    // so all of them must be resident at once.  Two plain streams may share one hardware queue (there
+    // are GPU_MAX_HW_QUEUES = 4 per process), and then the second grid's dispatch waits behind the
+    // first grid's spin until its bounded wait aborts (gpurun r5c7; tools/shard_queue_probe.py).  So
+    // a shard runs only on a stream of amp_stream_create_cu_range (its own queue and CUs), its
+    // workgroups must fit that CU range, and the ranges of one generation's shards must not overlap.
+    hipStream_t st = (hipStream_t)stream;
+    const bool any_stream = diag_env("AMP_SHARD_ANY_STREAM") != nullptr;   // (the probe's diagnostic build only)
+    int cu0 = 0, cu1 = 0;
+    if (!any_stream) {
+        AMP_REQUIRE(cu_range_of(st, &cu0, &cu1),
+                    "amp_vamp_detect_count_shard: the stream must come from amp_stream_create_cu_range (plain streams "
+                    "may share a hardware queue, and a shard's grid would then wait behind its partner's spin)");
+        AMP_REQUIRE(d->B > 0 && (long)cdiv(d->B, PBM) <= (long)vamp_persist_wg_per_cu(d, a->k, a->gemm) * (cu1 - cu0),
+                    "amp_vamp_detect_count_shard: %d workgroups do not fit the stream's CUs [%d, %d)", cdiv(d->B, PBM),
+                    cu0, cu1);
+    }
     AMP_REQUIRE(sh->row_offset >= 0 && sh->row_offset % PBM == 0 && sh->row_offset + d->B <= sh->B_global &&
                     (d->B % PBM == 0 || sh->row_offset + d->B == sh->B_global),
                 "amp_vamp_detect_count_shard: rows [%d, %d) of %d (a shard starts at a multiple of %d trials and "
@@ -1033,11 +1057,13 @@ int amp_vamp_detect_count_shard(const amp_dims* d, const amp_constellation* c, c
     const ShardX x = shard_carve(sh->xbuf, nwx, a->max_iter);
     AMP_REQUIRE(sh->xbuf_bytes >= x.bytes, "amp_vamp_detect_count_shard: exchange buffer %zu < %zu bytes",
                 sh->xbuf_bytes, x.bytes);
+    AMP_REQUIRE(any_stream || shard_claim_range(sh->xbuf, sh->gen, cu0, cu1),
+                "amp_vamp_detect_count_shard: CUs [%d, %d) overlap another shard of generation %u on this exchange "
+                "buffer (the shards' grids must be co-resident: disjoint CU ranges)", cu0, cu1, sh->gen);
     VampK P;
     Const64 c64;
     int rc = vamp_setup(d, c, a, P, c64);     // this shard's rows: workspace, operators, y~
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
     rc = vamp_persist_prepare(P, a, st);
     if (rc) return rc;
     // the batch's exchange: this grid's workgroups at their global index, the batch's size for

@@ -90,6 +90,10 @@ static int persist_wg_cap(int N, int gemm_mode) {
     return (N == 64 && (gemm_mode == 1 || gemm_mode == 2) && persist_wg2()) ? 2 : 1;
 }
 
+int vamp_persist_wg_per_cu(const amp_dims* d, int k, int gemm) {
+    return persist_wg_cap(d->N, vamp_gemm_select(d, k, gemm));
+}
+
 int vamp_persist_max_epochs(const amp_dims* d, int k, int ncu, int gemm) {
     const int gemm_mode = vamp_gemm_select(d, k, gemm);
     if (k != d->N || !(d->N == 64 || d->N == 128 || d->N == 256) || d->M > 64) return 0;

@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         } else if constexpr (H2)
             gemm_h2<NC, G3>(sP, ldx, Wx1, cc0, cr, ci);
         else if constexpr (X3)
-            gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx1, cc0, cr, ci);
+            gemm_x3<NC, G3, X3R, X3PIN, true>(sP, ldx, Wx1, cc0, cr, ci);
         else
             gemm16<NT, NT * NWV>(sA, lda, P.Wq1, ct0, acc);   // G = 2N / 16 = NT * NWV
         float hsc[4];                                 // H2: 2^-(e_row + H2_EX) of this lane's rows
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
 #pragma unroll
                     for (int r = 0; r < 4; ++r) { cr[t2][r] *= hsc[r]; ci[t2][r] *= hsc[r]; }
             }
-            if constexpr (!I8 && !H2) gemm_x3<NC, G3, X3R, X3PIN>(sP, ldx, Wx2, cc0, cr, ci);
+            if constexpr (!I8 && !H2) gemm_x3<NC, G3, X3R, X3PIN, true>(sP, ldx, Wx2, cc0, cr, ci);
             r_epi(cc0, cr, ci);
         } else {
         gemm16<NT, NT * NWV>(sA, lda, P.Wq2, ct0, acc);

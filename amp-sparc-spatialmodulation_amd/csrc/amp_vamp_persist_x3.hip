@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
     __syncthreads();
     f32x4 cr[NC], ci[NC];
     const void* wop = (const char*)wq + (long long)(row0 / rows_per_op) * wq_stride;
-    gemm_x3<NC, G, 1>(sP, ldx, wop, wave * NC, cr, ci);
+    gemm_x3<NC, G, 1, false, true>(sP, ldx, wop, wave * NC, cr, ci);   // HL: the engines' accumulation
 #pragma unroll
     for (int t = 0; t < NC; ++t) {
         const int o = 16 * (wave * NC + t) + (lane & 15);
@@ -88,10 +88,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void ytil_x3_kernel(const float* __res
 // D: operator groups in flight (the kernel has registers to spare: 94 VGPRs at D = 1).  hook():
 // called once after the first group's MFMAs (the next stage's y loads go there, behind this
 // stage's first operator loads in the in-order vmcnt).
+// lr / li: the cross-piece sums, apart from the leading-piece sums cr / ci (gemm_x3's HL form; the
+// caller adds them once after the last stage).
 template <int GH, int D, class Hook>
 __device__ __forceinline__ void x3_rows2(const unsigned short* sP0, const unsigned short* sP1, int ldx,
                                          __amdgpu_buffer_rsrc_t wr, int gbase, f32x4 (&cr)[2], f32x4 (&ci)[2],
-                                         Hook&& hook) {
+                                         f32x4 (&lr)[2], f32x4 (&li)[2], Hook&& hook) {
     const int lane = threadIdx.x & 63;
     const int vo = lane * 16;
     u32x4 ring[D][6];
@@ -124,23 +126,23 @@ __device__ __forceinline__ void x3_rows2(const unsigned short* sP0, const unsign
             else if (g + 1 < GH) lda(g + 1, 0, anx);
 #pragma unroll
             for (int f = 0; f < 3; ++f) na[f] = a[3 + f] ^ sgn;
-            f32x4 gr = cr[rt], gi = ci[rt];
+            f32x4 gr = cr[rt], gi = ci[rt], sr = lr[rt], si = li[rt];
 #define AMP_MF(acc, x, y) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(x), as_bf16x8(y), acc, 0, 0, 0)
-            // gemm_x3's product order (smallest terms first)
-            AMP_MF(gr, a[0], w[2]);  AMP_MF(gi, a[0], w[5]);
-            AMP_MF(gr, a[1], w[1]);  AMP_MF(gi, a[1], w[4]);
-            AMP_MF(gr, a[2], w[0]);  AMP_MF(gi, a[2], w[3]);
-            AMP_MF(gr, na[0], w[5]); AMP_MF(gi, a[3], w[2]);
-            AMP_MF(gr, na[1], w[4]); AMP_MF(gi, a[4], w[1]);
-            AMP_MF(gr, na[2], w[3]); AMP_MF(gi, a[5], w[0]);
-            AMP_MF(gr, a[0], w[1]);  AMP_MF(gi, a[0], w[4]);
-            AMP_MF(gr, a[1], w[0]);  AMP_MF(gi, a[1], w[3]);
-            AMP_MF(gr, na[0], w[4]); AMP_MF(gi, a[3], w[1]);
-            AMP_MF(gr, na[1], w[3]); AMP_MF(gi, a[4], w[0]);
+            // gemm_x3's product order (smallest terms first), HL form
+            AMP_MF(sr, a[0], w[2]);  AMP_MF(si, a[0], w[5]);
+            AMP_MF(sr, a[1], w[1]);  AMP_MF(si, a[1], w[4]);
+            AMP_MF(sr, a[2], w[0]);  AMP_MF(si, a[2], w[3]);
+            AMP_MF(sr, na[0], w[5]); AMP_MF(si, a[3], w[2]);
+            AMP_MF(sr, na[1], w[4]); AMP_MF(si, a[4], w[1]);
+            AMP_MF(sr, na[2], w[3]); AMP_MF(si, a[5], w[0]);
+            AMP_MF(sr, a[0], w[1]);  AMP_MF(si, a[0], w[4]);
+            AMP_MF(sr, a[1], w[0]);  AMP_MF(si, a[1], w[3]);
+            AMP_MF(sr, na[0], w[4]); AMP_MF(si, a[3], w[1]);
+            AMP_MF(sr, na[1], w[3]); AMP_MF(si, a[4], w[0]);
             AMP_MF(gr, a[0], w[0]);  AMP_MF(gi, a[0], w[3]);
             AMP_MF(gr, na[0], w[3]); AMP_MF(gi, a[3], w[0]);
 #undef AMP_MF
-            cr[rt] = gr; ci[rt] = gi;
+            cr[rt] = gr; ci[rt] = gi; lr[rt] = sr; li[rt] = si;
             if (rt == 0 || g + 1 < GH) {
 #pragma unroll
                 for (int f = 0; f < 6; ++f) acur[f] = anx[f];
@@ -177,6 +179,8 @@ __global__ __launch_bounds__(512, 1) void ytil_x3_r2_kernel(const float* __restr
         const_cast<char*>(wop) + (size_t)ctu * G * 6 * 1024, (short)0, 0x7ffffff0, 0x00020000);
     f32x4 cr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     f32x4 ci[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 lr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 li[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     // stage h's KS columns of the 32 rows: 8 complex values per item, rows fastest; the next
     // stage's loads are in flight while this stage's GEMM runs
     constexpr int ITEMS = 32 * (KS >> 3), PER = ITEMS / 512;
@@ -205,10 +209,12 @@ __global__ __launch_bounds__(512, 1) void ytil_x3_r2_kernel(const float* __restr
             x3_store8(row < 16 ? sP0 : sP1, ldx, row & 15, j0, re, im);
         }
         __syncthreads();
-        x3_rows2<GH, AMP_YTIL_RING>(sP0, sP1, ldx, wr, h * GH, cr, ci, [&] {
+        x3_rows2<GH, AMP_YTIL_RING>(sP0, sP1, ldx, wr, h * GH, cr, ci, lr, li, [&] {
             if (h + 1 < NH) load_stage(h + 1);
         });
     }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) { cr[rt] += lr[rt]; ci[rt] += li[rt]; }
     const int o = 16 * ct + (lane & 15);
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)

@@ -2,6 +2,9 @@
 #include <stdarg.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "amp_gemm.h"
 #include <hip/hip_ext.h>
@@ -482,6 +485,37 @@ int hook_failure(const char* what) {
 
 }  // namespace amp
 
+namespace amp {
+// The CU range of every stream amp_stream_create_cu_range made (until amp_stream_destroy), and per
+// shard exchange buffer the ranges its current generation's grids were launched on: what
+// amp_vamp_detect_count_shard checks before it launches a grid that spins on its partners.
+static std::mutex g_cu_mu;
+static std::map<hipStream_t, std::pair<int, int>> g_cu_streams;
+static std::map<const void*, std::pair<unsigned, std::vector<std::pair<int, int>>>> g_shard_ranges;
+
+bool cu_range_of(hipStream_t st, int* cu0, int* cu1) {
+    std::lock_guard<std::mutex> lk(g_cu_mu);
+    const auto it = g_cu_streams.find(st);
+    if (it == g_cu_streams.end()) return false;
+    *cu0 = it->second.first;
+    *cu1 = it->second.second;
+    return true;
+}
+
+bool shard_claim_range(const void* xbuf, unsigned gen, int cu0, int cu1) {
+    std::lock_guard<std::mutex> lk(g_cu_mu);
+    auto& e = g_shard_ranges[xbuf];
+    if (e.first != gen) {
+        e.first = gen;
+        e.second.clear();
+    }
+    for (const auto& r : e.second)
+        if (cu0 < r.second && r.first < cu1) return false;
+    e.second.emplace_back(cu0, cu1);
+    return true;
+}
+}  // namespace amp
+
 extern "C" {
 
 int amp_set_allreduce_hook(amp_allreduce_fn fn, void* ctx) {
@@ -505,11 +539,19 @@ int amp_stream_create_cu_range(int32_t cu0, int32_t cu1, void** stream) {
     hipStream_t st = nullptr;
     const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask);
     AMP_REQUIRE(e == hipSuccess, "amp_stream_create_cu_range: %s", hipGetErrorString(e));
+    {
+        std::lock_guard<std::mutex> lk(amp::g_cu_mu);
+        amp::g_cu_streams[st] = {cu0, cu1};
+    }
     *stream = st;
     return AMP_OK;
 }
 
 int amp_stream_destroy(void* stream) {
+    {
+        std::lock_guard<std::mutex> lk(amp::g_cu_mu);
+        amp::g_cu_streams.erase((hipStream_t)stream);
+    }
     const hipError_t e = hipStreamDestroy((hipStream_t)stream);
     AMP_REQUIRE(e == hipSuccess, "amp_stream_destroy: %s", hipGetErrorString(e));
     return AMP_OK;

@@ -144,6 +144,7 @@ class Model(nn.Module):
         if self.rank == 0:
             os.makedirs(self.path, exist_ok=True)
         self.group_cap = 0
+        self._ch_ok = None
         if group_epochs:
             if detector != 'vamp' or not hasattr(self.amp, 'forward_epochs'):
                 raise ValueError('group_epochs: side-by-side epochs are built for the VAMP detector')
@@ -176,12 +177,36 @@ class Model(nn.Module):
                 chunk.append((x, sym, idx, y, self._svd))
             chans = [v[4] for v in chunk]
             if all(c is chans[0] for c in chans):
-                U, s, Vh = chans[0]
+                runs = [chunk]
+            elif self._per_epoch_channels():
+                runs = [chunk]
             else:
-                U, s, Vh = [c[0] for c in chans], [c[1] for c in chans], [c[2] for c in chans]
-            out += self.amp.forward_epochs(U, s, Vh, [v[3] for v in chunk], SNR, [v[0] for v in chunk],
-                                           [v[1] for v in chunk], [v[2] for v in chunk])
+                # this arithmetic / shape takes one shared channel per launch only (e.g. GEMM_F32, or
+                # n != 2k): the chunk goes as runs of epochs that share a channel (single epochs at res = 1)
+                runs, cur = [], [chunk[0]]
+                for v in chunk[1:]:
+                    if v[4] is cur[-1][4]:
+                        cur.append(v)
+                    else:
+                        runs.append(cur)
+                        cur = [v]
+                runs.append(cur)
+            for run in runs:
+                cs = [v[4] for v in run]
+                if all(c is cs[0] for c in cs):
+                    U, s, Vh = cs[0]
+                else:
+                    U, s, Vh = [c[0] for c in cs], [c[1] for c in cs], [c[2] for c in cs]
+                out += self.amp.forward_epochs(U, s, Vh, [v[3] for v in run], SNR, [v[0] for v in run],
+                                               [v[1] for v in run], [v[2] for v in run])
         return out
+
+    def _per_epoch_channels(self) -> bool:
+        """Whether one launch may hold epochs with different channels (VAMP.epochs_channels_eligible)."""
+        if self._ch_ok is None:
+            n, N = self.config.Nr * self.config.Lout, self.config.Nt * self.config.Lin
+            self._ch_ok = self.amp.epochs_channels_eligible(min(n, N))
+        return self._ch_ok
 
     def _inputs(self, SNR: float, new_channel: bool):
         if new_channel:

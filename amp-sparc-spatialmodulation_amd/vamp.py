@@ -331,6 +331,15 @@ class VAMP(LazyResult, nn.Module):
             return 0
         return int(nat.lib().amp_vamp_max_epochs_gemm(C.byref(d), k, self.gemm))
 
+    def epochs_channels_eligible(self, k: int) -> bool:
+        """Whether forward_epochs takes one channel per epoch for this config and GEMM arithmetic
+        (amp_vamp_epochs_ch_eligible: the bf16x3 / int8x4 engine and n == 2 k); otherwise a call
+        must share one channel across its epochs."""
+        if self.max_epochs(k) < 1:
+            return False
+        d = self.config.dims()
+        return bool(nat.lib().amp_vamp_epochs_ch_eligible(C.byref(d), k, self.gemm))
+
     def epochs_eligible(self, n: int, k: int, epochs: int) -> bool:
         """Whether `epochs` forwards of this config fit ONE persistent launch
         (amp_vamp_detect_count_epochs)."""

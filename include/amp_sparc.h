@@ -264,6 +264,10 @@ int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
 /* The same for a given persistent GEMM arithmetic (amp_vamp_args.gemm): two workgroups per CU
  * only where that arithmetic has the two-per-CU build (the split-precision forms at N = 64). */
 int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm);
+/* 1 when amp_vamp_detect_count_epochs_ch takes ONE CHANNEL PER EPOCH for this config and GEMM
+ * arithmetic (the bf16x3 / int8x4 engine and n == 2 k), else 0 (then a chunk of epochs must share
+ * one channel, as amp_vamp_detect_count_epochs). */
+int amp_vamp_epochs_ch_eligible(const amp_dims* d, int32_t k, int32_t gemm);
 int amp_vamp_detect_count_epochs(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a,
                                  const amp_vamp_decide_args* dec, int32_t epochs, void* stream);
 /* The same with ONE CHANNEL PER EPOCH — Model.simulate at the reference's default res = 1

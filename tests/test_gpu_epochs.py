@@ -183,6 +183,33 @@ def test_simulate_group_epochs_res1_identical(device, tmp_path):
             assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
 
 
+@pytest.mark.parametrize('gemm', ['f32', 'x3_n_ne_2k'])
+def test_simulate_group_epochs_res1_shared_channel_only(device, tmp_path, gemm):
+    """Where one launch cannot hold a channel per epoch (amp_vamp_epochs_ch_eligible: GEMM_F32, or
+    n != 2 k), Model.simulate(group_epochs=True) at res = 1 sends runs of one channel and still writes
+    the points of the per-epoch loop (round-5 advisor: these runs failed with AMP_E_ARG)."""
+    import amp_native as nat
+    from model import Model
+    from vamp import VAMP
+    if gemm == 'f32':
+        cfg, g = _cfg(64, 4, 128, 1024, '16QAM'), nat.GEMM_F32
+    else:
+        cfg, g = _cfg(64, 4, 192, 1024, '16QAM'), nat.GEMM_AUTO   # n = 192 != 2 k = 128
+    det = VAMP(cfg, gemm=g)
+    assert not det.epochs_channels_eligible(64)
+    outs = []
+    for grouped in (False, True):
+        m = Model(cfg, 'vamp', path=str(tmp_path / f'r{int(grouped)}'), amp=VAMP(cfg, gemm=g), seed=5,
+                  group_epochs=grouped)
+        if grouped:
+            assert m.group_cap >= 1
+        outs.append(m.simulate(epochs=6, start=6.0, final=8.0, step=2.0, res=1))
+    assert len(outs[0]) == len(outs[1])
+    for a, b in zip(*outs):
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+
+
 def test_epochs_independent_rare_path(device):
     """One epoch driven into the exact float64 rare path (its y scaled up: logits beyond the
     float64 range of the global shift) while the others are not: the per-epoch barrier counters

@@ -164,3 +164,47 @@ def test_persistent_shards_equal_whole_batch(device, Nt, Na, Nr, B, alphabet, eb
         else:
             assert abs(tot[f] - getattr(wct, f)) <= 1e-12 * max(1.0, abs(getattr(wct, f))), f
     assert whole['T'] == wst.T
+
+
+def test_persistent_shard_stream_checks(device):
+    """amp_vamp_detect_count_shard refuses, before launching, every launch whose grid could fail to
+    be co-resident with its partners: a plain stream (two of them may share a
+    hardware queue: gpurun r5c7's lost grid), a CU range its workgroups do not fit, and a range
+    overlapping another shard of the same generation; then the valid pair runs to the whole batch's T."""
+    import amp_native as nat
+    from test_gpu_vamp import _config, _regen_inputs
+    from vamp import VAMP, PersistentShard, read_result
+    B = 4096
+    cfg = _config(256, 8, 512, B, '16QAM', iterations=20)
+    inp = _regen_inputs(cfg, 3, 8.0)
+    det = VAMP(cfg, engine=2)
+    L = det(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'], inp['x'], inp['sym'], inp['idx'])
+    T_whole = int(L.loss['T'])
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    half = ncu // 2
+    xbuf = PersistentShard.xbuf(cfg, device)
+    nat.check(nat.lib().amp_vamp_shard_reset(nat.dptr(xbuf), nat.stream_ptr(device)), 'reset')
+    torch.cuda.synchronize()
+    sym = torch.as_tensor(np.asarray(inp['sym'], np.int64)).reshape(B, cfg.L)
+    idx = torch.as_tensor(np.asarray(inp['idx'], np.int64)).reshape(B, cfg.L)
+    rows = B // 2
+    gen = 0x5EED0000 + ncu
+
+    def launch(b0, stream):
+        sh = PersistentShard(cfg, b0, rows)
+        with torch.cuda.stream(stream):
+            return sh.launch(inp['U'], inp['s'], inp['Vh'], inp['y'][b0:b0 + rows], inp['SNR'],
+                             inp['x'][b0:b0 + rows], sym[b0:b0 + rows], idx[b0:b0 + rows], xbuf, gen=gen)
+
+    with pytest.raises(nat.AmpError, match='amp_stream_create_cu_range'):
+        launch(0, torch.cuda.Stream(device))
+    with pytest.raises(nat.AmpError, match='do not fit'):
+        launch(0, nat.cu_range_stream(0, half // 2, device))
+    r0 = launch(0, nat.cu_range_stream(0, half, device))
+    with pytest.raises(nat.AmpError, match='overlap'):
+        launch(rows, nat.cu_range_stream(half // 2, half + half // 2, device))
+    r1 = launch(rows, nat.cu_range_stream(half, ncu, device))
+    torch.cuda.synchronize()
+    for res in (r0, r1):
+        st, _ = read_result(res)
+        assert st.nan_state >= 0 and st.T == T_whole, (st.nan_state, st.T, T_whole)

@@ -150,13 +150,17 @@ class FakeGroupedAmp(FakeAmp):
     (one shared channel, or one per epoch) and returns one Loss per epoch, the values a function
     of the epoch's y, so grouped and sequential sweeps can be compared."""
 
-    def __init__(self, config, cap):
+    def __init__(self, config, cap, ch_ok=True):
         super().__init__(config)
         self.cap = cap
+        self.ch_ok = ch_ok
         self.groups = []
 
     def max_epochs(self, k):
         return self.cap
+
+    def epochs_channels_eligible(self, k):
+        return self.ch_ok
 
     def _one(self, y):
         L = Loss(self.L.config) if hasattr(self.L, 'config') else Loss(_cfg())
@@ -177,17 +181,19 @@ class FakeGroupedAmp(FakeAmp):
         return [self._one(y) for y in ys]
 
 
-@pytest.mark.parametrize('res,cap', [(1, 4), (4, 3), (2, 8)])
-def test_simulate_group_epochs_host_logic(tmp_path, res, cap):
+@pytest.mark.parametrize('res,cap,ch_ok', [(1, 4, True), (4, 3, True), (2, 8, True), (1, 4, False), (2, 8, False)])
+def test_simulate_group_epochs_host_logic(tmp_path, res, cap, ch_ok):
     """Model.simulate(group_epochs=True) draws the epochs' inputs in the reference's call order
     (vamp_model.py:55-61: a channel when i % res == 0), hands chunks of at most max_epochs epochs to
     forward_epochs — one channel per epoch when the chunk spans channels (res = 1), the shared one
-    otherwise — and writes the same points as the sequential sweep."""
+    otherwise — and writes the same points as the sequential sweep.  Where the detector takes one
+    shared channel per launch only (ch_ok False: GEMM_F32 or n != 2k, amp_vamp_epochs_ch_eligible),
+    every call holds epochs of one channel."""
     from model import Model
     cfg = _cfg()
     outs, amps = [], []
     for grouped in (False, True):
-        amp = FakeGroupedAmp(cfg, cap)
+        amp = FakeGroupedAmp(cfg, cap, ch_ok)
         m = Model(cfg, 'vamp', path=str(tmp_path / f'g{int(grouped)}'), amp=amp, seed=3, group_epochs=grouped)
         outs.append(m.simulate(epochs=10, start=0, final=1.0, step=1, res=res))
         amps.append(amp)
@@ -197,7 +203,9 @@ def test_simulate_group_epochs_host_logic(tmp_path, res, cap):
     for n, per, Us in grp.groups:
         distinct = len({id(u) for u in Us})
         assert per == (distinct > 1), (n, per, distinct)
-        if res == 1:
+        if not ch_ok:
+            assert distinct == 1 and n <= res   # one channel per call
+        elif res == 1:
             assert distinct == n          # a channel per epoch
     # the channels each epoch was detected with: the same matrices in both sweeps
     grouped_U = [u for _, _, Us in grp.groups for u in Us]

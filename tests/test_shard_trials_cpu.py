@@ -150,3 +150,26 @@ def test_sharded_hook_gloo(tmp_path):
         assert o['rc'][:2] == [0, 0] and o['rc'][2] == 1 and 'outside the workspace' in o['err']
         assert o['w'] == [1.0 + 2.0, 0.0 - 2.0, 1.0, 7.0]       # SUM of words 0-1, MAX of words 2-3
         assert o['slice'] == [r * 8 // world, (r + 1) * 8 // world]
+
+
+def test_persistent_shard_refuses_plain_stream():
+    """amp_vamp_detect_count_shard launches a grid that spins on its partner shards' partials, so it
+    refuses (AMP_E_ARG, before any device call) a stream that amp_stream_create_cu_range did not
+    make: plain streams may share one hardware queue, and a shard's grid then waits behind its
+    partner's spin until the bounded wait aborts (gpurun r5c7)."""
+    import ctypes as C
+    import amp_native as nat
+    from config import Config
+    cfg = Config(256, 8, 512, 1, 1, batch=2048, generator_mode='sparc', iterations=20, alphabet='16QAM',
+                 channel_profile='uniform', channel_truncation='tail', device='cpu')
+    d, cst = cfg.dims(), cfg.constellation()
+    a = nat.AmpVampArgs()
+    a.k, a.max_iter, a.engine, a.gemm = 256, 20, nat.ENGINE_PERSISTENT, nat.GEMM_AUTO
+    dec = nat.AmpVampDecideArgs()
+    sh = nat.AmpVampShard()
+    sh.xbuf, sh.xbuf_bytes, sh.B_global, sh.row_offset, sh.gen = 0x1000, 1 << 20, 4096, 0, 7
+    for stream in (None, 0x1234):   # the null stream, a handle the library never made
+        rc = nat.lib().amp_vamp_detect_count_shard(C.byref(d), C.byref(cst), C.byref(a), C.byref(dec), C.byref(sh),
+                                                   stream)
+        assert rc == -1, rc   # AMP_E_ARG
+        assert 'amp_stream_create_cu_range' in nat.lib().amp_last_error().decode()

@@ -48,6 +48,10 @@ for s in ${STEPS:-bench}; do
     cfg3) run cfg3 300 python3 tools/configs_bench.py cfg3 cfg3-qpsk ;;
     cfg3w4) run cfg3w4 300 env AMP_SCAMP_X3_WAVES=4 python3 tools/configs_bench.py cfg3 cfg3-qpsk ;;
     tests_vamp) run tests_vamp 900 $PYT tests/test_gpu_vamp.py -m gpu ;;
+    qprobe) run_nogate qprobe 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_diag.so AMP_SHARD_ANY_STREAM=1 python3 tools/shard_queue_probe.py 8 ;;
+    tests_shard) run tests_shard 600 $PYT tests/test_gpu_shard_trials.py tests/test_gpu_epochs.py -m gpu ;;
+    acc) run acc 300 python3 tools/gemm_accuracy.py --variants launches,persistent,persistent-f32 ;;
+    tests_q4) run_nogate tests_q4 600 python3 -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_vamp.py -m gpu -k "curve_point and cfg4 and persistent and not f32 and not h2 and not i8" ;;
     tests_epochs) run tests_epochs 600 $PYT tests/test_gpu_epochs.py -m gpu ;;
     tests_cfg5) run tests_cfg5 900 $PYT tests/test_gpu_cfg5.py -m gpu ;;
     tests_bs) run tests_bs 900 $PYT tests/test_gpu_bamp_scamp.py -m gpu ;;
