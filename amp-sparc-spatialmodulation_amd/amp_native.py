@@ -114,6 +114,8 @@ SIGNATURES = {
     'amp_vamp_max_epochs': (C.c_int, [_D, _I]),
     'amp_vamp_max_epochs_gemm': (C.c_int, [_D, _I, _I]),
     'amp_vamp_epochs_ch_eligible': (C.c_int, [_D, _I, _I]),
+    'amp_debug_persist_timing': (C.c_int, [_I]),
+    'amp_debug_persist_time': (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
     'amp_set_allreduce_hook': (C.c_int, [_P, _P]),
     'amp_vamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpVampArgs), _I, _P]),
     'amp_bamp_run_sharded': (C.c_int, [_D, _K, C.POINTER(AmpBampArgs), _I, _P]),

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "amp_vamp_persist_kernel.h"
 
@@ -118,15 +119,32 @@ int persist_dispatch_x3(const VampK& P, const DecConst& dc, hipStream_t st);   /
 int persist_dispatch_h2(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_h2.hip
 int persist_dispatch_i8(const VampK& P, const DecConst& dc, hipStream_t st);   // amp_vamp_persist_i8.hip
 
+// amp_debug_persist_timing: while on, a HIP event pair around every vamp_persist launch (bench.py
+// times the kernel inside a loop of forwards, the conditions of its timed region).
+static std::mutex g_tm_mu;
+static bool g_tm_on = false;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tm_ev;
+
 // c64 is the rare path's float64 table; dc the decision's (dec_on) — one by-value table in the
 // launch: dc's Const64 base is overwritten with c64.
 int vamp_persist_launch(const VampK& P, const Const64& c64, const DecConst& dc, hipStream_t st, int ncu) {
     (void)ncu;
     DecConst d2 = dc;
     static_cast<Const64&>(d2) = c64;
+    hipEvent_t te[2] = {nullptr, nullptr};
+    {
+        std::lock_guard<std::mutex> lk(g_tm_mu);
+        if (g_tm_on && hipEventCreate(&te[0]) == hipSuccess && hipEventCreate(&te[1]) == hipSuccess) {
+            g_tm_ev.emplace_back(te[0], te[1]);
+            (void)hipEventRecord(te[0], st);
+        } else {
+            te[0] = te[1] = nullptr;
+        }
+    }
     // the decision's counter records are folded inside the launch (amp_decide_fused.h
     // dec_fold_gather; a shard folds its own workgroups), else by one block per epoch here
     const int rc = persist_dispatch(P, d2, st);
+    if (te[1]) (void)hipEventRecord(te[1], st);
     if (rc || !P.dec_on || P.fold_in) return rc;
     hipLaunchKernelGGL(vamp_decide_fold, dim3(P.E), dim3(256), 0, st, (const DecWG*)P.dwg, P.nwg / P.E, P.counts);
     AMP_LAUNCH_CHECK("vamp_decide_fold");
@@ -150,3 +168,29 @@ static int persist_dispatch(const VampK& P, const DecConst& dc, hipStream_t st) 
 }
 
 }  // namespace amp
+
+int amp_debug_persist_timing(int32_t on) {
+    std::lock_guard<std::mutex> lk(amp::g_tm_mu);
+    amp::g_tm_on = on != 0;
+    return AMP_OK;
+}
+
+int amp_debug_persist_time(int32_t* n, float* mean_ms) {
+    AMP_REQUIRE(n && mean_ms, "amp_debug_persist_time: null output");
+    std::lock_guard<std::mutex> lk(amp::g_tm_mu);
+    double tot = 0.0;
+    int cnt = 0;
+    for (auto& e : amp::g_tm_ev) {
+        float ms = 0.f;
+        if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+            tot += ms;
+            ++cnt;
+        }
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    amp::g_tm_ev.clear();
+    *n = cnt;
+    *mean_ms = cnt ? (float)(tot / cnt) : 0.f;
+    return AMP_OK;
+}

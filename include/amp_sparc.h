@@ -157,6 +157,11 @@ int amp_vamp_select_gemm(const amp_dims* d, int32_t k, int32_t gemm);
  * phase into trace (device, nwg * max_iter * 10 + 4 * nwg uint64; layout in amp_vamp.hip). */
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,
                            void* stream);
+/* Diagnostic (bench.py): while on != 0, every persistent VAMP launch records a HIP event pair
+ * around its vamp_persist kernel on its stream; amp_debug_persist_time synchronises them, returns
+ * how many launches were timed and their mean duration in ms, and clears the record. */
+int amp_debug_persist_timing(int32_t on);
+int amp_debug_persist_time(int32_t* n, float* mean_ms);
 size_t amp_vamp_workspace_bytes(const amp_dims* d, int32_t k, int32_t max_iter);
 int amp_vamp_run(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* stream);
 /* Layer-level pieces of amp_vamp_run: prepare = Tracker (vamp.py:13-28);

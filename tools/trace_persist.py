@@ -120,8 +120,8 @@ def arrival_spread(a, st, nwg, iters, Tn):
     per iteration, in cycles.  s_memtime counts each XCD's own clock (its own origin), so stamps
     are put on one time base with the per-workgroup (s_memtime, s_memrealtime) pairs taken at
     kernel start and end: rate = d memtime / d realtime (cycles per 10 ns tick), and
-    t = realtime_start + (memtime - memtime_start) / rate.  Within one XCD (workgroups wg, wg + 8,
-    ... on round-robin dispatch) the raw s_memtime values are compared directly as a check."""
+    t = realtime_start + (memtime - memtime_start) / rate.  (Raw s_memtime values are never compared
+    across workgroups: their origins differ, even within one XCD.)"""
     base = nwg * iters * STRIDE
     m0, r0 = a[base:base + 2 * nwg:2].astype(np.float64), a[base + 1:base + 2 * nwg:2].astype(np.float64)
     m1, r1 = a[base + 2 * nwg::2].astype(np.float64), a[base + 2 * nwg + 1::2].astype(np.float64)
