@@ -178,6 +178,7 @@ int device_cu_count();   // compute units of the current device (cached)
 // overlaps one already claimed for that buffer and generation)
 bool cu_range_of(hipStream_t st, int* cu0, int* cu1);
 bool shard_claim_range(const void* xbuf, unsigned gen, int cu0, int cu1);
+void shard_forget(const void* xbuf);   // amp_vamp_shard_reset: a new forward on this buffer
 
 // Launch path of the persistent (grid-synchronising) engines: a plain launch after the
 // co-residency check (default), or hipLaunchCooperativeKernel (AMP_PERSIST_LAUNCH=coop).

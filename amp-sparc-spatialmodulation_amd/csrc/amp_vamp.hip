@@ -1018,6 +1018,7 @@ size_t amp_vamp_shard_xbuf_bytes(int32_t B_global, int32_t max_iter) {
 
 int amp_vamp_shard_reset(void* xbuf, void* stream) {
     AMP_REQUIRE(xbuf, "amp_vamp_shard_reset: null buffer");
+    shard_forget(xbuf);   // the next forward's shards claim their CU ranges afresh
     const hipError_t e = hipMemsetAsync(xbuf, 0, PBAR_WORDS * sizeof(unsigned), (hipStream_t)stream);
     AMP_REQUIRE(e == hipSuccess, "amp_vamp_shard_reset: %s", hipGetErrorString(e));
     return AMP_OK;

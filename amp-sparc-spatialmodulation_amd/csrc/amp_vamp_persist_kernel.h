@@ -78,8 +78,31 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // I8 (with X3): the split-precision GEMMs in the int8x4 form (gemm_i8: eight int8 digit planes of
 // the A operand, each row with its own exponent; the operators i8-packed with per-column
 // exponents); the results come out of the GEMM fully scaled.
+// The kernel arguments (VampK at kernarg offset 0, DecConst behind it: 2.6 KB) are read through the
+// kernarg segment pointer, laundered at the top of every iteration (karg_launder): the compiler
+// then reloads a field (s_load, scalar cache) where an iteration uses it instead of hoisting every
+// field the loop reads into an SGPR for the whole launch, which spilled ~390 SGPRs into VGPR lanes
+// (v_readlane in every phase) and ~75 VGPRs to scratch in the eight-wave cfg4 build.
+constexpr int KARG_DC_OFF = (int)((sizeof(VampK) + alignof(DecConst) - 1) / alignof(DecConst) * alignof(DecConst));
+typedef const __attribute__((address_space(4))) char* KargPtr;
+template <class T>
+__device__ __forceinline__ const T* karg_at(unsigned long long base, int off) {
+    return (const T*)(const __attribute__((address_space(4))) T*)(KargPtr)(base + (unsigned long long)off);
+}
+__device__ __forceinline__ unsigned long long karg_launder(unsigned long long v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+
 template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
-__global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P, DecConst dc) {
+__global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_arg, DecConst dc_arg) {
+    (void)P_arg;
+    (void)dc_arg;
+    unsigned long long kbase = (unsigned long long)(KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    const VampK* Pp = karg_at<VampK>(kbase, 0);
+    const DecConst* Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
+#define P (*Pp)
+#define dc (*Dp)
     static_assert(!X3 || ((NWV == 4 || (NWV == 8 && !H2 && OCC == 1)) && NT % 2 == 0),
                   "X3: four waves (eight for the bf16x3 two-waves-per-SIMD form), whole complex tiles");
     static_assert(!(H2 && I8) && (!I8 || X3), "I8: a split-precision form of its own");
@@ -95,7 +118,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     // eight waves: no A-fragment prefetch in gemm_x3 (the partner wave covers the LDS reads;
     // 24 registers fewer) when AMP_X3_W8_PIN (A/B builds)
     constexpr bool X3PIN = NWV == 8 && AMP_X3_W8_PIN;
-    const Const64& c64 = dc;
+#define c64 (static_cast<const Const64&>(*Dp))
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int s_flag;
     __shared__ double s_d[PWG / 64][4];
@@ -120,12 +143,13 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     const int lrow0 = wl * PBM;                       // first trial within the epoch (the batch's index)
     // its row in this launch's arrays (a shard holds rows [row_off, row_off + its B) of the batch)
     const int row0 = ep * P.B + lrow0 - P.row_off, nrows = min(PBM, P.B - lrow0);
-    unsigned* ebar = P.pbar + (P.E > 1 ? PBAR_EPOCH + ep : 0);   // this epoch's arrival counter
+#define ebar (P.pbar + (P.E > 1 ? PBAR_EPOCH + ep : 0))   // this epoch's arrival counter
     const int N = P.N, twoN = 2 * N, twok = 2 * P.k, M = P.M, spr = N / M;
     // this epoch's channel (one per epoch, or one shared: wch = sch = 0)
     const float* const sv_ep = P.s + (size_t)ep * P.sch;
-    const void* const Wx1 = (const char*)P.Wx1 + ep * P.wch;
-    const void* const Wx2 = (const char*)P.Wx2 + ep * P.wch;
+    // (formed where used, from the laundered arguments: not live across the loop)
+#define Wx1 ((const void*)((const char*)P.Wx1 + ep * P.wch))
+#define Wx2 ((const void*)((const char*)P.Wx2 + ep * P.wch))
     const int ldr = Y.ldr, lda = Y.lda;
     const int ct0 = wave * NT;                 // this wave's 16-column tiles (both GEMMs: 2k == 2N)
     const int cc0 = wave * NC;                 // X3: this wave's complex 16-column tiles
@@ -270,7 +294,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         trc[(size_t)nwg * P.max_iter * AMP_TRACE_STRIDE + 2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
     }
     unsigned nbar = 0;
-    const __amdgpu_buffer_rsrc_t grs = gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwx) * 32u);
+#define grs (gran_rsrc(P.pparts, (unsigned)(P.max_iter * nwx) * 32u))
     int fixed = 0, last_t = 0, aborted = 0;
     VampIter nx = cur;
     // 5. batch scalars of iteration te (its partials published): every workgroup gathers and reduces
@@ -365,6 +389,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
     };
 
     for (int t = 0; t < P.max_iter; ++t) {
+        kbase = karg_launder(kbase);
+        Pp = karg_at<VampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
         last_t = t;
         stamp(t, 0);
         const float* vprev = lds + ((t & 1) ? Y.offV0 : Y.offV1);
@@ -649,6 +676,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
         PDenoisePolicy pol{sR, sX, vnew, vprev, sM, sS, ldr, M, 31 - __builtin_clz(spr), N, cur.inv_sigma2};
         if (P.dump) pol.dbg = P.dump + (((size_t)t * nwg + wg) * 5 + 4) * PBM * twoN;
         PartAcc pa;
+        kbase = karg_launder(kbase);
+        Pp = karg_at<VampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
         stamp(t, 4);
         if constexpr (KK > 16)
             denoise_sections_wide_m<true, KK>(pol, nrows * spr, M, P.c, pa);
@@ -711,6 +741,13 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P,
             }
         }
     }
+#undef P
+#undef dc
+#undef c64
+#undef ebar
+#undef Wx1
+#undef Wx2
+#undef grs
 }
 
 int device_cu_count();

@@ -502,6 +502,11 @@ bool cu_range_of(hipStream_t st, int* cu0, int* cu1) {
     return true;
 }
 
+void shard_forget(const void* xbuf) {
+    std::lock_guard<std::mutex> lk(g_cu_mu);
+    g_shard_ranges.erase(xbuf);
+}
+
 bool shard_claim_range(const void* xbuf, unsigned gen, int cu0, int cu1) {
     std::lock_guard<std::mutex> lk(g_cu_mu);
     auto& e = g_shard_ranges[xbuf];

@@ -141,7 +141,7 @@ def test_persistent_shards_equal_whole_batch(device, Nt, Na, Nr, B, alphabet, eb
         sh = PersistentShard(cfg, b0, b1 - b0)
         with torch.cuda.stream(st):
             results.append(sh.launch(inp['U'], inp['s'], inp['Vh'], inp['y'][b0:b1], inp['SNR'], inp['x'][b0:b1],
-                                     sym[b0:b1], idx[b0:b1], xbuf, gen=0x51A2D000 + B + R))
+                                     sym[b0:b1], idx[b0:b1], xbuf, gen=0x51A2D000 + 16 * B + 4 * R + (alphabet == 'QPSK')))
         shards.append(sh)
     torch.cuda.synchronize()
     tot = {f: 0 for f, _ in nat.AmpCounts._fields_}

@@ -221,21 +221,24 @@ VARIANTS = {'launches': (1, 0), 'persistent': (2, 0), 'persistent-f32': (2, 1), 
 
 
 # (curve, point, variant) -> measured T where an engine's allclose exit leaves the span of the
-# reference's own reruns (the exit is decided by O(1) elements of 10^6 at
-# these points, and the engines' GEMM accumulation rounding differs from the CPU BLAS's).
-# Measured on MI355X (gpurun_out r5c8, every other g4 point and variant inside its span):
-# * cfg4-QPSK 0 dB seed 1: the reference stops at 12 (its 29 reruns: 12-17); every engine, the
-#   f32-MFMA and launch forms included, runs to the cap (the GEMM
-#   accumulation error, not the denoiser, decides it; the oracle with float32-accumulated GEMMs
-#   also reaches the cap at this point's seed-0 neighbour, tools/gemm_order_probe.py);
-# * the opt-in int8x4 form at three 1 dB points where the reference runs to the cap (its reruns:
-#   20, 18-20 and 20) stops earlier: 18, 16, 14.  VER / SER stay within 1e-3 at all of them.
+# reference's own reruns: open parity gaps, reported as expected failures (strict: an entry whose
+# point comes back inside the span fails, so the list cannot go stale).  VER / SER stay enforced.
+# The exit at these points is decided by O(1) elements of 10^6, i.e. by the
+# GEMMs' accumulation rounding.  Measured on MI355X (gpurun r6c12, every other g4 point and variant
+# inside its span):
+# * cfg4-QPSK 0 dB seed 1: the reference stops at 12 (its reruns: 12-17).  The default engine's
+#   GEMMs now accumulate the leading-piece and cross-piece products apart (gemm_x3 HL: one-iteration
+#   r error rms 5.0e-8 against float64, the reference's BLAS path 6.5e-8, round 5's 1.21e-7) and stop
+#   at 12; the launch and f32-MFMA engines (f32 accumulation, rms 1.45e-7) still run to the cap;
+# * 1 dB, seeds 0 and 2: the reference runs to the cap in every rerun; the two engines more accurate
+#   than it — the default (HL) and the opt-in int8x4 — stop earlier (18 / 17 and 18 / 14).  (int8x4
+#   at seed 1 stopped at 16 with round 5's y~; with the HL y~ it runs to 20, inside the span.)
 T_DIVERGENCE = {
     ('cfg4_vamp_qpsk', '1/0', 'launches'): 20,
-    ('cfg4_vamp_qpsk', '1/0', 'persistent'): 20,
     ('cfg4_vamp_qpsk', '1/0', 'persistent-f32'): 20,
+    ('cfg4_vamp_qpsk', '0/1', 'persistent'): 18,
+    ('cfg4_vamp_qpsk', '2/1', 'persistent'): 17,
     ('cfg4_vamp_qpsk', '0/1', 'persistent-i8'): 18,
-    ('cfg4_vamp_qpsk', '1/1', 'persistent-i8'): 16,
     ('cfg4_vamp_qpsk', '2/1', 'persistent-i8'): 14,
 }
 
@@ -260,10 +263,15 @@ def test_vamp_curve_point(device, name, key, variant):
     assert abs(float(got['ser']) - ref['ser']) <= 1e-3, (float(got['ser']), ref['ser'])
     known = T_DIVERGENCE.get((name, key, variant))
     if known is not None:
-        # a measured exit divergence at a point whose allclose exit is decided by rounding
-        # (DESIGN.md §4 item 5): pinned to the measured T, so any change shows up
-        assert int(got['T']) == known, (int(got['T']), known, ref['T'])
-        return
+        # an open exit-parity gap (above): an expected failure while T stays outside the reference's
+        # span; a pass means the entry is stale
+        try:
+            _check_T(int(got['T']), int(ref['T']), ent['iterations'], ref['ver'], ref.get('T_pert'), ref.get('T_span'))
+        except AssertionError:
+            pytest.xfail(f'T {int(got["T"])} (measured {known}) outside the reference span at {name} {key} ({variant}): '
+                         'the allclose exit is decided by GEMM accumulation rounding (DESIGN.md §4 item 5)')
+        pytest.fail(f'{name} {key} {variant}: T {int(got["T"])} is inside the reference span: delete its '
+                    'T_DIVERGENCE entry')
     _check_T(int(got['T']), int(ref['T']), ent['iterations'], ref['ver'], ref.get('T_pert'), ref.get('T_span'))
 
 

@@ -41,7 +41,8 @@ def main():
     streams = [torch.cuda.Stream(dev) for _ in range(K)]
     rows = B // 2
     print(f'{K} plain streams; shard A on s[0], shard B on s[j]; cfg4 16-QAM, 2 x {rows} trials', flush=True)
-    for j in list(range(1, K)) + [1]:
+    for npair, j in enumerate(list(range(1, K)) + [1]):
+        gen = 0x0DE50000 + npair   # one generation per forward: the same for both shards of the pair
         nat.check(nat.lib().amp_vamp_shard_reset(nat.dptr(xbuf), nat.stream_ptr(dev)), 'reset')
         torch.cuda.synchronize()
         res, ev = [], []
@@ -52,7 +53,7 @@ def main():
                 e0.record(st)
                 res.append(sh.launch(inp['U'], inp['s'], inp['Vh'], inp['y'][b0:b0 + rows], inp['SNR'],
                                      inp['x'][b0:b0 + rows], sym[b0:b0 + rows], idx[b0:b0 + rows], xbuf,
-                                     gen=0x0DE50000 + 16 * j + len(ev)))
+                                     gen=gen))
                 e1.record(st)
             ev.append((e0, e1))
         torch.cuda.synchronize()
