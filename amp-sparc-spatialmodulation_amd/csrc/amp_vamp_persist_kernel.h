@@ -619,6 +619,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
         }
         __syncthreads();
         stamp(t, 3);
+        kbase = karg_launder(kbase);
+        Pp = karg_at<VampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
         // 3. x~ = V w + r~ ; r = (x~ - alpha r~) / (1 - alpha)   (vamp.py:72, 79)
         // r = (x~ - alpha r~) / (1 - alpha) for the complex column tiles ccs ... of this wave.  The
         // lane index pinned here: the 4 NC LDS addresses below are then formed in this epilogue
@@ -701,6 +704,9 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
             }
         }
         stamp(t, 5);
+        kbase = karg_launder(kbase);
+        Pp = karg_at<VampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
         if (!exchange(t, vnew, vprev)) { aborted = 1; break; }
         if (nx.stopped || t + 1 == P.max_iter) break;
         cur = nx;
