@@ -101,6 +101,29 @@ __device__ __forceinline__ int pl_opaque(int x) {
     return x;
 }
 
+// ---- kernel arguments through a laundered kernarg pointer (the persistent engines) ----
+// A persistent kernel's loop reads dozens of argument fields; left alone, the compiler hoists all
+// of them into SGPRs for the whole launch.  Reading them through the kernarg segment pointer,
+// passed through an empty asm at chosen points (karg_launder), makes each phase reload what it uses
+// (s_load from the scalar cache).  karg_second_offset: the kernarg offset of a kernel's second
+// by-value argument (the first at 0; the amdhsa metadata's .args offsets agree).
+typedef const __attribute__((address_space(4))) char* KargPtr;
+template <class A, class B>
+constexpr int karg_second_offset() {
+    return (int)((sizeof(A) + alignof(B) - 1) / alignof(B) * alignof(B));
+}
+template <class T>
+__device__ __forceinline__ const T* karg_at(unsigned long long base, int off) {
+    return (const T*)(const __attribute__((address_space(4))) T*)(KargPtr)(base + (unsigned long long)off);
+}
+__device__ __forceinline__ unsigned long long karg_launder(unsigned long long v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned long long karg_base() {
+    return (unsigned long long)(KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 // ---- split-precision complex GEMM (bf16x3) ----
 // x = x0 + x1 + x2 with bf16 pieces (round-to-nearest-even; each residual is exact in f32), so
 // a product a.b keeps the six terms a0b0 a0b1 a1b0 a0b2 a1b1 a2b0 (dropped terms <= 2^-24 |ab|)

@@ -96,11 +96,21 @@ __device__ __forceinline__ float block_psi(const float* xrow, int lc, int Nt, in
 // NWV: waves per workgroup — 4 (one per SIMD) or, for bf16x3, 8 (two per SIMD, 256 registers
 // each, half the column tiles per wave; the per-point packed denoiser is then replaced by the
 // scalar one, the 16-point alphabets keep the packed product grid: DESIGN.md §3.1, §3.8).
+// The arguments are read through the laundered kernarg pointer (amp_persist.h karg_launder), as in
+// vamp_persist: the eight-wave cfg3 build held them in SGPRs for the whole launch (387 spilled).
+constexpr int SKARG_DC_OFF = karg_second_offset<ScampK, DecConst>();
 template <int NT1, int G1, int NT2, int G2, int KK, bool X3, bool H2 = false, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, DecConst dc) {
+__global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P_arg, DecConst dc_arg) {
+    (void)P_arg;
+    (void)dc_arg;
+    unsigned long long kbase = karg_base();
+    const ScampK* Pp = karg_at<ScampK>(kbase, 0);
+    const DecConst* Dp = karg_at<DecConst>(kbase, SKARG_DC_OFF);
+#define P (*Pp)
+#define dc (*Dp)
+#define c64 (static_cast<const Const64&>(*Dp))   // the rare path's float64 table; dc also the fused decision's (dec_on)
     constexpr int PWG = 64 * NWV, NW = NWV;
     static_assert(NWV == 4 || (NWV == 8 && X3 && !H2), "eight waves: the bf16x3 form only");
-    const Const64& c64 = dc;   // the rare path's float64 table; dc also the fused decision's (dec_on)
     constexpr int NC1 = X3 ? NT1 / 2 : 1, NC2 = X3 ? NT2 / 2 : 1;
     static_assert(!X3 || (NT1 % 2 == 0 && NT2 % 2 == 0), "X3: whole complex tiles");
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -172,6 +182,9 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
     };
 
     for (int t = 0; t < P.max_iter; ++t) {
+        kbase = karg_launder(kbase);
+        Pp = karg_at<ScampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, SKARG_DC_OFF);
         last_t = t;
         stamp(t, 0);
         float* psi_prev = lds + ((t & 1) ? Y.offP0 : Y.offP1);
@@ -396,6 +409,9 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
         }
         __syncthreads();
         stamp(t, 4);
+        kbase = karg_launder(kbase);
+        Pp = karg_at<ScampK>(kbase, 0);
+        Dp = karg_at<DecConst>(kbase, SKARG_DC_OFF);
         // 4. denoiser -> x, then psi and its allclose count
         SPDenoisePolicy pol{sR, sX, sITau, sM, sA, ldx, M, 31 - __builtin_clz(spr), Nt, Lin};
         PartAcc pa;
@@ -569,6 +585,9 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P, Dec
             }
         }
     }
+#undef P
+#undef dc
+#undef c64
 }
 
 int device_cu_count();

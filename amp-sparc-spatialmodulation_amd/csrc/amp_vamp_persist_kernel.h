@@ -79,26 +79,18 @@ __host__ __device__ inline PLayout playout(int N, int k, int L, bool x3 = false)
 // the A operand, each row with its own exponent; the operators i8-packed with per-column
 // exponents); the results come out of the GEMM fully scaled.
 // The kernel arguments (VampK at kernarg offset 0, DecConst behind it: 2.6 KB) are read through the
-// kernarg segment pointer, laundered at the top of every iteration (karg_launder): the compiler
-// then reloads a field (s_load, scalar cache) where an iteration uses it instead of hoisting every
-// field the loop reads into an SGPR for the whole launch, which spilled ~390 SGPRs into VGPR lanes
-// (v_readlane in every phase) and ~75 VGPRs to scratch in the eight-wave cfg4 build.
-constexpr int KARG_DC_OFF = (int)((sizeof(VampK) + alignof(DecConst) - 1) / alignof(DecConst) * alignof(DecConst));
-typedef const __attribute__((address_space(4))) char* KargPtr;
-template <class T>
-__device__ __forceinline__ const T* karg_at(unsigned long long base, int off) {
-    return (const T*)(const __attribute__((address_space(4))) T*)(KargPtr)(base + (unsigned long long)off);
-}
-__device__ __forceinline__ unsigned long long karg_launder(unsigned long long v) {
-    asm volatile("" : "+s"(v));
-    return v;
-}
+// kernarg segment pointer, laundered at the top of every iteration and before the denoiser, GEMM2
+// and the exchange (amp_persist.h karg_launder): the compiler then reloads a field (s_load, scalar
+// cache) where a phase uses it instead of hoisting every field the loop reads into an SGPR for the
+// whole launch, which spilled ~390 SGPRs into VGPR lanes (v_readlane in every phase) and ~75 VGPRs
+// to scratch in the eight-wave cfg4 build.
+constexpr int KARG_DC_OFF = karg_second_offset<VampK, DecConst>();
 
 template <int NT, int KK, int NWV, int DU, bool X3, int OCC = 1, bool H2 = false, bool I8 = false>
 __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_arg, DecConst dc_arg) {
     (void)P_arg;
     (void)dc_arg;
-    unsigned long long kbase = (unsigned long long)(KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    unsigned long long kbase = karg_base();
     const VampK* Pp = karg_at<VampK>(kbase, 0);
     const DecConst* Dp = karg_at<DecConst>(kbase, KARG_DC_OFF);
 #define P (*Pp)

@@ -124,22 +124,24 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = threadIdx.x; i < P.nzero; i += blockDim.x) P.zero[i] = 0u;
     if (J.packed == WPACKX3) {
-        // bf16x3 planes of X itself (no real expansion): kap = J, ncp = O (complex counts).  One
-        // thread per 16-byte chunk of x3_index's layout: lane l of (tile ct, group g) holds
-        // X[16 ct + (l & 15)][32 g + 8 (l >> 4) .. + 7], so thread e takes lane e & 63 of block
-        // e >> 6 and writes one whole chunk per plane (64 threads: 1 KB contiguous per plane)
-        unsigned short* w3 = reinterpret_cast<unsigned short*>(J.wt);
+        // bf16x3 planes of X itself (no real expansion): kap = J, ncp = O (complex counts).  Lane l
+        // of (tile ct, group g) holds X[16 ct + (l & 15)][32 g + 8 (l >> 4) .. + 7] (x3_index) as one
+        // 16-byte chunk per plane; thread e takes the element pair e & 3 of chunk e >> 2 (lane
+        // (e >> 2) & 63 of block e >> 8) and writes its 4-byte word of every plane: consecutive
+        // threads write consecutive words (1 KB per plane per 256 threads), and the launch has
+        // enough threads to cover the load latency (one per chunk was latency-bound: 7.4 us)
+        unsigned* w3 = reinterpret_cast<unsigned*>(J.wt);
         const int gpt = J.kap >> 5;                               // groups per 16-column tile
-        const long tot = (long)(J.ncp >> 4) * gpt * 64;
+        const long tot = (long)(J.ncp >> 4) * gpt * 256;
         for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
-            const int l = (int)(e & 63);
-            const long blk = e >> 6;
+            const int part = (int)(e & 3), l = (int)((e >> 2) & 63);
+            const long blk = e >> 8;
             const int ct = (int)(blk / gpt), g = (int)(blk - (long)ct * gpt);
-            const int o = 16 * ct + (l & 15), j0 = 32 * g + 8 * (l >> 4);
-            float xr[8], xi[8];
+            const int o = 16 * ct + (l & 15), j0 = 32 * g + 8 * (l >> 4) + 2 * part;
+            float xr[2], xi[2];
             const float s = (J.rowscale && o < J.O) ? J.rowscale[o] : 1.0f;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < 2; ++q) {
                 const int j = j0 + q;
                 float a = 0.f, b = 0.f;
                 if (o < J.O && j < J.J) {
@@ -154,17 +156,12 @@ __global__ void build_cweights_kernel(CWeightJobs P) {
                 xr[q] = a;
                 xi[q] = b;
             }
-            u32x4 c[6];
+            unsigned c[6];
+            split3x2(xr[0], xr[1], c[0], c[1], c[2]);
+            split3x2(xi[0], xi[1], c[3], c[4], c[5]);
+            unsigned* dst = w3 + ((size_t)blk * 6 * 64 + l) * 4 + part;
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                unsigned a0, a1, a2, b0, b1, b2;
-                split3x2(xr[2 * h], xr[2 * h + 1], a0, a1, a2);
-                split3x2(xi[2 * h], xi[2 * h + 1], b0, b1, b2);
-                c[0][h] = a0; c[1][h] = a1; c[2][h] = a2; c[3][h] = b0; c[4][h] = b1; c[5][h] = b2;
-            }
-            u32x4* dst = reinterpret_cast<u32x4*>(w3 + ((size_t)blk * 6 * 64 + l) * 8);
-#pragma unroll
-            for (int f = 0; f < 6; ++f) dst[f * 64] = c[f];   // plane f of the block: 64 chunks of 16 B
+            for (int f = 0; f < 6; ++f) dst[f * 256] = c[f];   // plane f: 64 chunks of 4 words
         }
         return;
     }
