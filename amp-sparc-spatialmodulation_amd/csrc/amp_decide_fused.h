@@ -41,28 +41,31 @@ __device__ __forceinline__ void decide_epilogue(const PK& P, const DecConst& dc,
     const long long* gsym = P.sym + (size_t)row0 * L;
     const long long* gidx = P.idx + (size_t)row0 * L;
     {
-        // PBM rows of 2N floats = PBM * N / 2 float4: all loads in flight before the LDS stores
-        constexpr int CH = 8;
+        // PBM rows of 2N floats = PBM * N / 2 float4: all eight loads in flight before the LDS
+        // stores, at a clamped index with no branch (a lane past the end rewrites the last element
+        // with the same value).  Named values, not an array: inlined into the engines, a float4[8]
+        // stayed a 128-byte scratch array per lane (written by every workgroup: ~17 MB of
+        // WRITE_SIZE per cfg4 launch)
         const int tot = nrows * (N >> 1);
-        for (int e0 = 0; e0 < tot; e0 += PWG * CH) {
-            float4 v[CH];
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    v[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.xtrue) +
-                                                            (size_t)(row0 + row) * 2 * N + c4);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int e = e0 + u * PWG + tid;
-                if (e < tot) {
-                    const int row = e / (N >> 1), c4 = 4 * (e - row * (N >> 1));
-                    *reinterpret_cast<float4*>(sT + row * ldr + c4) = v[u];
-                }
-            }
+        auto at = [&](int e) {
+            e = min(e, tot - 1);
+            const int row = e / (N >> 1);
+            return make_int2(row, 4 * (e - row * (N >> 1)));
+        };
+        auto ldv = [&](int e) {
+            const int2 rc = at(e);
+            return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.xtrue) +
+                                                    (size_t)(row0 + rc.x) * 2 * N + rc.y);
+        };
+        auto stv = [&](int e, const float4& v) {
+            const int2 rc = at(e);
+            *reinterpret_cast<float4*>(sT + rc.x * ldr + rc.y) = v;
+        };
+        for (int e0 = tid; e0 < tot; e0 += 8 * PWG) {
+            const float4 v0 = ldv(e0), v1 = ldv(e0 + PWG), v2 = ldv(e0 + 2 * PWG), v3 = ldv(e0 + 3 * PWG);
+            const float4 v4 = ldv(e0 + 4 * PWG), v5 = ldv(e0 + 5 * PWG), v6 = ldv(e0 + 6 * PWG), v7 = ldv(e0 + 7 * PWG);
+            stv(e0, v0); stv(e0 + PWG, v1); stv(e0 + 2 * PWG, v2); stv(e0 + 3 * PWG, v3);
+            stv(e0 + 4 * PWG, v4); stv(e0 + 5 * PWG, v5); stv(e0 + 6 * PWG, v6); stv(e0 + 7 * PWG, v7);
         }
     }
     if (stage) {
