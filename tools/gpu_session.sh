@@ -37,7 +37,7 @@ for s in ${STEPS:-bench}; do
            run ab_du1 300 env AMP_LIB_PATH=amp-sparc-spatialmodulation_amd/lib_diag/libampsparc_w8du1.so python3 bench.py --no-cpu-baseline &&
            run ab_def2 300 python3 bench.py --no-cpu-baseline ;;
     bench_i8) run bench_i8 300 python3 bench.py --no-cpu-baseline --gemm i8 ;;
-    trace_i8) run trace_i8 300 env AMP_VAMP_GEMM=i8 python3 tools/trace_persist.py --config cfg4 ;;
+    trace_i8) run trace_i8 300 python3 tools/trace_persist.py --config cfg4 --gemm i8 ;;
     tests_i8) run tests_i8 900 $PYT tests/test_gpu_vamp.py -m gpu -k "i8 or split_engines" ;;
     bench_f32) run bench_f32 300 python3 bench.py --no-cpu-baseline --gemm f32 ;;
     trace) run trace 300 python3 tools/trace_persist.py --config cfg4 ;;

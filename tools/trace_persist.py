@@ -2,7 +2,7 @@
 """Phase timing of the persistent engines (amp_vamp_persist_trace / amp_scamp_persist_trace): per
 iteration and workgroup s_memtime stamps -> median cycles per phase, barrier skew across workgroups.
 
-  python tools/trace_persist.py [--config cfg4] [--ebn0 8]
+  python tools/trace_persist.py [--config cfg4] [--ebn0 8] [--gemm auto|x3|f32|h2|i8]
   python tools/trace_persist.py --config cfg3        (SCAMP, tools/configs_bench.py's cfg3 inputs)
 """
 import argparse
@@ -76,6 +76,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='cfg4')
     ap.add_argument('--ebn0', type=float, default=None)
+    ap.add_argument('--gemm', default='auto', choices=['auto', 'x3', 'f32', 'h2', 'i8'])
     args = ap.parse_args()
     if args.config.startswith('cfg3'):
         return scamp_trace(args.config, args.ebn0)
@@ -86,7 +87,9 @@ def main():
                  channel_profile='uniform', channel_truncation='tail', device='cuda')
     dev = torch.device('cuda', 0)
     inp = bench.make_inputs(cfg, 0, args.ebn0, dev)
-    det = VAMP(cfg, engine=nat.ENGINE_PERSISTENT)
+    gemm = {'auto': nat.GEMM_AUTO, 'x3': nat.GEMM_X3, 'f32': nat.GEMM_F32, 'h2': nat.GEMM_H2,
+            'i8': nat.GEMM_I8}[args.gemm]
+    det = VAMP(cfg, engine=nat.ENGINE_PERSISTENT, gemm=gemm)
     for _ in range(3):
         det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
     T = det.detect(inp['U'], inp['s'], inp['Vh'], inp['y'], inp['SNR'])
