@@ -97,7 +97,7 @@ def cpu_baseline(cfgname, EbN0, seed, sample_trials, repeats=3):
 # The PMC summary (tools/profile.sh -> tools/prof_summary.py) of THIS build's default command, per
 # GEMM arithmetic; `roofline.traffic` names it (`traffic_source`).  The counters cannot be read by
 # the timed run itself (rocprofv3 --pmc replays the launch), so the file is the measurement.
-TRAFFIC_PROFILE = {'bf16x3': 'profiles/r06_cfg4_vamp_x3_write.txt', 'fp16x2': 'profiles/r03_cfg4_vamp_swz.txt'}
+TRAFFIC_PROFILE = {'bf16x3': 'profiles/r06_cfg4_vamp_x3.txt', 'fp16x2': 'profiles/r03_cfg4_vamp_swz.txt'}
 
 
 def traffic_from_profile(persistent, gname):
