@@ -1,6 +1,11 @@
 #!/usr/bin/env bash
 # Same-box A/B of the persistent VAMP engine's epilogue parts (diagnostic builds whose results are
 # wrong by construction: no output stores / no fused decision / no in-kernel fold), in-loop time.
+# The libraries need guards in amp_vamp_persist_kernel.h's epilogue (#ifndef AMP_DIAG_NO_OUT around
+# the r / xmmse / var stores, AMP_DIAG_NO_DECIDE around decide_epilogue, AMP_DIAG_NO_FOLD on the
+# fold condition; profiles/r06_epilogue_cost.txt) and are built in the container, e.g.
+#   make -C amp-sparc-spatialmodulation_amd/csrc SPILLCHECK=true OBJDIR=../build_nofold \
+#     OUT=../lib_diag/libampsparc_nofold.so CXXFLAGS="<Makefile flags> -DAMP_DIAG_NO_FOLD=1" ../lib_diag/libampsparc_nofold.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-epi}; mkdir -p "$OUT"
