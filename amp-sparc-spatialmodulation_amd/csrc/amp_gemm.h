@@ -263,6 +263,12 @@ __device__ __forceinline__ void gemm_tile(const AL& al, const float* __restrict_
 #pragma unroll
                 for (int j = 0; j < C::NACC; ++j) ring[d][j] = wcol[j][(size_t)gn * 64];
                 acur = anext;
+                // the next group's A read goes out BEFORE this group's MFMAs: left alone the
+                // scheduler put it after them, into the registers they read, and every group then
+                // waited out the LDS latency with one wave per SIMD (lgkmcnt(0) before its MFMAs)
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 4 * C::NACC, 0);      // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x020, C::NACC, 0);          // VMEM read
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
