@@ -764,7 +764,7 @@ int amp_vamp_run_sharded(const amp_dims* d, const amp_constellation* c, const am
 
 // Diagnostic: one persistent-engine forward whose workgroups stamp s_memtime at every phase
 // boundary: trace[(wg * max_iter + t) * 10 + phase], phases = start, r~ built, GEMM1, w stored,
-// GEMM2 + r, partial published, barrier passed, scalars ready, (unused), denoiser done; then per
+// GEMM2 + r, partial published, barrier passed, scalars ready, denoiser done, vamp_advance started; then per
 // workgroup [nwg * max_iter * 10 + 2 * wg] = s_memtime / s_memrealtime at kernel start and
 // [nwg * max_iter * 10 + 2 * nwg + 2 * wg] the same pair at its end (trace: 4 nwg more words).
 int amp_vamp_persist_trace(const amp_dims* d, const amp_constellation* c, const amp_vamp_args* a, void* trace,

@@ -264,8 +264,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
             }
         }
     }
-    const S2Lane s2l = s2_lane(P, sv_ep);     // s^2 in registers for the per-iteration LMMSE sum
-    VampIter cur = vamp_first_iter(P, scr, &s2l);   // vamp.py:26, 66-82 at t = 0
+    VampIter cur;
+    {
+        const S2Lane s2l = s2_lane(P, sv_ep);     // s^2 for the first LMMSE sum (re-read per exchange below)
+        cur = vamp_first_iter(P, scr, &s2l);      // vamp.py:26, 66-82 at t = 0
+    }
     // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
     {
         const float p = (float)P.sparsity;
@@ -294,6 +297,11 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
     // vnew / vprev: te's var buffers.  False: a grid exchange timed out (the grid is released).
     auto exchange = [&](int te, float* vnew, const float* vprev) -> bool {
             PartAcc g;
+            // this lane's s^2 for the LMMSE sum of vamp_advance, loaded here so that the loads
+            // complete during the gather's wait: through the per-phase kernel-argument pointer
+            // they are not hoisted out of the loop (held across it, the values were spilled, and
+            // vamp_advance waited on their scratch reload)
+            const S2Lane s2x = s2_lane(P, P.s + (size_t)ep * P.sch);
             const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)te + 1u;
             if (!part_gather(grs, ((unsigned)te * nwx + wg0) * 32u, P.wpe, tag, P.pbar + 1, g, scr, &s_flag)) return false;
             stamp(te, 6);
@@ -375,7 +383,8 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
                 g.maxabs = G;
                 fixed = (int)c;
             }
-        nx = vamp_advance(P, cur, g, fixed, te, scr, &s2l);
+        stamp(te, 9);   // (slot 9: vamp_advance starts)
+        nx = vamp_advance(P, cur, g, fixed, te, scr, &s2x);
         stamp(te, 7);
         return true;
     };

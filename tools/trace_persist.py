@@ -115,6 +115,10 @@ def main():
         v = d[:, 1:, i] if Tn > 1 else d[:, :, i]
         print(f'  {name:22s} median {np.median(v):9.0f}  p10 {np.percentile(v, 10):9.0f}  p90 {np.percentile(v, 90):9.0f}'
               f'  ({100 * np.median(v) / per_it:5.1f} %)' if per_it else '')
+    raw = a[:nwg * iters * STRIDE].reshape(nwg, iters, STRIDE).astype(np.int64)[:, 1:Tn]
+    if Tn > 1 and np.all(raw[:, :, 9] > 0):   # slot 9: the start of vamp_advance (the scalars' own work)
+        print(f'  scalars: gather end -> advance start median {np.median(raw[:, :, 9] - raw[:, :, 6]):.0f}, '
+              f'vamp_advance median {np.median(raw[:, :, 7] - raw[:, :, 9]):.0f} cycles')
     arrival_spread(a, st, nwg, iters, Tn)
 
 
