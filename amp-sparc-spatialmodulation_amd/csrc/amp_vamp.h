@@ -234,26 +234,6 @@ __device__ inline VampIter vamp_advance(const VampK& P, const VampIter& cur, con
     return nx;
 }
 
-// Every lane of a wave holds the same iteration record (the scalars are formed redundantly in
-// each lane); readfirstlane makes that explicit, so the record lives in scalar registers (or VGPR
-// lanes) instead of one VGPR per field that the eight-wave engine spills to scratch across the loop
-// and reloads at the top of the next iteration, on the r~ build's critical path.
-__device__ __forceinline__ VampIter vamp_iter_uniform(const VampIter& a) {
-    VampIter u = a;
-    auto rf = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
-    u.stopped = __builtin_amdgcn_readfirstlane(a.stopped);
-    u.T = __builtin_amdgcn_readfirstlane(a.T);
-    u.fixed = __builtin_amdgcn_readfirstlane(a.fixed);
-    u.fixed_all = __builtin_amdgcn_readfirstlane(a.fixed_all);
-    u.vr = rf(a.vr); u.alpha = rf(a.alpha); u.inv1ma = rf(a.inv1ma); u.sigma2 = rf(a.sigma2);
-    u.inv_sigma2 = rf(a.inv_sigma2); u.dxdr_prev = rf(a.dxdr_prev); u.ns_prev = rf(a.ns_prev); u.s2t = rf(a.s2t);
-    const long long g = __double_as_longlong(a.G);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)g);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(g >> 32));
-    u.G = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-    return u;
-}
-
 __device__ inline amp_status vamp_make_status(const VampK& P, const VampIter& cur, const VampIter& nx, int fixed) {
     amp_status s;
     s.T = nx.stopped ? nx.T : P.max_iter;

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
     VampIter cur;
     {
         const S2Lane s2l = s2_lane(P, sv_ep);     // s^2 for the first LMMSE sum (re-read per exchange below)
-        cur = vamp_iter_uniform(vamp_first_iter(P, scr, &s2l));   // vamp.py:26, 66-82 at t = 0
+        cur = vamp_first_iter(P, scr, &s2l);      // vamp.py:26, 66-82 at t = 0
     }
     // Tracker (vamp.py:22-26): xmmse = p, r = 0 (so r~ = p at t = 0), var(prev) = 1
     {
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
                 fixed = (int)c;
             }
         stamp(te, 9);   // (slot 9: vamp_advance starts)
-        nx = vamp_iter_uniform(vamp_advance(P, cur, g, fixed, te, scr, &s2x));
+        nx = vamp_advance(P, cur, g, fixed, te, scr, &s2x);
         stamp(te, 7);
         return true;
     };
