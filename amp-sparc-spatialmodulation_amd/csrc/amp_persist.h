@@ -736,11 +736,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(void* base, unsigned
     return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
 }
 
-// NW: the workgroup's waves as a compile-time constant (0: blockDim.x / 64 at run time).  With it
-// the fold over the waves' records unrolls, so thread 0 issues all their LDS reads before the
-// first add (with a run-time bound every record waited out its own LDS latency, on the path every
-// other workgroup's gather waits for); the adds keep their order.
-template <int NW = 0>
 __device__ __forceinline__ void part_publish(PartAcc p, __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned tag,
                                              void* lds_scratch) {
     part_wave_reduce(p);
@@ -752,35 +747,12 @@ __device__ __forceinline__ void part_publish(PartAcc p, __amdgpu_buffer_rsrc_t r
         s[wave].minsecmax = p.minsecmax; s[wave].notclose = p.notclose;
     }
     __syncthreads();
-    double sv = 0.0, mx = 0.0, mn = 0.0;
-    uint32_t nc = 0;
-    if constexpr (NW > 0) {
-        // wave 0: lane w reads wave w's record (one LDS round trip for all of them), then every lane
-        // folds them in wave order through v_readlane
-        if (threadIdx.x < 64) {
-            const Partial q = s[min((int)threadIdx.x, NW - 1)];
-            auto rl = [](double x, int l) {
-                const long long b = __double_as_longlong(x);
-                const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
-                const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-            };
-            sv = rl(q.sumvar, 0); mx = rl(q.maxabs, 0); mn = rl(q.minsecmax, 0);
-            nc = (uint32_t)__builtin_amdgcn_readlane((int)q.notclose, 0);
-#pragma unroll
-            for (int w = 1; w < NW; ++w) {
-                sv += rl(q.sumvar, w); mx = nan_max(mx, rl(q.maxabs, w)); mn = nan_min(mn, rl(q.minsecmax, w));
-                nc += (uint32_t)__builtin_amdgcn_readlane((int)q.notclose, w);
-            }
-        }
-    } else if (threadIdx.x == 0) {
-        sv = s[0].sumvar; mx = s[0].maxabs; mn = s[0].minsecmax;
-        nc = s[0].notclose;
+    if (threadIdx.x == 0) {
+        double sv = s[0].sumvar, mx = s[0].maxabs, mn = s[0].minsecmax;
+        uint32_t nc = s[0].notclose;
         for (int w = 1; w < (int)(blockDim.x / 64); ++w) {
             sv += s[w].sumvar; mx = nan_max(mx, s[w].maxabs); mn = nan_min(mn, s[w].minsecmax); nc += s[w].notclose;
         }
-    }
-    if (threadIdx.x == 0) {
         const unsigned long long b = (unsigned long long)__double_as_longlong(sv);
         const u32x4 g0 = {(unsigned)b, (unsigned)(b >> 32), nc, tag};
         const u32x4 g1 = {__float_as_uint((float)mx), __float_as_uint((float)mn), 0u, tag};

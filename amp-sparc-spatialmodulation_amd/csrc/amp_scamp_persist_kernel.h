@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * NWV, NWV / 4) void scamp_persist(ScampK P_arg,
         }
         pa.notclose += nc;
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;
-        part_publish<PWG / 64>(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
+        part_publish(pa, grs, ((unsigned)t * nwg + wg) * 32u, tag, scr);
         stamp(t, 6);
         // 5. batch-global max|xi| / danger test / allclose count
         PartAcc g;

@@ -690,7 +690,7 @@ __global__ __launch_bounds__(64 * NWV, OCC * NWV / 4) void vamp_persist(VampK P_
             denoise_sections_u<true, KK, DU, PKDEN>(pol, nrows * spr, M, P.c, pa);   // two waves per SIMD: scalar f32 (amp_denoise.h)
         stamp(t, 8);
         const unsigned tag = P.gen * (unsigned)(P.max_iter + 1) + (unsigned)t + 1u;   // never 0 mod 2^32 in practice
-        part_publish<PWG / 64>(pa, grs, ((unsigned)t * nwx + wgx) * 32u, tag, scr);
+        part_publish(pa, grs, ((unsigned)t * nwx + wgx) * 32u, tag, scr);
         if (P.dump) {   // xmmse and var after the denoiser (part_publish's barrier ordered the LDS writes)
             float* dp = P.dump + (((size_t)t * nwg + wg) * 5 + 2) * PBM * twoN;
             for (int e = tid; e < PBM * twoN; e += PWG) dp[e] = sX[(e / twoN) * ldr + e % twoN];
