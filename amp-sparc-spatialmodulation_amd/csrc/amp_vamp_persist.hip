@@ -85,10 +85,23 @@ bool persist_wg2() {
     }();
     return v;
 }
+// Side-by-side epochs at two workgroups per CU only in the diagnostic build, with
+// AMP_EPOCHS_TWO_PER_CU=1 (tools/occ2_repro.py, tests/test_gpu_epochs.py's 8-epoch cases).  The launches
+// keep the two-per-CU build (same bits as one epoch), but by default an epoch group holds at most
+// one workgroup per CU: gpurun r6c49 saw one 8-epoch cfg2 launch (two per CU) differ from its
+// sequential forwards in one epoch's bit errors, on the tree whose full suite had passed (DESIGN.md
+// §3.8, the unexplained two-per-CU corruption).
+static bool persist_pair_epochs() {
+    static const bool v = [] {
+        const char* e = diag_env("AMP_EPOCHS_TWO_PER_CU");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 // gemm_mode: the persistent GEMM arithmetic of the call (vamp_gemm_select: 0 f32, 1 bf16x3,
 // 2 fp16x2); only the split-precision engines have a two-per-CU instantiation
 static int persist_wg_cap(int N, int gemm_mode) {
-    return (N == 64 && (gemm_mode == 1 || gemm_mode == 2) && persist_wg2()) ? 2 : 1;
+    return (N == 64 && (gemm_mode == 1 || gemm_mode == 2) && persist_wg2() && persist_pair_epochs()) ? 2 : 1;
 }
 
 int vamp_persist_wg_per_cu(const amp_dims* d, int k, int gemm) {

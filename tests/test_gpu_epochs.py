@@ -39,6 +39,13 @@ def _epochs(cfg, E, ebn0, seed, scales=None):
     return (U, s, Vh), SNR, eps
 
 
+def _two_per_cu(det, N):
+    """Whether epoch groups may hold two workgroups per CU (diagnostic build with
+    AMP_EPOCHS_TWO_PER_CU=1; the shipped library caps a group at one per CU since round 6)."""
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    return det.max_epochs(N) == 2 * ncu // ((det.config.B + 15) // 16)
+
+
 def _run_both(cfg, chan, SNR, eps, device):
     from vamp import VAMP
     mv = lambda t: t.to(device).contiguous()  # noqa: E731
@@ -58,11 +65,17 @@ def _run_both(cfg, chan, SNR, eps, device):
                                              ('QPSK', 6.0, 8), ('16QAM', 8.0, 8), ('QPSK', 2.0, 8),
                                              ('16QAM', 20.0, 8)])
 def test_epochs_equal_sequential_cfg2(device, alphabet, ebn0, E):
+    from vamp import VAMP
     cfg = _cfg(64, 4, 128, 1024, alphabet)
+    # one workgroup of 16 trials per CU at N = 64: 4 epochs of 64 workgroups on 256 CUs (8 at two
+    # per CU, diagnostic build only)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    m = VAMP(cfg).max_epochs(64)
+    assert m in (ncu // 64, 2 * ncu // 64)
+    if E > m:
+        pytest.skip(f'{E} epochs need two workgroups per CU (diagnostic build, AMP_EPOCHS_TWO_PER_CU=1)')
     chan, SNR, eps = _epochs(cfg, E, ebn0, seed=3)
     det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
-    # two workgroups of 16 trials per CU at N = 64: 8 epochs of 64 workgroups on 256 CUs
-    assert det.max_epochs(64) == 2 * torch.cuda.get_device_properties(0).multi_processor_count // 64
     r, xm, var = det.last_epochs
     assert len(grp) == E
     for e, (ls, st, r0, x0, v0) in enumerate(seq):
@@ -131,8 +144,8 @@ def _epochs_per_channel(cfg, E, ebn0, seed):
     return SNR, out
 
 
-@pytest.mark.parametrize('Nt,Na,Nr,B,alphabet,ebn0,E', [(64, 4, 128, 1024, '16QAM', 8.0, 8),
-                                                        (64, 4, 128, 1024, 'QPSK', 4.0, 8),
+@pytest.mark.parametrize('Nt,Na,Nr,B,alphabet,ebn0,E', [(64, 4, 128, 1024, '16QAM', 8.0, 4),
+                                                        (64, 4, 128, 1024, 'QPSK', 4.0, 4),
                                                         (256, 8, 512, 1024, '16QAM', 10.0, 4),
                                                         (256, 8, 512, 1024, 'QPSK', 2.0, 4)])
 def test_epochs_per_channel_equal_sequential(device, Nt, Na, Nr, B, alphabet, ebn0, E):
@@ -260,11 +273,15 @@ def test_simulate_group_epochs_identical(device, tmp_path):
 
 @pytest.mark.parametrize('alphabet,ebn0', [('QPSK', 6.0), ('16QAM', 8.0)])
 def test_epochs8_two_per_cu_reproducible(device, alphabet, ebn0):
-    """8 cfg2 epochs in one launch (two workgroups per CU) three times over: every r / xmmse / var
+    """8 cfg2 epochs in one launch (two workgroups per CU; diagnostic build only since round 6, when
+    gpurun r6c49 saw such a launch differ once) three times over: every r / xmmse / var
     word equal to the sequential forwards in every repetition.  Round 2 saw these co-resident epochs
     change run to run; the cause was the packed-math variance sum of the denoiser (one half of a
     v_pk_fma_f32 result lost in lanes 48-63 with two waves per SIMD)."""
+    from vamp import VAMP
     cfg = _cfg(64, 4, 128, 1024, alphabet)
+    if not _two_per_cu(VAMP(cfg), 64):
+        pytest.skip('two workgroups per CU: diagnostic build only (AMP_EPOCHS_TWO_PER_CU=1)')
     chan, SNR, eps = _epochs(cfg, 8, ebn0, seed=3)
     det, seq, grp = _run_both(cfg, chan, SNR, eps, device)
     mv = lambda t: t.to(device).contiguous()  # noqa: E731

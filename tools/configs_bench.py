@@ -39,9 +39,10 @@ CFGS = {
     'cfg4': ('vamp', 256, 8, 512, 4096, '16QAM', 20, 8.0),
     # cfg2 with the 4 epochs of one res = 4 block side by side (VAMP.forward_epochs: 256 workgroups)
     'cfg2-epochs4': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
-    # 8 epochs: two workgroups per CU (AMP_PERSIST_WG2, the N = 64 default since round 3)
+    # 8 epochs: two workgroups per CU, diagnostic build only since round 6 (AMP_EPOCHS_TWO_PER_CU=1)
     'cfg2-epochs8': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
-    # cfg2 at the reference's default res = 1: 8 epochs with a channel each side by side
+    # cfg2 at the reference's default res = 1: max_epochs (4; 8 at two per CU) epochs with a channel
+    # each side by side
     # (amp_vamp_detect_count_epochs_ch); the inputs include each epoch's own SVD factors
     'cfg2-res1': ('vamp', 64, 4, 128, 1024, '16QAM', 20, 8.0),
 }
@@ -68,6 +69,13 @@ def main(steps=50, warmup=30, only=None):
         sym, idx = lab(sym), lab(idx)
         E = EPOCHS.get(name, 1)
         if E > 1:
+            cap = VAMP(cfg).max_epochs(Nt)
+            if E > cap:   # two workgroups per CU: diagnostic build only (AMP_EPOCHS_TWO_PER_CU=1)
+                if name == 'cfg2-epochs8':
+                    print(json.dumps({'config': name, 'skipped': f'{E} epochs need two workgroups per CU '
+                                      f'(max_epochs {cap})'}), flush=True)
+                    continue
+                E = cap
             res1 = name.endswith('res1')
             eps = [(x, sym, idx, y)]
             chans = [torch.linalg.svd(A, full_matrices=False)]
