@@ -197,7 +197,7 @@ def build(verbose: bool = False) -> str:
 # Environment switches that only the diagnostic build reads (amp_host.h diag_env)
 DIAG_SWITCHES = ('AMP_BAMP_KC', 'AMP_BAND_GEMM', 'AMP_BAMP_GEMM', 'AMP_BAMP_X3_ROWS', 'AMP_SCAMP_KC', 'AMP_SCAMP_GEMM',
                  'AMP_SCAMP_LAUNCH_GEMM', 'AMP_SCAMP_X3_WAVES', 'AMP_VAMP_GEMM', 'AMP_YTIL_IN_KERNEL', 'AMP_YTIL_X3',
-                 'AMP_PERSIST_WG2', 'AMP_VAMP_X3_WAVES', 'AMP_FIX_GRID', 'AMP_GRID_DENOISER', 'AMP_SECTION_BN',
+                 'AMP_PERSIST_WG2', 'AMP_EPOCHS_TWO_PER_CU', 'AMP_VAMP_X3_WAVES', 'AMP_FIX_GRID', 'AMP_GRID_DENOISER', 'AMP_SECTION_BN',
                  'AMP_FOLD_LAUNCH', 'AMP_HOST_RECORD', 'AMP_SHARD_ANY_STREAM')
 
 

@@ -201,7 +201,7 @@ int amp_vamp_detect_count(const amp_dims* d, const amp_constellation* c, const a
  * idx hold the epochs' rows back to back ([epochs * B] rows); status -> amp_status[epochs],
  * dec->counts -> amp_counts[epochs]; workspace: amp_vamp_epochs_workspace_bytes.  Needs the
  * persistent engine with B % 16 == 0 and epochs <= amp_vamp_max_epochs (one workgroup of 16
- * trials per CU; two per CU at N = 64 on the bf16x3 engine, AMP_PERSIST_WG2=0 keeps one). */
+ * trials per CU; two per CU at N = 64 only in the diagnostic build with AMP_EPOCHS_TWO_PER_CU=1). */
 /* ---- Trial sharding across ranks (SURVEY §8(e) exact-compat mode) ----
  * One batch of B_global trials split over ranks (rank r holds a contiguous slice of d->B rows);
  * every per-iteration batch-global value of VAMP.forward (var.mean() vamp.py:85, the float64
@@ -266,8 +266,9 @@ int amp_vamp_debug_offsets(const amp_dims* d, int32_t k, int32_t max_iter, int32
 int amp_vamp_debug_dump(void* buf);
 /* The most epochs of d->B trials one launch holds on this device (0: not persistent-eligible). */
 int amp_vamp_max_epochs(const amp_dims* d, int32_t k);
-/* The same for a given persistent GEMM arithmetic (amp_vamp_args.gemm): two workgroups per CU
- * only where that arithmetic has the two-per-CU build (the split-precision forms at N = 64). */
+/* The same for a given persistent GEMM arithmetic (amp_vamp_args.gemm).  One workgroup per CU;
+ * the diagnostic build with AMP_EPOCHS_TWO_PER_CU=1 allows two where that arithmetic has the
+ * two-per-CU build (the split-precision forms at N = 64). */
 int amp_vamp_max_epochs_gemm(const amp_dims* d, int32_t k, int32_t gemm);
 /* 1 when amp_vamp_detect_count_epochs_ch takes ONE CHANNEL PER EPOCH for this config and GEMM
  * arithmetic (the bf16x3 / int8x4 engine and n == 2 k), else 0 (then a chunk of epochs must share
